@@ -1,0 +1,83 @@
+// gp_internal.hpp -- device-memory layout and kernel launch wrappers shared by
+// the translation units of libgossip_hip.so.  Not part of the C-ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gp_device.hpp"
+
+namespace gp {
+
+constexpr int HIST = 4096;            // per-round alert ring (host syncs at least every HIST rounds)
+constexpr uint32_t INJ_CHUNK = 65536; // injector live-list chunk (ids); 2048 bitmap words
+constexpr int BULK_THREADS = 256;
+constexpr int FIN_THREADS = 1024;
+
+// Device-resident control block.  Written by the single-block finalize kernel
+// between bulk rounds; bulk kernels only read it (plus atomics on the
+// round_* accumulators, which nobody reads inside the same kernel).
+struct Ctl {
+    unsigned long long alerts_total;  // cumulative alerts through the last finalized round
+    unsigned long long round_alerts;  // accumulated by the bulk kernel of the current round
+    unsigned long long active_total;  // push-sum: nodes ever activated (monotone)
+    unsigned long long round_active;  // accumulated newly-active count of the current round
+    unsigned long long live;          // injector |L| (Program.fs:142-158)
+    long long inj_target;             // node the injector delivers to this round, -1 none
+    unsigned int done;                // cumulative alerts reached T (Program.fs:53)
+    unsigned int all_active;          // every node active at round start (push-sum)
+    unsigned long long hist[HIST];    // alerts of round r at hist[r % HIST]
+};
+
+// Node state in HBM (structure of arrays, single GPU / one slab).
+struct DevState {
+    Geom G;
+    int topo, alg;
+    uint32_t k0, k1;    // Philox key = seed
+    uint32_t seed_node;
+    Ctl* ctl;
+    // push-sum: (s, w) interleaved, double buffered; node byte double buffered
+    double2* sw[2];
+    uint8_t* nb[2];
+    // gossip: rumour counters (in place), direction byte double buffered (nb)
+    int32_t* c;
+    // Imp3D: random edge and receiver-sorted in-lists (CSR)
+    uint32_t* rnd;
+    uint32_t* in_off;  // P+1
+    uint32_t* in_src;  // P
+    // gossip injector
+    uint32_t* live_bits;   // ceil(T / INJ_CHUNK) * 2048 words, bit = id still listed
+    uint32_t* chunk_live;  // live ids per chunk
+    uint32_t nchunks;
+    // full topology scratch
+    int32_t* inc;          // gossip deliveries per node
+    uint32_t* key[2];      // push-sum: target per sender / sorted
+    uint32_t* val[2];      // push-sum: sender ids / sorted
+    uint32_t* head;        // push-sum: first sorted position per receiver
+    void* sort_tmp;
+    size_t sort_tmp_bytes;
+    uint32_t key_bits;
+};
+
+// ---- kernels (gp_kernels.hip)
+hipError_t launch_init(const DevState& S, int grid, hipStream_t st);
+hipError_t launch_topo_rnd(const DevState& S, int grid, hipStream_t st);
+hipError_t launch_injector_init(const DevState& S, int grid, hipStream_t st);
+hipError_t launch_bulk(const DevState& S, uint32_t round, int grid, hipStream_t st);
+hipError_t launch_finalize(const DevState& S, uint32_t round_done, uint32_t round_next, hipStream_t st);
+hipError_t launch_full_pushsum_send(const DevState& S, uint32_t round, int grid, hipStream_t st);
+hipError_t launch_full_pushsum_mark(const DevState& S, int grid, hipStream_t st);
+hipError_t launch_full_pushsum_recv(const DevState& S, uint32_t round, int grid, hipStream_t st);
+hipError_t launch_iota(uint32_t* v, uint32_t n, int grid, hipStream_t st);
+hipError_t launch_histogram(const uint32_t* keys, uint32_t n, uint32_t* counts, int grid, hipStream_t st);
+const char* bulk_kernel_name(const DevState& S);
+
+// ---- sorting (gp_sort.hip, rocPRIM)
+// Stable sort of (key, value) pairs on the low `bits` bits of the key.
+hipError_t sort_pairs(void* tmp, size_t& tmp_bytes, const uint32_t* kin, uint32_t* kout,
+                      const uint32_t* vin, uint32_t* vout, uint32_t n, uint32_t bits, hipStream_t st);
+// out[0] = 0, out[i] = sum(in[0..i-1]) for i <= n-1 (n entries).
+hipError_t exclusive_scan_u32(void* tmp, size_t& tmp_bytes, const uint32_t* in, uint32_t* out, uint32_t n,
+                              hipStream_t st);
+
+}  // namespace gp

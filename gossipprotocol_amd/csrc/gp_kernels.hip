@@ -1,0 +1,611 @@
+// gp_kernels.hip -- CDNA4 (gfx950) kernels of the synchronous gossip /
+// push-sum round (SRS v1).
+//
+// Design:
+//   * one bulk kernel per round for line / 3D / Imp3D: every node PULLS its
+//     in-messages -- lattice neighbours through the 1-byte direction each
+//     sender chose one round earlier, Imp3D random edges through the
+//     receiver-sorted in-list -- and folds them in the canonical order, then
+//     draws its own direction for the next round.  No message is staged in HBM;
+//   * state is double-buffered (round r reads buffer r&1, writes r&1^1), so the
+//     bulk kernel needs no inter-workgroup synchronisation;
+//   * a single-workgroup finalize kernel closes the round: alert bookkeeping
+//     (scheduler, Program.fs:41-61), done flag, and the gossip injector
+//     (Actor2, Program.fs:141-163) for the next round.
+// Built with -ffp-contract=off: the push-sum fold must round exactly like the
+// CPU oracle.
+#include "gp_internal.hpp"
+
+namespace gp {
+
+// ---------------------------------------------------------------- helpers
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Sum over a 256-thread block; result valid in thread 0.
+__device__ __forceinline__ void block_sum2(uint32_t& a, uint32_t& b, uint32_t (*lds)[BULK_THREADS / 64]) {
+    a = wave_sum(a);
+    b = wave_sum(b);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) {
+        lds[0][wid] = a;
+        lds[1][wid] = b;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        a = 0;
+        b = 0;
+#pragma unroll
+        for (int i = 0; i < BULK_THREADS / 64; ++i) {
+            a += lds[0][i];
+            b += lds[1][i];
+        }
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ T ld_agent(const T* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ void st_agent(T* p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int TOPO>
+__device__ __forceinline__ uint32_t degree_of(uint32_t mask) {
+    return popc6(mask) + (TOPO == IMP3D ? 1u : 0u);
+}
+
+// Direction node j sends in during `round` (slot U(deg) of its neighbour array,
+// Program.fs:86 / 103 / 128).
+template <int TOPO>
+__device__ __forceinline__ uint32_t draw_dir(const DevState& S, uint32_t stream, uint32_t j, uint32_t mask,
+                                             uint32_t round) {
+    const uint32_t deg = degree_of<TOPO>(mask);
+    if (deg == 0) return DIR_NONE;
+    return slot_to_dir(mask, uniform(S.k0, S.k1, stream, j, round, deg));
+}
+
+// ---------------------------------------------------------------- init
+// InitialSum x / weight 1.0 / count 1 / rumours 0 (Program.fs:67-71,78,174);
+// only the seed (Program.fs:193) is active in round 0.
+template <int TOPO, int ALG>
+__global__ __launch_bounds__(BULK_THREADS) void k_init(DevState S) {
+    const uint32_t P = S.G.P;
+    for (uint32_t j = blockIdx.x * BULK_THREADS + threadIdx.x; j < P; j += gridDim.x * BULK_THREADS) {
+        const bool seed = j == S.seed_node;
+        uint32_t dir = DIR_NONE;
+        if (TOPO != FULL && seed) {
+            const uint32_t mask = present_mask<TOPO>(j, S.G);
+            dir = draw_dir<TOPO>(S, ALG == GOSSIP ? S_GOSSIP : S_PUSHSUM, j, mask, 0);
+        }
+        if (ALG == PUSHSUM) {
+            S.sw[0][j] = make_double2((double)j, 1.0);
+            S.nb[0][j] = (uint8_t)((1u << CNT_SHIFT) | (seed ? B_ACTIVE : 0u) | dir);
+        } else {
+            S.c[j] = 0;
+            if (TOPO != FULL) S.nb[0][j] = (uint8_t)dir;
+            else S.inc[j] = 0;
+        }
+    }
+}
+
+// Imp3D random neighbour Random().Next(0, nodes-1) in [0, P-2] (Program.fs:259).
+__global__ __launch_bounds__(BULK_THREADS) void k_topo_rnd(DevState S) {
+    const uint32_t P = S.G.P;
+    for (uint32_t i = blockIdx.x * BULK_THREADS + threadIdx.x; i < P; i += gridDim.x * BULK_THREADS)
+        S.rnd[i] = uniform(S.k0, S.k1, S_TOPO, i, 0, P - 1);
+}
+
+__global__ __launch_bounds__(BULK_THREADS) void k_iota(uint32_t* v, uint32_t n) {
+    for (uint32_t i = blockIdx.x * BULK_THREADS + threadIdx.x; i < n; i += gridDim.x * BULK_THREADS) v[i] = i;
+}
+
+__global__ __launch_bounds__(BULK_THREADS) void k_histogram(const uint32_t* keys, uint32_t n, uint32_t* counts) {
+    for (uint32_t i = blockIdx.x * BULK_THREADS + threadIdx.x; i < n; i += gridDim.x * BULK_THREADS)
+        atomicAdd(&counts[keys[i]], 1u);
+}
+
+// Injector list = ids 0..T-1 (Program.fs:147-148) as a bitmap + per-chunk counts.
+__global__ __launch_bounds__(BULK_THREADS) void k_injector_init(DevState S) {
+    const uint32_t T = S.G.T;
+    const uint32_t nwords = S.nchunks * (INJ_CHUNK / 32);
+    for (uint32_t w = blockIdx.x * BULK_THREADS + threadIdx.x; w < nwords; w += gridDim.x * BULK_THREADS) {
+        const uint64_t lo = (uint64_t)w * 32;
+        uint32_t bits = 0;
+        if (lo + 32 <= T) bits = 0xFFFFFFFFu;
+        else if (lo < T) bits = (1u << (uint32_t)(T - lo)) - 1u;
+        S.live_bits[w] = bits;
+    }
+    for (uint32_t c = blockIdx.x * BULK_THREADS + threadIdx.x; c < S.nchunks; c += gridDim.x * BULK_THREADS) {
+        const uint64_t lo = (uint64_t)c * INJ_CHUNK;
+        const uint64_t hi = lo + INJ_CHUNK < T ? lo + INJ_CHUNK : T;
+        S.chunk_live[c] = (uint32_t)(hi - lo);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) S.ctl->live = T;
+}
+
+// ---------------------------------------------------------------- push-sum round
+// MainPushSum (Program.fs:101-131) as one synchronous round, pull form:
+//   own half (Program.fs:104-105,125-126) -> lattice in-messages in the
+//   receiver's slot order -> Imp3D random-edge messages by ascending sender ->
+//   ratio test against the round-start ratio (Program.fs:114-123, SRS D5) ->
+//   direction for round r+1.
+template <int TOPO>
+__global__ __launch_bounds__(BULK_THREADS) void k_pushsum_round(DevState S, uint32_t r) {
+    __shared__ uint32_t red[2][BULK_THREADS / 64];
+    Ctl* ctl = S.ctl;
+    if (ld_agent(&ctl->done)) return;
+    const bool all_active = ld_agent(&ctl->all_active) != 0;
+    const int cur = r & 1;
+    const double2* __restrict__ swc = S.sw[cur];
+    double2* __restrict__ swn = S.sw[cur ^ 1];
+    const uint8_t* __restrict__ nbc = S.nb[cur];
+    uint8_t* __restrict__ nbn = S.nb[cur ^ 1];
+    const uint32_t* __restrict__ in_off = S.in_off;
+    const uint32_t* __restrict__ in_src = S.in_src;
+    const uint32_t P = S.G.P;
+    uint32_t alerts = 0, newly = 0;
+    for (uint32_t j = blockIdx.x * BULK_THREADS + threadIdx.x; j < P; j += gridDim.x * BULK_THREADS) {
+        const uint8_t b = nbc[j];
+        const double2 sv = swc[j];
+        const uint32_t mask = present_mask<TOPO>(j, S.G);
+        const uint32_t deg = degree_of<TOPO>(mask);
+        bool active = (b & B_ACTIVE) != 0;
+        const bool halve = active && deg > 0;
+        double acc_s = halve ? sv.x * 0.5 : sv.x;
+        double acc_w = halve ? sv.y * 0.5 : sv.y;
+        bool recv = false;
+        constexpr uint32_t ND = TOPO == LINE ? 2 : 6;
+#pragma unroll
+        for (uint32_t d = 0; d < ND; ++d) {
+            if (mask & (1u << d)) {
+                const uint32_t n = nbr<TOPO>(j, d, S.G);
+                if ((uint32_t)(nbc[n] & DIR_MASK) == (d ^ 1u)) {
+                    const double2 m = swc[n];
+                    acc_s = acc_s + m.x * 0.5;
+                    acc_w = acc_w + m.y * 0.5;
+                    recv = true;
+                }
+            }
+        }
+        if (TOPO == IMP3D) {
+            const uint32_t e1 = in_off[j + 1];
+            for (uint32_t e = in_off[j]; e < e1; ++e) {
+                const uint32_t i = in_src[e];
+                bool sent;
+                if (all_active) {
+                    // every sender is active: recompute its draw instead of a
+                    // random 1-byte gather
+                    const uint32_t di = degree_of<IMP3D>(present_mask<IMP3D>(i, S.G));
+                    sent = uniform(S.k0, S.k1, S_PUSHSUM, i, r, di) == di - 1;
+                } else {
+                    sent = (nbc[i] & DIR_MASK) == DIR_RANDOM;
+                }
+                if (sent) {
+                    const double2 m = swc[i];
+                    acc_s = acc_s + m.x * 0.5;
+                    acc_w = acc_w + m.y * 0.5;
+                    recv = true;
+                }
+            }
+        }
+        uint32_t flags = b & (B_ACTIVE | B_CONV | (3u << CNT_SHIFT));
+        if (recv) {
+            if (!(b & B_CONV)) {
+                const double r_old = sv.x / sv.y;
+                const double r_new = acc_s / acc_w;
+                uint32_t cnt = (b >> CNT_SHIFT) & 3u;
+                cnt = fabs(r_new - r_old) > 1e-10 ? 0u : cnt + 1u;
+                flags = (flags & ~(3u << CNT_SHIFT)) | (cnt << CNT_SHIFT);
+                if (cnt == 3) {
+                    flags |= B_CONV;
+                    ++alerts;
+                }
+            }
+            if (!active) {
+                ++newly;
+                flags |= B_ACTIVE;
+                active = true;
+            }
+        }
+        const uint32_t dir = active ? draw_dir<TOPO>(S, S_PUSHSUM, j, mask, r + 1) : DIR_NONE;
+        nbn[j] = (uint8_t)(flags | dir);
+        swn[j] = make_double2(acc_s, acc_w);
+    }
+    block_sum2(alerts, newly, red);
+    if (threadIdx.x == 0) {
+        if (alerts) atomicAdd(&ctl->round_alerts, (unsigned long long)alerts);
+        if (newly) atomicAdd(&ctl->round_active, (unsigned long long)newly);
+    }
+}
+
+// ---------------------------------------------------------------- gossip round
+// Process1/Process2 (Program.fs:84-98) as one synchronous round, pull form:
+// deliveries = lattice senders whose direction points here + Imp3D random-edge
+// senders + the injector; dropped if this node was converged at round start
+// (the sender-side `dictionary` check, Program.fs:87, applied at the receiver).
+template <int TOPO>
+__global__ __launch_bounds__(BULK_THREADS) void k_gossip_round(DevState S, uint32_t r) {
+    __shared__ uint32_t red[2][BULK_THREADS / 64];
+    Ctl* ctl = S.ctl;
+    if (ld_agent(&ctl->done)) return;
+    const long long inj = ld_agent(&ctl->inj_target);
+    const int cur = r & 1;
+    const uint8_t* __restrict__ nbc = S.nb[cur];
+    uint8_t* __restrict__ nbn = S.nb[cur ^ 1];
+    int32_t* __restrict__ cc = S.c;
+    const uint32_t P = S.G.P;
+    uint32_t alerts = 0, unused = 0;
+    for (uint32_t j = blockIdx.x * BULK_THREADS + threadIdx.x; j < P; j += gridDim.x * BULK_THREADS) {
+        const int32_t c0 = cc[j];
+        const uint32_t mask = present_mask<TOPO>(j, S.G);
+        int32_t c1 = c0;
+        if (c0 < (int32_t)GOSSIP_DONE) {
+            uint32_t inc = (long long)j == inj ? 1u : 0u;
+            constexpr uint32_t ND = TOPO == LINE ? 2 : 6;
+#pragma unroll
+            for (uint32_t d = 0; d < ND; ++d)
+                if (mask & (1u << d)) inc += (uint32_t)(nbc[nbr<TOPO>(j, d, S.G)] & DIR_MASK) == (d ^ 1u);
+            if (TOPO == IMP3D) {
+                const uint32_t e1 = S.in_off[j + 1];
+                for (uint32_t e = S.in_off[j]; e < e1; ++e)
+                    inc += (uint32_t)(nbc[S.in_src[e]] & DIR_MASK) == DIR_RANDOM;
+            }
+            if (inc) {
+                c1 = c0 + (int32_t)inc;
+                cc[j] = c1;
+                alerts += c1 > 10;  // the receipt that finds rumours == 10 (Program.fs:92-94)
+            }
+        }
+        const bool active = ((j == S.seed_node) || c1 >= 1) && c1 <= 10;
+        nbn[j] = (uint8_t)(active ? draw_dir<TOPO>(S, S_GOSSIP, j, mask, r + 1) : DIR_NONE);
+    }
+    block_sum2(alerts, unused, red);
+    if (threadIdx.x == 0 && alerts) atomicAdd(&ctl->round_alerts, (unsigned long long)alerts);
+}
+
+// ---------------------------------------------------------------- full topology
+// Gossip: every active node sends to a uniform j != i (Program.fs:211-216,86-88).
+__global__ __launch_bounds__(BULK_THREADS) void k_full_gossip_send(DevState S, uint32_t r) {
+    if (ld_agent(&S.ctl->done)) return;
+    const uint32_t P = S.G.P;
+    for (uint32_t i = blockIdx.x * BULK_THREADS + threadIdx.x; i < P; i += gridDim.x * BULK_THREADS) {
+        const int32_t ci = S.c[i];
+        if (((i == S.seed_node) || ci >= 1) && ci <= 10) {
+            const uint32_t t = full_target(i, uniform(S.k0, S.k1, S_GOSSIP, i, r, P - 1));
+            atomicAdd(&S.inc[t], 1);  // integer: order-independent, bit-exact
+        }
+    }
+}
+
+__global__ __launch_bounds__(BULK_THREADS) void k_full_gossip_recv(DevState S, uint32_t r) {
+    __shared__ uint32_t red[2][BULK_THREADS / 64];
+    (void)r;
+    Ctl* ctl = S.ctl;
+    if (ld_agent(&ctl->done)) return;
+    const uint32_t P = S.G.P;
+    uint32_t alerts = 0, unused = 0;
+    for (uint32_t j = blockIdx.x * BULK_THREADS + threadIdx.x; j < P; j += gridDim.x * BULK_THREADS) {
+        const int32_t d = S.inc[j];
+        if (!d) continue;
+        S.inc[j] = 0;
+        const int32_t c0 = S.c[j];
+        if (c0 < (int32_t)GOSSIP_DONE) {
+            S.c[j] = c0 + d;
+            alerts += c0 + d > 10;
+        }
+    }
+    block_sum2(alerts, unused, red);
+    if (threadIdx.x == 0 && alerts) atomicAdd(&ctl->round_alerts, (unsigned long long)alerts);
+}
+
+// Push-sum full: stage (target, sender) pairs; a stable radix sort by target
+// then yields every receiver's senders in ascending order.
+__global__ __launch_bounds__(BULK_THREADS) void k_full_ps_send(DevState S, uint32_t r) {
+    if (ld_agent(&S.ctl->done)) return;
+    const uint32_t P = S.G.P;
+    for (uint32_t i = blockIdx.x * BULK_THREADS + threadIdx.x; i < P; i += gridDim.x * BULK_THREADS) {
+        const bool act = (S.nb[0][i] & B_ACTIVE) != 0;
+        S.key[0][i] = act ? full_target(i, uniform(S.k0, S.k1, S_PUSHSUM, i, r, P - 1)) : P;
+    }
+}
+
+__global__ __launch_bounds__(BULK_THREADS) void k_full_ps_mark(DevState S) {
+    if (ld_agent(&S.ctl->done)) return;
+    const uint32_t P = S.G.P;
+    const uint32_t* __restrict__ ks = S.key[1];
+    for (uint32_t p = blockIdx.x * BULK_THREADS + threadIdx.x; p < P; p += gridDim.x * BULK_THREADS) {
+        const uint32_t k = ks[p];
+        if (k < P && (p == 0 || ks[p - 1] != k)) S.head[k] = p;
+    }
+}
+
+__global__ __launch_bounds__(BULK_THREADS) void k_full_ps_recv(DevState S, uint32_t r) {
+    __shared__ uint32_t red[2][BULK_THREADS / 64];
+    Ctl* ctl = S.ctl;
+    if (ld_agent(&ctl->done)) return;
+    const int cur = r & 1;
+    const double2* __restrict__ swc = S.sw[cur];
+    double2* __restrict__ swn = S.sw[cur ^ 1];
+    const uint32_t* __restrict__ ks = S.key[1];
+    const uint32_t* __restrict__ vs = S.val[1];
+    const uint32_t P = S.G.P;
+    uint32_t alerts = 0, newly = 0;
+    for (uint32_t j = blockIdx.x * BULK_THREADS + threadIdx.x; j < P; j += gridDim.x * BULK_THREADS) {
+        const uint8_t b = S.nb[0][j];
+        const double2 sv = swc[j];
+        const bool active = (b & B_ACTIVE) != 0;
+        double acc_s = active ? sv.x * 0.5 : sv.x;
+        double acc_w = active ? sv.y * 0.5 : sv.y;
+        uint32_t p = S.head[j];
+        bool recv = false;
+        if (p != 0xFFFFFFFFu) {
+            for (; p < P && ks[p] == j; ++p) {
+                const double2 m = swc[vs[p]];
+                acc_s = acc_s + m.x * 0.5;
+                acc_w = acc_w + m.y * 0.5;
+                recv = true;
+            }
+        }
+        uint32_t flags = b;
+        if (recv) {
+            if (!(b & B_CONV)) {
+                const double r_old = sv.x / sv.y;
+                const double r_new = acc_s / acc_w;
+                uint32_t cnt = (b >> CNT_SHIFT) & 3u;
+                cnt = fabs(r_new - r_old) > 1e-10 ? 0u : cnt + 1u;
+                flags = (flags & ~(3u << CNT_SHIFT)) | (cnt << CNT_SHIFT);
+                if (cnt == 3) {
+                    flags |= B_CONV;
+                    ++alerts;
+                }
+            }
+            if (!active) {
+                ++newly;
+                flags |= B_ACTIVE;
+            }
+            S.nb[0][j] = (uint8_t)flags;
+        }
+        swn[j] = make_double2(acc_s, acc_w);
+    }
+    block_sum2(alerts, newly, red);
+    if (threadIdx.x == 0) {
+        if (alerts) atomicAdd(&ctl->round_alerts, (unsigned long long)alerts);
+        if (newly) atomicAdd(&ctl->round_active, (unsigned long long)newly);
+    }
+}
+
+// ---------------------------------------------------------------- finalize
+// Block-wide inclusive scan over FIN_THREADS values (one per thread).
+__device__ uint32_t block_incl_scan(uint32_t v, uint32_t* lds) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    if (lane == 63) lds[wid] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (int i = 0; i < FIN_THREADS / 64; ++i) {
+            const uint32_t t = lds[i];
+            lds[i] = run;
+            run += t;
+        }
+    }
+    __syncthreads();
+    v += lds[wid];
+    __syncthreads();
+    return v;
+}
+
+// Closes round `round_done` (if has_done) and prepares round `round_next`:
+// scheduler bookkeeping (Program.fs:51-56) and, for gossip on line / 3D /
+// Imp3D, one injector step (Program.fs:150-159): k = U(|L|), t = k-th live id;
+// if t converged remove it, else deliver one rumour to t in round_next.
+__global__ __launch_bounds__(FIN_THREADS) void k_finalize(DevState S, uint32_t round_done, uint32_t round_next,
+                                                          int has_done, int injector) {
+    __shared__ uint32_t lds[FIN_THREADS / 64];
+    __shared__ int sh_skip;
+    __shared__ uint32_t sh_chunk, sh_k;
+    __shared__ long long sh_target;
+    Ctl* ctl = S.ctl;
+    if (threadIdx.x == 0) {
+        int skip = (int)ld_agent(&ctl->done);
+        if (!skip && has_done) {
+            const unsigned long long a = atomicExch(&ctl->round_alerts, 0ull);
+            const unsigned long long na = atomicExch(&ctl->round_active, 0ull);
+            const unsigned long long tot = ld_agent(&ctl->alerts_total) + a;
+            st_agent(&ctl->alerts_total, tot);
+            ctl->hist[round_done % HIST] = a;
+            const unsigned long long act = ld_agent(&ctl->active_total) + na;
+            st_agent(&ctl->active_total, act);
+            if (act >= S.G.P) st_agent(&ctl->all_active, 1u);
+            if (tot >= S.G.T) {
+                st_agent(&ctl->done, 1u);
+                skip = 1;
+            }
+        }
+        sh_skip = skip;
+        sh_target = -1;
+        sh_chunk = 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    if (sh_skip || !injector) return;
+
+    const uint32_t live = (uint32_t)ld_agent(&ctl->live);
+    if (live == 0) {
+        if (threadIdx.x == 0) st_agent(&ctl->inj_target, -1ll);
+        return;
+    }
+    const uint32_t k = uniform(S.k0, S.k1, S_INJECT, 0, round_next, live);
+    // phase A: which chunk holds the k-th live id
+    const uint32_t nch = S.nchunks;
+    const uint32_t per = (nch + FIN_THREADS - 1) / FIN_THREADS;
+    const uint32_t c_lo = threadIdx.x * per;
+    const uint32_t c_hi = c_lo + per < nch ? c_lo + per : nch;
+    uint32_t local = 0;
+    for (uint32_t c = c_lo; c < c_hi; ++c) local += S.chunk_live[c];
+    const uint32_t incl = block_incl_scan(local, lds);
+    const uint32_t excl = incl - local;
+    if (k >= excl && k < incl) {
+        uint32_t run = excl;
+        for (uint32_t c = c_lo; c < c_hi; ++c) {
+            const uint32_t n = S.chunk_live[c];
+            if (k < run + n) {
+                sh_chunk = c;
+                sh_k = k - run;
+                break;
+            }
+            run += n;
+        }
+    }
+    __syncthreads();
+    if (sh_chunk >= nch) {  // unreachable when chunk_live sums to live; never index past the bitmap
+        if (threadIdx.x == 0) st_agent(&ctl->inj_target, -1ll);
+        return;
+    }
+    // phase B: which bit of the chunk's 2048 words
+    const uint32_t chunk = sh_chunk, kk = sh_k;
+    constexpr uint32_t WPT = (INJ_CHUNK / 32) / FIN_THREADS;  // words per thread (2)
+    const uint32_t* words = S.live_bits + (size_t)chunk * (INJ_CHUNK / 32);
+    uint32_t wv[WPT];
+    uint32_t wl = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < WPT; ++q) {
+        wv[q] = words[threadIdx.x * WPT + q];
+        wl += (uint32_t)__popc(wv[q]);
+    }
+    const uint32_t wincl = block_incl_scan(wl, lds);
+    const uint32_t wexcl = wincl - wl;
+    if (kk >= wexcl && kk < wincl) {
+        uint32_t rem = kk - wexcl;
+#pragma unroll
+        for (uint32_t q = 0; q < WPT; ++q) {
+            const uint32_t pc = (uint32_t)__popc(wv[q]);
+            if (rem < pc) {
+                uint32_t m = wv[q];
+                for (uint32_t z = 0; z < rem; ++z) m &= m - 1;  // drop `rem` lowest set bits
+                const uint32_t bit = (uint32_t)__ffs(m) - 1;
+                const uint32_t word = threadIdx.x * WPT + q;
+                const uint32_t id = chunk * INJ_CHUNK + word * 32 + bit;
+                if (S.c[id] >= (int32_t)GOSSIP_DONE) {  // converged: remove (Program.fs:158)
+                    S.live_bits[(size_t)chunk * (INJ_CHUNK / 32) + word] = wv[q] & ~(1u << bit);
+                    S.chunk_live[chunk] -= 1;
+                    st_agent(&ctl->live, (unsigned long long)(live - 1));
+                    sh_target = -1;
+                } else {
+                    sh_target = id;  // Process2 to the pick (Program.fs:155)
+                }
+                break;
+            }
+            rem -= pc;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) st_agent(&ctl->inj_target, sh_target);
+}
+
+// ---------------------------------------------------------------- launchers
+hipError_t launch_init(const DevState& S, int grid, hipStream_t st) {
+#define GP_INIT(T, A) hipLaunchKernelGGL((k_init<T, A>), dim3(grid), dim3(BULK_THREADS), 0, st, S)
+    if (S.alg == PUSHSUM) {
+        switch (S.topo) {
+            case LINE: GP_INIT(LINE, PUSHSUM); break;
+            case FULL: GP_INIT(FULL, PUSHSUM); break;
+            case GRID3D: GP_INIT(GRID3D, PUSHSUM); break;
+            default: GP_INIT(IMP3D, PUSHSUM); break;
+        }
+    } else {
+        switch (S.topo) {
+            case LINE: GP_INIT(LINE, GOSSIP); break;
+            case FULL: GP_INIT(FULL, GOSSIP); break;
+            case GRID3D: GP_INIT(GRID3D, GOSSIP); break;
+            default: GP_INIT(IMP3D, GOSSIP); break;
+        }
+    }
+#undef GP_INIT
+    return hipGetLastError();
+}
+
+hipError_t launch_topo_rnd(const DevState& S, int grid, hipStream_t st) {
+    hipLaunchKernelGGL(k_topo_rnd, dim3(grid), dim3(BULK_THREADS), 0, st, S);
+    return hipGetLastError();
+}
+
+hipError_t launch_injector_init(const DevState& S, int grid, hipStream_t st) {
+    hipLaunchKernelGGL(k_injector_init, dim3(grid), dim3(BULK_THREADS), 0, st, S);
+    return hipGetLastError();
+}
+
+hipError_t launch_iota(uint32_t* v, uint32_t n, int grid, hipStream_t st) {
+    hipLaunchKernelGGL(k_iota, dim3(grid), dim3(BULK_THREADS), 0, st, v, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_histogram(const uint32_t* keys, uint32_t n, uint32_t* counts, int grid, hipStream_t st) {
+    hipLaunchKernelGGL(k_histogram, dim3(grid), dim3(BULK_THREADS), 0, st, keys, n, counts);
+    return hipGetLastError();
+}
+
+hipError_t launch_bulk(const DevState& S, uint32_t round, int grid, hipStream_t st) {
+    const dim3 g(grid), b(BULK_THREADS);
+    if (S.alg == PUSHSUM) {
+        switch (S.topo) {
+            case LINE: hipLaunchKernelGGL(k_pushsum_round<LINE>, g, b, 0, st, S, round); break;
+            case GRID3D: hipLaunchKernelGGL(k_pushsum_round<GRID3D>, g, b, 0, st, S, round); break;
+            case IMP3D: hipLaunchKernelGGL(k_pushsum_round<IMP3D>, g, b, 0, st, S, round); break;
+            default: hipLaunchKernelGGL(k_full_ps_recv, g, b, 0, st, S, round); break;
+        }
+    } else {
+        switch (S.topo) {
+            case LINE: hipLaunchKernelGGL(k_gossip_round<LINE>, g, b, 0, st, S, round); break;
+            case GRID3D: hipLaunchKernelGGL(k_gossip_round<GRID3D>, g, b, 0, st, S, round); break;
+            case IMP3D: hipLaunchKernelGGL(k_gossip_round<IMP3D>, g, b, 0, st, S, round); break;
+            default:
+                hipLaunchKernelGGL(k_full_gossip_send, g, b, 0, st, S, round);
+                hipLaunchKernelGGL(k_full_gossip_recv, g, b, 0, st, S, round);
+                break;
+        }
+    }
+    return hipGetLastError();
+}
+
+const char* bulk_kernel_name(const DevState& S) {
+    static const char* ps[] = {"k_pushsum_round<LINE>", "k_full_ps_recv", "k_pushsum_round<GRID3D>",
+                               "k_pushsum_round<IMP3D>"};
+    static const char* go[] = {"k_gossip_round<LINE>", "k_full_gossip_send+recv", "k_gossip_round<GRID3D>",
+                               "k_gossip_round<IMP3D>"};
+    return S.alg == PUSHSUM ? ps[S.topo] : go[S.topo];
+}
+
+hipError_t launch_finalize(const DevState& S, uint32_t round_done, uint32_t round_next, hipStream_t st) {
+    const int has_done = round_next > 0;
+    const int injector = (S.alg == GOSSIP && S.topo != FULL) ? 1 : 0;
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(FIN_THREADS), 0, st, S, round_done, round_next, has_done,
+                       injector);
+    return hipGetLastError();
+}
+
+hipError_t launch_full_pushsum_send(const DevState& S, uint32_t round, int grid, hipStream_t st) {
+    hipLaunchKernelGGL(k_full_ps_send, dim3(grid), dim3(BULK_THREADS), 0, st, S, round);
+    return hipGetLastError();
+}
+
+hipError_t launch_full_pushsum_mark(const DevState& S, int grid, hipStream_t st) {
+    hipLaunchKernelGGL(k_full_ps_mark, dim3(grid), dim3(BULK_THREADS), 0, st, S);
+    return hipGetLastError();
+}
+
+hipError_t launch_full_pushsum_recv(const DevState& S, uint32_t round, int grid, hipStream_t st) {
+    hipLaunchKernelGGL(k_full_ps_recv, dim3(grid), dim3(BULK_THREADS), 0, st, S, round);
+    return hipGetLastError();
+}
+
+}  // namespace gp
