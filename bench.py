@@ -1,0 +1,211 @@
+"""bench.py -- headline benchmark (BASELINE.json `metric`).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+Workload: push-sum on the imperfect-3D lattice with 1e9 nodes (g = 1000,
+BASELINE config 4 = C5), which fits one MI355X (46 GB of state).  A "step" is one
+synchronous round over all P nodes; the metric is node-updates/s = P * rounds /
+wall time of the K timed rounds (max over ranks), with the state already
+resident in HBM.  Before the timed region the simulation is advanced until
+every node is active (steady state: every node sends a message each round),
+then W warmup rounds; convergence is never reached inside the timed window.
+
+One JSON line on stdout (rank 0).  `roofline` is measured live: HIP events on
+the library's stream bracket every round kernel (k_pushsum_round<IMP3D>); its
+algorithmic bytes per node-round are DESIGN.md §4's figure.  `traffic` comes
+from the committed rocprofv3 PMC summary (profiles/) when it matches the
+workload.  `cpu_baseline` times the SRS v1 C oracle on the host cores over a
+bounded sample of the same workload (steady state, smaller lattice).
+
+Multi-GPU (N > 1, launched by torch.distributed.run): one process per GPU,
+contiguous plane-aligned node slabs, RCCL exchange inside libgossip_hip.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "node-updates/sec (whole node) + achieved HBM GB/s %, imp3D push-sum 1e9 nodes"
+HBM_PEAK_GBPS = 8000.0  # MI355X spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def preroll(sim, population, cap=2000):
+    """Advance until every node is active (push-sum activation front has swept the lattice)."""
+    rounds = 0
+    while rounds < cap:
+        info = sim.info()
+        if info.active >= population:
+            return rounds
+        rounds += len(sim.step(8))
+    raise RuntimeError("activation did not complete within %d rounds" % cap)
+
+
+def traffic_from_profiles(workload_key):
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    rec = d.get(workload_key)
+    return rec.get("hbm_bytes_per_launch") if rec else None
+
+
+def cpu_baseline(args):
+    """SRS v1 C oracle on the host cores, steady state, bounded to ~10-20 s."""
+    from tests.oracle_ctypes import Oracle
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    threads = min(threads, os.cpu_count() or threads)
+    n = args.cpu_nodes
+    orc = Oracle(n, args.topology, args.algorithm, args.seed, threads=threads)
+    P = orc.P
+    t0 = time.perf_counter()
+    while orc.active_count() < P:
+        orc.step(5)
+        if time.perf_counter() - t0 > 120:
+            break
+    pre = orc.rounds
+    rounds, t = 0, 0.0
+    while t < args.cpu_seconds and rounds < 400:
+        t1 = time.perf_counter()
+        rounds += len(orc.step(2))
+        t += time.perf_counter() - t1
+    orc.close()
+    return {
+        "value": P * rounds / t,
+        "unit": "node-updates/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"SRS v1 C oracle (oracle/srs_oracle.c, OpenMP), {args.topology} {args.algorithm} "
+                  f"n={n} (P={P}), {rounds} steady-state rounds after a {pre}-round activation pre-roll, "
+                  f"{t:.1f} s timed",
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--nodes", type=int, default=10**9)
+    ap.add_argument("--topology", default="Imp3D")
+    ap.add_argument("--algorithm", default="push-sum")
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--cpu-nodes", type=int, default=200**3)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--converge", action="store_true", help="also run a fresh simulation to convergence")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    from gossipprotocol_amd import Simulation
+    from gossipprotocol_amd import _lib as L
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # gloo: host-side barrier / max only; data path is RCCL in the library
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    def max_over_ranks(x):
+        if dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    sim = Simulation(args.nodes, args.topology, args.algorithm, seed=args.seed, device=local_rank,
+                     kernel_timing=True, rank=rank, world=world, dist=dist)
+    P = sim.population
+    t_pre = time.perf_counter()
+    pre = preroll(sim, P) if args.algorithm == "push-sum" else 0
+    log(f"[bench] rank {rank}: P={P} activation pre-roll {pre} rounds ({time.perf_counter() - t_pre:.1f} s)")
+    sim.step(args.warmup)
+    sim.sync()
+    sim.kernel_stats(reset=True)
+    barrier()
+    t0 = time.perf_counter()
+    got = sim.step(args.steps)
+    sim.sync()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if len(got) != args.steps:
+        raise RuntimeError(f"only {len(got)} of {args.steps} timed rounds ran (converged inside the window)")
+    elapsed = max_over_ranks(elapsed)
+    kms, launches, kname = sim.kernel_stats()
+    bytes_per_node = sim.alg_bytes_per_node()
+    local_nodes = sim.local_population
+    sim.close()
+
+    value = P * args.steps / elapsed
+    avg_ms = kms / max(1, launches)
+    achieved = bytes_per_node * local_nodes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    key = f"{args.topology}-{args.algorithm}-{args.nodes}-gpus{world}"
+    traffic = traffic_from_profiles(key)
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "node-updates/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": {
+            "workload": f"push-sum rounds, {args.topology} lattice, n={args.nodes} (P={P}), steady state "
+                        f"(all nodes active), seed {args.seed}",
+            "num_nodes": args.nodes, "population": P, "topology": args.topology, "algorithm": args.algorithm,
+            "parallelism": f"slab{world}", "activation_preroll_rounds": pre,
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": kname,
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBPS,
+            "traffic": traffic,
+            "alg_bytes_per_node_round": bytes_per_node,
+            "kernel_avg_ms": avg_ms,
+        },
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(args)
+    if rank == 0 and world == 1 and args.converge:
+        with Simulation(args.nodes, args.topology, args.algorithm, seed=args.seed, device=local_rank) as s2:
+            res = s2.run()
+            out["config"]["convergence"] = {"rounds": res.rounds, "converged": res.status == L.GP_STATUS_CONVERGED,
+                                            "elapsed_ms": res.elapsed_ms}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

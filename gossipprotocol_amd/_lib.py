@@ -10,6 +10,8 @@ import os
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "libgossip_hip.so")
+# experiments (tools/ablate.py) may point at an ablation build; the product uses the in-tree library
+LIB_PATH = os.environ.get("GOSSIP_HIP_LIB_EXPERIMENT", LIB_PATH)
 
 GP_LINE, GP_FULL, GP_3D, GP_IMP3D = 0, 1, 2, 3
 GP_GOSSIP, GP_PUSHSUM = 0, 1
@@ -34,7 +36,8 @@ class GpInfo(C.Structure):
     _fields_ = [("population", C.c_int64), ("threshold", C.c_int64), ("grid", C.c_int64),
                 ("seed_node", C.c_int64), ("rounds", C.c_int64), ("alerts_total", C.c_int64),
                 ("active", C.c_int64), ("topology", C.c_int32), ("algorithm", C.c_int32),
-                ("device", C.c_int32), ("num_gpus", C.c_int32)]
+                ("device", C.c_int32), ("num_gpus", C.c_int32), ("slab_first", C.c_int64),
+                ("slab_count", C.c_int64)]
 
 
 # (name, restype, argtypes) for every symbol include/gossip_hip.h declares

@@ -350,6 +350,10 @@ int gp_create(const gp_config* cfg, gp_sim** out) {
     std::memset(s->host_ctl, 0, sizeof(Ctl));
     s->host_ctl->active_total = 1;  // the seed
     s->host_ctl->all_active = P <= 1 ? 1u : 0u;
+#if defined(GP_ABLATE) && (GP_ABLATE & 1)
+    s->host_ctl->active_total = (unsigned long long)P;  // experiment builds only (tools/ablate.py)
+    s->host_ctl->all_active = 1u;
+#endif
     s->host_ctl->inj_target = -1;
     if (hipMemcpyAsync(S.ctl, s->host_ctl, sizeof(Ctl), hipMemcpyHostToDevice, s->stream) != hipSuccess ||
         launch_init(S, s->grid, s->stream) != hipSuccess) {
@@ -576,6 +580,8 @@ int gp_get_info(gp_sim* s, gp_info* o) {
     o->algorithm = s->S.alg;
     o->device = s->device;
     o->num_gpus = 1;
+    o->slab_first = 0;
+    o->slab_count = s->P;
     return GP_OK;
 }
 

@@ -16,6 +16,18 @@
 // CPU oracle.
 #include "gp_internal.hpp"
 
+// Experiment-only ablation switches (tools/ablate.py builds variants with
+// -DGP_ABLATE=<mask>); the product is built with GP_ABLATE = 0.
+#ifndef GP_ABLATE
+#define GP_ABLATE 0
+#endif
+#define ABL_ALLACTIVE 1   // init: every node active (steady state from round 0)
+#define ABL_NO_INLIST 2   // skip the Imp3D in-list
+#define ABL_NO_RGATHER 4  // in-list: decide but do not gather the sender's (s, w)
+#define ABL_NO_LATTICE 8  // skip lattice in-messages
+#define ABL_NO_NEXTDIR 16 // skip the next-round Philox draw
+#define ABL_NO_RATIO 32   // skip the ratio test
+
 namespace gp {
 
 // ---------------------------------------------------------------- helpers
@@ -77,7 +89,7 @@ template <int TOPO, int ALG>
 __global__ __launch_bounds__(BULK_THREADS) void k_init(DevState S) {
     const uint32_t P = S.G.P;
     for (uint32_t j = blockIdx.x * BULK_THREADS + threadIdx.x; j < P; j += gridDim.x * BULK_THREADS) {
-        const bool seed = j == S.seed_node;
+        const bool seed = (GP_ABLATE & ABL_ALLACTIVE) ? true : j == S.seed_node;
         uint32_t dir = DIR_NONE;
         if (TOPO != FULL && seed) {
             const uint32_t mask = present_mask<TOPO>(j, S.G);
@@ -163,7 +175,7 @@ __global__ __launch_bounds__(BULK_THREADS) void k_pushsum_round(DevState S, uint
         constexpr uint32_t ND = TOPO == LINE ? 2 : 6;
 #pragma unroll
         for (uint32_t d = 0; d < ND; ++d) {
-            if (mask & (1u << d)) {
+            if (!(GP_ABLATE & ABL_NO_LATTICE) && (mask & (1u << d))) {
                 const uint32_t n = nbr<TOPO>(j, d, S.G);
                 if ((uint32_t)(nbc[n] & DIR_MASK) == (d ^ 1u)) {
                     const double2 m = swc[n];
@@ -173,7 +185,7 @@ __global__ __launch_bounds__(BULK_THREADS) void k_pushsum_round(DevState S, uint
                 }
             }
         }
-        if (TOPO == IMP3D) {
+        if (TOPO == IMP3D && !(GP_ABLATE & ABL_NO_INLIST)) {
             const uint32_t e1 = in_off[j + 1];
             for (uint32_t e = in_off[j]; e < e1; ++e) {
                 const uint32_t i = in_src[e];
@@ -187,7 +199,7 @@ __global__ __launch_bounds__(BULK_THREADS) void k_pushsum_round(DevState S, uint
                     sent = (nbc[i] & DIR_MASK) == DIR_RANDOM;
                 }
                 if (sent) {
-                    const double2 m = swc[i];
+                    const double2 m = (GP_ABLATE & ABL_NO_RGATHER) ? make_double2((double)i, 1.0) : swc[i];
                     acc_s = acc_s + m.x * 0.5;
                     acc_w = acc_w + m.y * 0.5;
                     recv = true;
@@ -196,7 +208,7 @@ __global__ __launch_bounds__(BULK_THREADS) void k_pushsum_round(DevState S, uint
         }
         uint32_t flags = b & (B_ACTIVE | B_CONV | (3u << CNT_SHIFT));
         if (recv) {
-            if (!(b & B_CONV)) {
+            if (!(GP_ABLATE & ABL_NO_RATIO) && !(b & B_CONV)) {
                 const double r_old = sv.x / sv.y;
                 const double r_new = acc_s / acc_w;
                 uint32_t cnt = (b >> CNT_SHIFT) & 3u;
@@ -213,7 +225,8 @@ __global__ __launch_bounds__(BULK_THREADS) void k_pushsum_round(DevState S, uint
                 active = true;
             }
         }
-        const uint32_t dir = active ? draw_dir<TOPO>(S, S_PUSHSUM, j, mask, r + 1) : DIR_NONE;
+        const uint32_t dir = (GP_ABLATE & ABL_NO_NEXTDIR) ? (j % 7u)
+                             : active ? draw_dir<TOPO>(S, S_PUSHSUM, j, mask, r + 1) : DIR_NONE;
         nbn[j] = (uint8_t)(flags | dir);
         swn[j] = make_double2(acc_s, acc_w);
     }

@@ -40,7 +40,8 @@ class Simulation:
     """One simulated network on one MI355X (handle over gp_sim)."""
 
     def __init__(self, num_nodes: int, topology: str, algorithm: str, seed: int = 1,
-                 max_rounds: int = 0, device: int = 0, kernel_timing: bool = False):
+                 max_rounds: int = 0, device: int = 0, kernel_timing: bool = False,
+                 rank: int = 0, world: int = 1, dist=None):
         cfg = L.GpConfig()
         cfg.num_nodes = num_nodes
         cfg.topology = parse_topology(topology)
@@ -52,7 +53,20 @@ class Simulation:
         cfg.flags = L.GP_FLAG_KERNEL_TIMING if kernel_timing else 0
         self.topology, self.algorithm = topology, algorithm
         h = C.c_void_p()
-        L.check(L.lib().gp_create(C.byref(cfg), C.byref(h)))
+        if world > 1:
+            # one process per GPU: rank 0 makes the RCCL id, the caller's process
+            # group (gloo is enough) broadcasts it, every rank joins its slab
+            uid = C.create_string_buffer(128)
+            if rank == 0:
+                L.check(L.lib().gp_get_unique_id(uid))
+            if dist is None:
+                raise ValueError("world > 1 needs a torch.distributed process group to share the RCCL id")
+            box = [uid.raw if rank == 0 else None]
+            dist.broadcast_object_list(box, src=0)
+            uid = C.create_string_buffer(box[0], 128)
+            L.check(L.lib().gp_create_rank(C.byref(cfg), rank, world, uid, C.byref(h)))
+        else:
+            L.check(L.lib().gp_create(C.byref(cfg), C.byref(h)))
         self._h = h
 
     # -- lifecycle -------------------------------------------------------
@@ -95,6 +109,11 @@ class Simulation:
     @property
     def population(self):
         return self.info().population
+
+    @property
+    def local_population(self):
+        """Nodes owned by this handle (its slab; all P for a single GPU)."""
+        return self.info().slab_count
 
     @property
     def threshold(self):

@@ -84,7 +84,8 @@ typedef struct gp_info {
     int64_t seed_node;                    /* `choice` (Program.fs:193,221,263) */
     int64_t rounds, alerts_total, active; /* progress */
     int32_t topology, algorithm;
-    int32_t device, num_gpus;
+    int32_t device, num_gpus;             /* num_gpus = ranks sharing the population */
+    int64_t slab_first, slab_count;       /* node ids owned by this handle */
 } gp_info;
 
 /* Library version (GP_VERSION). */
