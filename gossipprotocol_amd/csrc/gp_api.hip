@@ -285,7 +285,9 @@ int gp_create(const gp_config* cfg, gp_sim** out) {
     hipDeviceProp_t prop;
     (void)hipGetDeviceProperties(&prop, s->device);
     const int64_t blocks = (P + BULK_THREADS - 1) / BULK_THREADS;
-    int64_t cap = (int64_t)prop.multiProcessorCount * 8;
+    // 64 workgroups per CU: measured best for the tiled round kernels (tools/ablate.py:
+    // 2048 -> 27.5, 8192 -> 22.1, 16384 -> 21.2 ms/round at P = 1e9)
+    int64_t cap = (int64_t)prop.multiProcessorCount * 64;
     if (const char* e = std::getenv("GP_GRID")) cap = std::max<int64_t>(1, std::atoll(e));
     s->grid = (int)std::max<int64_t>(1, std::min(blocks, cap));
 
@@ -305,17 +307,18 @@ int gp_create(const gp_config* cfg, gp_sim** out) {
 
     const size_t Pn = (size_t)P;
     if ((rc = dev_alloc_t(s, &S.ctl, 1))) return fail(rc);
+    const size_t Pnb = Pn + 1024;  // node-byte arrays: tiles read/write whole words past P
     if (S.alg == PUSHSUM) {
         if ((rc = dev_alloc_t(s, &S.sw[0], Pn)) || (rc = dev_alloc_t(s, &S.sw[1], Pn)) ||
-            (rc = dev_alloc_t(s, &S.nb[0], Pn)))
+            (rc = dev_alloc_t(s, &S.nb[0], Pnb)))
             return fail(rc);
-        if (S.topo != FULL && (rc = dev_alloc_t(s, &S.nb[1], Pn))) return fail(rc);
+        if (S.topo != FULL && (rc = dev_alloc_t(s, &S.nb[1], Pnb))) return fail(rc);
     } else {
         if ((rc = dev_alloc_t(s, &S.c, Pn))) return fail(rc);
         if (S.topo == FULL) {
             if ((rc = dev_alloc_t(s, &S.inc, Pn))) return fail(rc);
         } else {
-            if ((rc = dev_alloc_t(s, &S.nb[0], Pn)) || (rc = dev_alloc_t(s, &S.nb[1], Pn))) return fail(rc);
+            if ((rc = dev_alloc_t(s, &S.nb[0], Pnb)) || (rc = dev_alloc_t(s, &S.nb[1], Pnb))) return fail(rc);
             S.nchunks = (uint32_t)((T + INJ_CHUNK - 1) / INJ_CHUNK);
             if ((rc = dev_alloc_t(s, &S.live_bits, (size_t)S.nchunks * (INJ_CHUNK / 32))) ||
                 (rc = dev_alloc_t(s, &S.chunk_live, S.nchunks)))
@@ -341,7 +344,12 @@ int gp_create(const gp_config* cfg, gp_sim** out) {
         S.sort_tmp_bytes = tb;
         if ((rc = dev_alloc(s, &S.sort_tmp, tb))) return fail(rc);
     }
-    if (S.topo == IMP3D && (rc = build_imp3d(s))) return fail(rc);
+    if (S.topo == IMP3D) {
+        S.rbits_words = rbits_words_for(S.G.P);
+        if ((rc = dev_alloc_t(s, &S.rbits[0], S.rbits_words)) || (rc = dev_alloc_t(s, &S.rbits[1], S.rbits_words)))
+            return fail(rc);
+        if ((rc = build_imp3d(s))) return fail(rc);
+    }
 
     if (hipHostMalloc((void**)&s->host_ctl, sizeof(Ctl), hipHostMallocDefault) != hipSuccess) {
         set_err("hipHostMalloc failed");
@@ -350,14 +358,14 @@ int gp_create(const gp_config* cfg, gp_sim** out) {
     std::memset(s->host_ctl, 0, sizeof(Ctl));
     s->host_ctl->active_total = 1;  // the seed
     s->host_ctl->all_active = P <= 1 ? 1u : 0u;
-#if defined(GP_ABLATE) && (GP_ABLATE & 1)
-    s->host_ctl->active_total = (unsigned long long)P;  // experiment builds only (tools/ablate.py)
-    s->host_ctl->all_active = 1u;
-#endif
     s->host_ctl->inj_target = -1;
     if (hipMemcpyAsync(S.ctl, s->host_ctl, sizeof(Ctl), hipMemcpyHostToDevice, s->stream) != hipSuccess ||
         launch_init(S, s->grid, s->stream) != hipSuccess) {
         set_err("init launch failed");
+        return fail(GP_EHIP);
+    }
+    if (S.topo == IMP3D && launch_rbits_init(S, s->grid, s->stream) != hipSuccess) {
+        set_err("random-edge bitmap init failed");
         return fail(GP_EHIP);
     }
     if (S.alg == GOSSIP && S.topo != FULL && launch_injector_init(S, s->grid, s->stream) != hipSuccess) {

@@ -41,6 +41,10 @@ struct DevState {
     uint8_t* nb[2];
     // gossip: rumour counters (in place), direction byte double buffered (nb)
     int32_t* c;
+    // Imp3D: bit i of rbits[b] = node i sends on its random edge in the round
+    // of buffer b (ballot-packed by the round kernel)
+    uint64_t* rbits[2];
+    uint32_t rbits_words;
     // Imp3D: random edge and receiver-sorted in-lists (CSR)
     uint32_t* rnd;
     uint32_t* in_off;  // P+1
@@ -58,6 +62,28 @@ struct DevState {
     size_t sort_tmp_bytes;
     uint32_t key_bits;
 };
+
+// Arguments of the tiled round kernels (gp_round.hip): only what they read.
+struct RoundArgs {
+    const double2* swc;
+    double2* swn;
+    const uint8_t* nbc;
+    uint8_t* nbn;
+    const uint64_t* rbc;
+    uint64_t* rbn;
+    const uint32_t* in_off;
+    const uint32_t* in_src;
+    int32_t* c;
+    Ctl* ctl;
+    Geom G;
+    uint32_t k0, k1, seed_node, ntiles;
+};
+
+// ---- tiled round kernels (gp_round.hip)
+uint32_t round_tiles(uint32_t P);
+uint32_t rbits_words_for(uint32_t P);
+hipError_t launch_round_tile(const DevState& S, uint32_t round, int grid, hipStream_t st);
+hipError_t launch_rbits_init(const DevState& S, int grid, hipStream_t st);
 
 // ---- kernels (gp_kernels.hip)
 hipError_t launch_init(const DevState& S, int grid, hipStream_t st);

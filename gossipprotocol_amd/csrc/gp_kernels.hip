@@ -2,31 +2,17 @@
 // push-sum round (SRS v1).
 //
 // Design:
-//   * one bulk kernel per round for line / 3D / Imp3D: every node PULLS its
-//     in-messages -- lattice neighbours through the 1-byte direction each
-//     sender chose one round earlier, Imp3D random edges through the
-//     receiver-sorted in-list -- and folds them in the canonical order, then
-//     draws its own direction for the next round.  No message is staged in HBM;
+//   * the per-round bulk kernels for line / 3D / Imp3D live in gp_round.hip;
+//     this file holds setup kernels, the full-topology round and the finalize
+//     kernel;
 //   * state is double-buffered (round r reads buffer r&1, writes r&1^1), so the
-//     bulk kernel needs no inter-workgroup synchronisation;
+//     bulk kernels need no inter-workgroup synchronisation;
 //   * a single-workgroup finalize kernel closes the round: alert bookkeeping
 //     (scheduler, Program.fs:41-61), done flag, and the gossip injector
 //     (Actor2, Program.fs:141-163) for the next round.
 // Built with -ffp-contract=off: the push-sum fold must round exactly like the
 // CPU oracle.
 #include "gp_internal.hpp"
-
-// Experiment-only ablation switches (tools/ablate.py builds variants with
-// -DGP_ABLATE=<mask>); the product is built with GP_ABLATE = 0.
-#ifndef GP_ABLATE
-#define GP_ABLATE 0
-#endif
-#define ABL_ALLACTIVE 1   // init: every node active (steady state from round 0)
-#define ABL_NO_INLIST 2   // skip the Imp3D in-list
-#define ABL_NO_RGATHER 4  // in-list: decide but do not gather the sender's (s, w)
-#define ABL_NO_LATTICE 8  // skip lattice in-messages
-#define ABL_NO_NEXTDIR 16 // skip the next-round Philox draw
-#define ABL_NO_RATIO 32   // skip the ratio test
 
 namespace gp {
 
@@ -89,7 +75,7 @@ template <int TOPO, int ALG>
 __global__ __launch_bounds__(BULK_THREADS) void k_init(DevState S) {
     const uint32_t P = S.G.P;
     for (uint32_t j = blockIdx.x * BULK_THREADS + threadIdx.x; j < P; j += gridDim.x * BULK_THREADS) {
-        const bool seed = (GP_ABLATE & ABL_ALLACTIVE) ? true : j == S.seed_node;
+        const bool seed = j == S.seed_node;
         uint32_t dir = DIR_NONE;
         if (TOPO != FULL && seed) {
             const uint32_t mask = present_mask<TOPO>(j, S.G);
@@ -139,147 +125,6 @@ __global__ __launch_bounds__(BULK_THREADS) void k_injector_init(DevState S) {
         S.chunk_live[c] = (uint32_t)(hi - lo);
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) S.ctl->live = T;
-}
-
-// ---------------------------------------------------------------- push-sum round
-// MainPushSum (Program.fs:101-131) as one synchronous round, pull form:
-//   own half (Program.fs:104-105,125-126) -> lattice in-messages in the
-//   receiver's slot order -> Imp3D random-edge messages by ascending sender ->
-//   ratio test against the round-start ratio (Program.fs:114-123, SRS D5) ->
-//   direction for round r+1.
-template <int TOPO>
-__global__ __launch_bounds__(BULK_THREADS) void k_pushsum_round(DevState S, uint32_t r) {
-    __shared__ uint32_t red[2][BULK_THREADS / 64];
-    Ctl* ctl = S.ctl;
-    if (ld_agent(&ctl->done)) return;
-    const bool all_active = ld_agent(&ctl->all_active) != 0;
-    const int cur = r & 1;
-    const double2* __restrict__ swc = S.sw[cur];
-    double2* __restrict__ swn = S.sw[cur ^ 1];
-    const uint8_t* __restrict__ nbc = S.nb[cur];
-    uint8_t* __restrict__ nbn = S.nb[cur ^ 1];
-    const uint32_t* __restrict__ in_off = S.in_off;
-    const uint32_t* __restrict__ in_src = S.in_src;
-    const uint32_t P = S.G.P;
-    uint32_t alerts = 0, newly = 0;
-    for (uint32_t j = blockIdx.x * BULK_THREADS + threadIdx.x; j < P; j += gridDim.x * BULK_THREADS) {
-        const uint8_t b = nbc[j];
-        const double2 sv = swc[j];
-        const uint32_t mask = present_mask<TOPO>(j, S.G);
-        const uint32_t deg = degree_of<TOPO>(mask);
-        bool active = (b & B_ACTIVE) != 0;
-        const bool halve = active && deg > 0;
-        double acc_s = halve ? sv.x * 0.5 : sv.x;
-        double acc_w = halve ? sv.y * 0.5 : sv.y;
-        bool recv = false;
-        constexpr uint32_t ND = TOPO == LINE ? 2 : 6;
-#pragma unroll
-        for (uint32_t d = 0; d < ND; ++d) {
-            if (!(GP_ABLATE & ABL_NO_LATTICE) && (mask & (1u << d))) {
-                const uint32_t n = nbr<TOPO>(j, d, S.G);
-                if ((uint32_t)(nbc[n] & DIR_MASK) == (d ^ 1u)) {
-                    const double2 m = swc[n];
-                    acc_s = acc_s + m.x * 0.5;
-                    acc_w = acc_w + m.y * 0.5;
-                    recv = true;
-                }
-            }
-        }
-        if (TOPO == IMP3D && !(GP_ABLATE & ABL_NO_INLIST)) {
-            const uint32_t e1 = in_off[j + 1];
-            for (uint32_t e = in_off[j]; e < e1; ++e) {
-                const uint32_t i = in_src[e];
-                bool sent;
-                if (all_active) {
-                    // every sender is active: recompute its draw instead of a
-                    // random 1-byte gather
-                    const uint32_t di = degree_of<IMP3D>(present_mask<IMP3D>(i, S.G));
-                    sent = uniform(S.k0, S.k1, S_PUSHSUM, i, r, di) == di - 1;
-                } else {
-                    sent = (nbc[i] & DIR_MASK) == DIR_RANDOM;
-                }
-                if (sent) {
-                    const double2 m = (GP_ABLATE & ABL_NO_RGATHER) ? make_double2((double)i, 1.0) : swc[i];
-                    acc_s = acc_s + m.x * 0.5;
-                    acc_w = acc_w + m.y * 0.5;
-                    recv = true;
-                }
-            }
-        }
-        uint32_t flags = b & (B_ACTIVE | B_CONV | (3u << CNT_SHIFT));
-        if (recv) {
-            if (!(GP_ABLATE & ABL_NO_RATIO) && !(b & B_CONV)) {
-                const double r_old = sv.x / sv.y;
-                const double r_new = acc_s / acc_w;
-                uint32_t cnt = (b >> CNT_SHIFT) & 3u;
-                cnt = fabs(r_new - r_old) > 1e-10 ? 0u : cnt + 1u;
-                flags = (flags & ~(3u << CNT_SHIFT)) | (cnt << CNT_SHIFT);
-                if (cnt == 3) {
-                    flags |= B_CONV;
-                    ++alerts;
-                }
-            }
-            if (!active) {
-                ++newly;
-                flags |= B_ACTIVE;
-                active = true;
-            }
-        }
-        const uint32_t dir = (GP_ABLATE & ABL_NO_NEXTDIR) ? (j % 7u)
-                             : active ? draw_dir<TOPO>(S, S_PUSHSUM, j, mask, r + 1) : DIR_NONE;
-        nbn[j] = (uint8_t)(flags | dir);
-        swn[j] = make_double2(acc_s, acc_w);
-    }
-    block_sum2(alerts, newly, red);
-    if (threadIdx.x == 0) {
-        if (alerts) atomicAdd(&ctl->round_alerts, (unsigned long long)alerts);
-        if (newly) atomicAdd(&ctl->round_active, (unsigned long long)newly);
-    }
-}
-
-// ---------------------------------------------------------------- gossip round
-// Process1/Process2 (Program.fs:84-98) as one synchronous round, pull form:
-// deliveries = lattice senders whose direction points here + Imp3D random-edge
-// senders + the injector; dropped if this node was converged at round start
-// (the sender-side `dictionary` check, Program.fs:87, applied at the receiver).
-template <int TOPO>
-__global__ __launch_bounds__(BULK_THREADS) void k_gossip_round(DevState S, uint32_t r) {
-    __shared__ uint32_t red[2][BULK_THREADS / 64];
-    Ctl* ctl = S.ctl;
-    if (ld_agent(&ctl->done)) return;
-    const long long inj = ld_agent(&ctl->inj_target);
-    const int cur = r & 1;
-    const uint8_t* __restrict__ nbc = S.nb[cur];
-    uint8_t* __restrict__ nbn = S.nb[cur ^ 1];
-    int32_t* __restrict__ cc = S.c;
-    const uint32_t P = S.G.P;
-    uint32_t alerts = 0, unused = 0;
-    for (uint32_t j = blockIdx.x * BULK_THREADS + threadIdx.x; j < P; j += gridDim.x * BULK_THREADS) {
-        const int32_t c0 = cc[j];
-        const uint32_t mask = present_mask<TOPO>(j, S.G);
-        int32_t c1 = c0;
-        if (c0 < (int32_t)GOSSIP_DONE) {
-            uint32_t inc = (long long)j == inj ? 1u : 0u;
-            constexpr uint32_t ND = TOPO == LINE ? 2 : 6;
-#pragma unroll
-            for (uint32_t d = 0; d < ND; ++d)
-                if (mask & (1u << d)) inc += (uint32_t)(nbc[nbr<TOPO>(j, d, S.G)] & DIR_MASK) == (d ^ 1u);
-            if (TOPO == IMP3D) {
-                const uint32_t e1 = S.in_off[j + 1];
-                for (uint32_t e = S.in_off[j]; e < e1; ++e)
-                    inc += (uint32_t)(nbc[S.in_src[e]] & DIR_MASK) == DIR_RANDOM;
-            }
-            if (inc) {
-                c1 = c0 + (int32_t)inc;
-                cc[j] = c1;
-                alerts += c1 > 10;  // the receipt that finds rumours == 10 (Program.fs:92-94)
-            }
-        }
-        const bool active = ((j == S.seed_node) || c1 >= 1) && c1 <= 10;
-        nbn[j] = (uint8_t)(active ? draw_dir<TOPO>(S, S_GOSSIP, j, mask, r + 1) : DIR_NONE);
-    }
-    block_sum2(alerts, unused, red);
-    if (threadIdx.x == 0 && alerts) atomicAdd(&ctl->round_alerts, (unsigned long long)alerts);
 }
 
 // ---------------------------------------------------------------- full topology
@@ -569,32 +414,21 @@ hipError_t launch_histogram(const uint32_t* keys, uint32_t n, uint32_t* counts, 
 
 hipError_t launch_bulk(const DevState& S, uint32_t round, int grid, hipStream_t st) {
     const dim3 g(grid), b(BULK_THREADS);
+    if (S.topo != FULL) return launch_round_tile(S, round, grid, st);
     if (S.alg == PUSHSUM) {
-        switch (S.topo) {
-            case LINE: hipLaunchKernelGGL(k_pushsum_round<LINE>, g, b, 0, st, S, round); break;
-            case GRID3D: hipLaunchKernelGGL(k_pushsum_round<GRID3D>, g, b, 0, st, S, round); break;
-            case IMP3D: hipLaunchKernelGGL(k_pushsum_round<IMP3D>, g, b, 0, st, S, round); break;
-            default: hipLaunchKernelGGL(k_full_ps_recv, g, b, 0, st, S, round); break;
-        }
+        hipLaunchKernelGGL(k_full_ps_recv, g, b, 0, st, S, round);
     } else {
-        switch (S.topo) {
-            case LINE: hipLaunchKernelGGL(k_gossip_round<LINE>, g, b, 0, st, S, round); break;
-            case GRID3D: hipLaunchKernelGGL(k_gossip_round<GRID3D>, g, b, 0, st, S, round); break;
-            case IMP3D: hipLaunchKernelGGL(k_gossip_round<IMP3D>, g, b, 0, st, S, round); break;
-            default:
-                hipLaunchKernelGGL(k_full_gossip_send, g, b, 0, st, S, round);
-                hipLaunchKernelGGL(k_full_gossip_recv, g, b, 0, st, S, round);
-                break;
-        }
+        hipLaunchKernelGGL(k_full_gossip_send, g, b, 0, st, S, round);
+        hipLaunchKernelGGL(k_full_gossip_recv, g, b, 0, st, S, round);
     }
     return hipGetLastError();
 }
 
 const char* bulk_kernel_name(const DevState& S) {
-    static const char* ps[] = {"k_pushsum_round<LINE>", "k_full_ps_recv", "k_pushsum_round<GRID3D>",
-                               "k_pushsum_round<IMP3D>"};
-    static const char* go[] = {"k_gossip_round<LINE>", "k_full_gossip_send+recv", "k_gossip_round<GRID3D>",
-                               "k_gossip_round<IMP3D>"};
+    static const char* ps[] = {"k_ps_tile<LINE>", "k_full_ps_send+sort+mark+recv", "k_ps_tile<GRID3D>",
+                               "k_ps_tile<IMP3D>"};
+    static const char* go[] = {"k_gossip_tile<LINE>", "k_full_gossip_send+recv", "k_gossip_tile<GRID3D>",
+                               "k_gossip_tile<IMP3D>"};
     return S.alg == PUSHSUM ? ps[S.topo] : go[S.topo];
 }
 

@@ -1,0 +1,499 @@
+// gp_round.hip -- the per-round bulk kernels for line / 3D / Imp3D (gfx950).
+//
+// One synchronous round of SRS v1 in PULL form: every node
+// reads who sent to it and folds the messages in canonical order, then draws
+// its own direction for the next round.  Layout per workgroup (256 threads,
+// TILE = 1024 consecutive nodes, 4 per thread, lane-contiguous):
+//
+//   1. stage in LDS with wide coalesced loads: the direction bytes of the tile
+//      and its +-g rows (y/z neighbours, or +-1 for line), the x-1 and x+1
+//      plane segments (3D), the tile's in-list offsets and senders (Imp3D);
+//   2. per node: lattice senders are read from LDS and only the (s, w) of the
+//      neighbours that actually sent here are gathered (independent loads, no
+//      dependent byte loads); Imp3D in-edges decide "sent on its random edge"
+//      from the sender's Philox draw (every node active) or from a ballot-packed
+//      bitmap (activation phase), then gather;
+//   3. fold in canonical order (own half, lattice slots, random edges by
+//      ascending sender), ratio test, next-round Philox draw; node bytes leave
+//      through LDS as 32-bit words, random-edge bits as one 64-bit ballot per
+//      wave.
+// Tiles are walked XCD-contiguously (blocks b and b+8 share an XCD on
+// MI355X), so the +-g rows a tile gathers from were just read by its XCD.
+// Built with -ffp-contract=off: the fold must round exactly like the oracle.
+#include "gp_internal.hpp"
+
+namespace gp {
+
+// Experiment knobs (tools/ablate.py); the product build uses the defaults.
+#ifndef GP_NPT
+#define GP_NPT 4
+#endif
+#ifndef GP_ABLATE
+#define GP_ABLATE 0
+#endif
+#ifndef GP_MINB
+#define GP_MINB 1  // __launch_bounds__ minimum waves per SIMD (= resident 256-thread blocks per CU)
+#endif
+#define ABL_NO_RGATHER 1   // in-list: decide but do not gather the sender's (s, w)
+#define ABL_NO_LGATHER 2   // lattice: decide but do not gather
+#define ABL_NO_INLIST 4    // skip the Imp3D in-list
+#define ABL_NO_NEXTDIR 8   // skip the next-round Philox draw
+#define ABL_NO_EPHILOX 16  // in-list: no Philox (sender never random)
+#define ABL_BITMAP_ONLY 32 // in-list: always read the random-edge bitmap, never recompute Philox
+#define ABL_NO_RATIO 64    // skip the ratio test
+
+namespace {
+
+constexpr int TPB = BULK_THREADS;          // 256
+constexpr int NPT = GP_NPT;                // nodes per thread per tile
+constexpr int TILE = TPB * NPT;            // 1024
+constexpr int HMAX = 1625;                 // largest lattice edge with g^3 < 2^32
+constexpr int W_ROWS = (TILE + 2 * HMAX) / 4 + 4;
+constexpr int W_PLANE = TILE / 4 + 4;
+constexpr int SRC_CAP = 1536;              // staged in-list entries per tile (mean 1024)
+constexpr int MSG_CAP = 384;               // random-edge messages parked per tile (mean ~146)
+constexpr uint16_t POS_NONE = 0xFFFF, POS_GLOBAL = 0xFFFE;
+
+struct TileLds {
+    uint32_t rows[W_ROWS];     // direction bytes of [j0 - H, j1 + H)
+    uint32_t xm[W_PLANE];      // direction bytes of [j0 - g^2, j1 - g^2)
+    uint32_t xp[W_PLANE];      // direction bytes of [j0 + g^2, j1 + g^2)
+    uint32_t off[TILE + 1];    // in_off[j0 .. j1]
+    uint32_t src[SRC_CAP];     // in_src[in_off[j0] .. in_off[j1])
+    uint32_t sent[SRC_CAP / 4];  // gossip: byte per staged in-edge, sender used its random edge
+    uint16_t pos[SRC_CAP];     // push-sum: slot of the edge's parked message (POS_NONE: not sent)
+    double2 msg[MSG_CAP];      // push-sum: random-edge messages gathered by the flattened pass
+    uint32_t nmsg;
+    uint32_t out[TILE / 4];    // next-round node bytes, stored as words
+    uint32_t red[2][TPB / 64];
+};
+
+__device__ __forceinline__ uint32_t lds_byte(const uint32_t* w, uint32_t idx) {
+    return reinterpret_cast<const uint8_t*>(w)[idx];
+}
+
+// Copy the bytes of nb[lo, hi) (clamped to [0, P)) into LDS words; returns the
+// node id of LDS byte 0.  Reads at most 3 bytes past hi (allocations are padded).
+__device__ __forceinline__ uint32_t stage_bytes(uint32_t* lds, const uint8_t* nb, int64_t lo, int64_t hi,
+                                                uint32_t P) {
+    if (lo < 0) lo = 0;
+    if (hi > (int64_t)P) hi = P;
+    const uint32_t ws = (uint32_t)lo & ~3u;
+    const int nw = hi > lo ? (int)(((uint32_t)hi + 3u - ws) >> 2) : 0;
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(nb + ws);
+    for (int w = threadIdx.x; w < nw; w += TPB) lds[w] = src[w];
+    return ws;
+}
+
+template <typename T>
+__device__ __forceinline__ T ld_agent(const T* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// XCD-contiguous tile walk: blocks with equal blockIdx % 8 own one contiguous
+// eighth of the tiles (speed only -- any placement is correct).
+struct TileWalk {
+    uint32_t t, end, step;
+    __device__ TileWalk(uint32_t ntiles) {
+        const uint32_t G = gridDim.x;
+        if (G >= 8 && (G & 7) == 0) {
+            const uint32_t x = blockIdx.x & 7, k = blockIdx.x >> 3;
+            const uint32_t lo = (uint32_t)((uint64_t)ntiles * x / 8);
+            end = (uint32_t)((uint64_t)ntiles * (x + 1) / 8);
+            t = lo + k;
+            step = G >> 3;
+        } else {
+            t = blockIdx.x;
+            end = ntiles;
+            step = G;
+        }
+    }
+};
+
+__device__ __forceinline__ double2 ld_sw(const double2* p) { return *p; }
+
+}  // namespace
+
+// ---------------------------------------------------------------- push-sum
+template <int TOPO>
+__global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t r) {
+    __shared__ TileLds L;
+    Ctl* ctl = a.ctl;
+    if (ld_agent(&ctl->done)) return;
+    const bool all_active = ld_agent(&ctl->all_active) != 0;
+    const double2* __restrict__ swc = a.swc;
+    double2* __restrict__ swn = a.swn;
+    const uint64_t* __restrict__ rbc = a.rbc;
+    const uint32_t* __restrict__ in_src = a.in_src;
+    const Geom G = a.G;
+    const uint32_t P = G.P;
+    const uint32_t H = TOPO == LINE ? 1u : G.g;
+    uint32_t alerts = 0, newly = 0;
+    const int lane = threadIdx.x & 63;
+
+    for (TileWalk tw(a.ntiles); tw.t < tw.end; tw.t += tw.step) {
+        const uint32_t j0 = tw.t * TILE;
+        const uint32_t j1 = min(P, j0 + TILE);
+        // own (s, w): issue first, consumed after staging
+        double2 own[NPT];
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            const uint32_t j = j0 + k * TPB + threadIdx.x;
+            own[k] = j < j1 ? swc[j] : make_double2(0.0, 1.0);
+        }
+        const uint32_t b_rows = stage_bytes(L.rows, a.nbc, (int64_t)j0 - H, (int64_t)j1 + H, P);
+        uint32_t b_xm = 0, b_xp = 0;
+        if (TOPO != LINE) {
+            b_xm = stage_bytes(L.xm, a.nbc, (int64_t)j0 - G.g2, (int64_t)j1 - G.g2, P);
+            b_xp = stage_bytes(L.xp, a.nbc, (int64_t)j0 + G.g2, (int64_t)j1 + G.g2, P);
+        }
+        if (TOPO == IMP3D)
+            for (uint32_t q = threadIdx.x; q <= j1 - j0; q += TPB) L.off[q] = a.in_off[j0 + q];
+        __syncthreads();
+        uint32_t e_lo = 0;
+        bool staged = true;
+        if (TOPO == IMP3D) {
+            e_lo = L.off[0];
+            const uint32_t cnt = L.off[j1 - j0] - e_lo;
+            staged = cnt <= (uint32_t)SRC_CAP;
+            if (threadIdx.x == 0) L.nmsg = 0;
+            if (staged)
+                for (uint32_t q = threadIdx.x; q < cnt; q += TPB) L.src[q] = in_src[e_lo + q];
+            __syncthreads();
+            if (staged) {
+                // Flattened, lane-balanced pass over the tile's in-edges: decide
+                // whether each sender used its random edge and gather its (s, w)
+                // into a compact LDS buffer, so the per-receiver loop below
+                // neither runs a wave's max in-degree of Philox draws nor waits
+                // on a random HBM read.  The LDS slot order is irrelevant: the
+                // fold walks edges in canonical (ascending sender) order.
+                for (uint32_t q = threadIdx.x; q < cnt; q += TPB) {
+                    const uint32_t i = L.src[q];
+                    bool sent;
+                    if (GP_ABLATE & ABL_NO_EPHILOX) {
+                        sent = false;
+                    } else if (all_active && !(GP_ABLATE & ABL_BITMAP_ONLY)) {
+                        const uint32_t di = popc6(present_mask<IMP3D>(i, G)) + 1u;
+                        sent = uniform(a.k0, a.k1, S_PUSHSUM, i, r, di) == di - 1u;
+                    } else {
+                        sent = (rbc[i >> 6] >> (i & 63)) & 1ull;
+                    }
+                    uint16_t p = POS_NONE;
+                    if (sent) {
+                        const uint32_t slot = atomicAdd(&L.nmsg, 1u);
+                        if (slot < (uint32_t)MSG_CAP) {
+                            L.msg[slot] = (GP_ABLATE & ABL_NO_RGATHER) ? make_double2((double)i, 1.0) : ld_sw(swc + i);
+                            p = (uint16_t)slot;
+                        } else {
+                            p = POS_GLOBAL;
+                        }
+                    }
+                    L.pos[q] = p;
+                }
+            }
+            __syncthreads();
+        }
+
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            const uint32_t jl = k * TPB + threadIdx.x;
+            const uint32_t j = j0 + jl;
+            const bool valid = j < j1;
+            uint32_t dir = DIR_NONE;
+            if (valid) {
+                const uint32_t b = lds_byte(L.rows, j - b_rows);
+                const uint32_t mask = present_mask<TOPO>(j, G);
+                const uint32_t deg = popc6(mask) + (TOPO == IMP3D ? 1u : 0u);
+                bool active = (b & B_ACTIVE) != 0;
+                const double2 sv = own[k];
+                const bool halve = active && deg > 0;
+                double acc_s = halve ? sv.x * 0.5 : sv.x;
+                double acc_w = halve ? sv.y * 0.5 : sv.y;
+                // lattice senders: direction bytes from LDS, (s, w) gathered only for real senders
+                uint32_t from = 0;
+                if (TOPO == LINE) {
+                    if ((mask & 1u) && (lds_byte(L.rows, j - 1 - b_rows) & DIR_MASK) == 1u) from |= 1u;
+                    if ((mask & 2u) && (lds_byte(L.rows, j + 1 - b_rows) & DIR_MASK) == 0u) from |= 2u;
+                } else {
+                    if ((mask & 1u) && (lds_byte(L.xm, j - G.g2 - b_xm) & DIR_MASK) == 1u) from |= 1u;
+                    if ((mask & 2u) && (lds_byte(L.xp, j + G.g2 - b_xp) & DIR_MASK) == 0u) from |= 2u;
+                    if ((mask & 4u) && (lds_byte(L.rows, j + G.g - b_rows) & DIR_MASK) == 3u) from |= 4u;
+                    if ((mask & 8u) && (lds_byte(L.rows, j - G.g - b_rows) & DIR_MASK) == 2u) from |= 8u;
+                    if ((mask & 16u) && (lds_byte(L.rows, j + 1 - b_rows) & DIR_MASK) == 5u) from |= 16u;
+                    if ((mask & 32u) && (lds_byte(L.rows, j - 1 - b_rows) & DIR_MASK) == 4u) from |= 32u;
+                }
+                constexpr uint32_t ND = TOPO == LINE ? 2 : 6;
+                double2 m[ND];
+#pragma unroll
+                for (uint32_t d = 0; d < ND; ++d)
+                    m[d] = (!(GP_ABLATE & ABL_NO_LGATHER) && (from & (1u << d))) ? ld_sw(swc + nbr<TOPO>(j, d, G))
+                                                                               : make_double2(0.0, 0.0);
+                bool recv = from != 0;
+#pragma unroll
+                for (uint32_t d = 0; d < ND; ++d) {
+                    if (from & (1u << d)) {
+                        acc_s = acc_s + m[d].x * 0.5;
+                        acc_w = acc_w + m[d].y * 0.5;
+                    }
+                }
+                if (TOPO == IMP3D && !(GP_ABLATE & ABL_NO_INLIST)) {
+                    const uint32_t e_b = L.off[jl], e_e = L.off[jl + 1];
+                    for (uint32_t e = e_b; e < e_e; ++e) {
+                        bool sent = false;
+                        double2 mi = make_double2(0.0, 0.0);
+                        if (staged) {
+                            const uint16_t p = L.pos[e - e_lo];
+                            sent = p != POS_NONE;
+                            if (p < (uint16_t)MSG_CAP) mi = L.msg[p];
+                            else if (p == POS_GLOBAL) mi = ld_sw(swc + L.src[e - e_lo]);
+                        } else {  // rare: tile in-degree above SRC_CAP
+                            const uint32_t i = in_src[e];
+                            if (all_active) {
+                                const uint32_t di = popc6(present_mask<IMP3D>(i, G)) + 1u;
+                                sent = uniform(a.k0, a.k1, S_PUSHSUM, i, r, di) == di - 1u;
+                            } else {
+                                sent = (rbc[i >> 6] >> (i & 63)) & 1ull;
+                            }
+                            if (sent) mi = ld_sw(swc + i);
+                        }
+                        if (sent) {
+                            acc_s = acc_s + mi.x * 0.5;
+                            acc_w = acc_w + mi.y * 0.5;
+                            recv = true;
+                        }
+                    }
+                }
+                uint32_t flags = b & (B_ACTIVE | B_CONV | (3u << CNT_SHIFT));
+                if (recv) {
+                    if (!(GP_ABLATE & ABL_NO_RATIO) && !(b & B_CONV)) {
+                        const double r_old = sv.x / sv.y;
+                        const double r_new = acc_s / acc_w;
+                        uint32_t cnt = (b >> CNT_SHIFT) & 3u;
+                        cnt = fabs(r_new - r_old) > 1e-10 ? 0u : cnt + 1u;
+                        flags = (flags & ~(3u << CNT_SHIFT)) | (cnt << CNT_SHIFT);
+                        if (cnt == 3) {
+                            flags |= B_CONV;
+                            ++alerts;
+                        }
+                    }
+                    if (!active) {
+                        ++newly;
+                        flags |= B_ACTIVE;
+                        active = true;
+                    }
+                }
+                if (active && deg > 0)
+                    dir = (GP_ABLATE & ABL_NO_NEXTDIR) ? (j % 7u) % (deg) : slot_to_dir(mask, uniform(a.k0, a.k1, S_PUSHSUM, j, r + 1, deg));
+                reinterpret_cast<uint8_t*>(L.out)[jl] = (uint8_t)(flags | dir);
+                swn[j] = make_double2(acc_s, acc_w);
+            }
+            if (TOPO == IMP3D) {
+                const unsigned long long bits = __ballot(valid && dir == DIR_RANDOM);
+                if (lane == 0) a.rbn[(j0 + k * TPB + (threadIdx.x & ~63u)) >> 6] = bits;
+            }
+        }
+        __syncthreads();
+        // node bytes out as words (allocations are padded past P)
+        for (uint32_t w = threadIdx.x; w < (uint32_t)(TILE / 4) && j0 + w * 4 < j1; w += TPB)
+            reinterpret_cast<uint32_t*>(a.nbn)[(j0 >> 2) + w] = L.out[w];
+        __syncthreads();
+    }
+    // block reduction of alerts / newly active
+    uint32_t x = alerts, y = newly;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        x += __shfl_xor(x, o, 64);
+        y += __shfl_xor(y, o, 64);
+    }
+    if (lane == 0) {
+        L.red[0][threadIdx.x >> 6] = x;
+        L.red[1][threadIdx.x >> 6] = y;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        x = 0;
+        y = 0;
+        for (int w = 0; w < TPB / 64; ++w) {
+            x += L.red[0][w];
+            y += L.red[1][w];
+        }
+        if (x) atomicAdd(&ctl->round_alerts, (unsigned long long)x);
+        if (y) atomicAdd(&ctl->round_active, (unsigned long long)y);
+    }
+}
+
+// ---------------------------------------------------------------- gossip
+// Deliveries to j = lattice senders pointing here + Imp3D random-edge senders
+// (bitmap) + the injector; all dropped if j was converged at round start.
+template <int TOPO>
+__global__ __launch_bounds__(TPB) void k_gossip_tile(RoundArgs a, uint32_t r) {
+    __shared__ TileLds L;
+    Ctl* ctl = a.ctl;
+    if (ld_agent(&ctl->done)) return;
+    const long long inj = ld_agent(&ctl->inj_target);
+    const Geom G = a.G;
+    const uint32_t P = G.P;
+    const uint32_t H = TOPO == LINE ? 1u : G.g;
+    uint32_t alerts = 0;
+    const int lane = threadIdx.x & 63;
+
+    for (TileWalk tw(a.ntiles); tw.t < tw.end; tw.t += tw.step) {
+        const uint32_t j0 = tw.t * TILE;
+        const uint32_t j1 = min(P, j0 + TILE);
+        int32_t c0[NPT];
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            const uint32_t j = j0 + k * TPB + threadIdx.x;
+            c0[k] = j < j1 ? a.c[j] : (int32_t)GOSSIP_DONE;
+        }
+        const uint32_t b_rows = stage_bytes(L.rows, a.nbc, (int64_t)j0 - H, (int64_t)j1 + H, P);
+        uint32_t b_xm = 0, b_xp = 0;
+        if (TOPO != LINE) {
+            b_xm = stage_bytes(L.xm, a.nbc, (int64_t)j0 - G.g2, (int64_t)j1 - G.g2, P);
+            b_xp = stage_bytes(L.xp, a.nbc, (int64_t)j0 + G.g2, (int64_t)j1 + G.g2, P);
+        }
+        if (TOPO == IMP3D)
+            for (uint32_t q = threadIdx.x; q <= j1 - j0; q += TPB) L.off[q] = a.in_off[j0 + q];
+        __syncthreads();
+        uint32_t e_lo = 0;
+        bool staged = true;
+        if (TOPO == IMP3D) {
+            e_lo = L.off[0];
+            const uint32_t cnt = L.off[j1 - j0] - e_lo;
+            staged = cnt <= (uint32_t)SRC_CAP;
+            if (staged) {
+                for (uint32_t q = threadIdx.x; q < cnt; q += TPB) {
+                    const uint32_t i = a.in_src[e_lo + q];
+                    reinterpret_cast<uint8_t*>(L.sent)[q] = (uint8_t)((a.rbc[i >> 6] >> (i & 63)) & 1ull);
+                }
+            }
+            __syncthreads();
+        }
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            const uint32_t jl = k * TPB + threadIdx.x;
+            const uint32_t j = j0 + jl;
+            const bool valid = j < j1;
+            uint32_t dir = DIR_NONE;
+            if (valid) {
+                const uint32_t mask = present_mask<TOPO>(j, G);
+                int32_t c1 = c0[k];
+                if (c1 < (int32_t)GOSSIP_DONE) {
+                    uint32_t inc = (long long)j == inj ? 1u : 0u;
+                    if (TOPO == LINE) {
+                        inc += (mask & 1u) && (lds_byte(L.rows, j - 1 - b_rows) & DIR_MASK) == 1u;
+                        inc += (mask & 2u) && (lds_byte(L.rows, j + 1 - b_rows) & DIR_MASK) == 0u;
+                    } else {
+                        inc += (mask & 1u) && (lds_byte(L.xm, j - G.g2 - b_xm) & DIR_MASK) == 1u;
+                        inc += (mask & 2u) && (lds_byte(L.xp, j + G.g2 - b_xp) & DIR_MASK) == 0u;
+                        inc += (mask & 4u) && (lds_byte(L.rows, j + G.g - b_rows) & DIR_MASK) == 3u;
+                        inc += (mask & 8u) && (lds_byte(L.rows, j - G.g - b_rows) & DIR_MASK) == 2u;
+                        inc += (mask & 16u) && (lds_byte(L.rows, j + 1 - b_rows) & DIR_MASK) == 5u;
+                        inc += (mask & 32u) && (lds_byte(L.rows, j - 1 - b_rows) & DIR_MASK) == 4u;
+                    }
+                    if (TOPO == IMP3D) {
+                        const uint32_t e_b = L.off[jl], e_e = L.off[jl + 1];
+                        if (staged) {
+                            for (uint32_t e = e_b; e < e_e; ++e) inc += lds_byte(L.sent, e - e_lo);
+                        } else {
+                            for (uint32_t e = e_b; e < e_e; ++e) {
+                                const uint32_t i = a.in_src[e];
+                                inc += (uint32_t)((a.rbc[i >> 6] >> (i & 63)) & 1ull);
+                            }
+                        }
+                    }
+                    if (inc) {
+                        c1 += (int32_t)inc;
+                        a.c[j] = c1;
+                        alerts += c1 > 10;  // the receipt that finds rumours == 10 (Program.fs:92-94)
+                    }
+                }
+                const bool active = ((j == a.seed_node) || c1 >= 1) && c1 <= 10;
+                if (active) {
+                    const uint32_t deg = popc6(mask) + (TOPO == IMP3D ? 1u : 0u);
+                    if (deg > 0) dir = slot_to_dir(mask, uniform(a.k0, a.k1, S_GOSSIP, j, r + 1, deg));
+                }
+                reinterpret_cast<uint8_t*>(L.out)[jl] = (uint8_t)dir;
+            }
+            if (TOPO == IMP3D) {
+                const unsigned long long bits = __ballot(valid && dir == DIR_RANDOM);
+                if (lane == 0) a.rbn[(j0 + k * TPB + (threadIdx.x & ~63u)) >> 6] = bits;
+            }
+        }
+        __syncthreads();
+        for (uint32_t w = threadIdx.x; w < (uint32_t)(TILE / 4) && j0 + w * 4 < j1; w += TPB)
+            reinterpret_cast<uint32_t*>(a.nbn)[(j0 >> 2) + w] = L.out[w];
+        __syncthreads();
+    }
+    uint32_t x = alerts;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+    if (lane == 0) L.red[0][threadIdx.x >> 6] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        x = 0;
+        for (int w = 0; w < TPB / 64; ++w) x += L.red[0][w];
+        if (x) atomicAdd(&ctl->round_alerts, (unsigned long long)x);
+    }
+}
+
+// Random-edge bits of round 0 (only the seed can be sending).
+__global__ __launch_bounds__(TPB) void k_rbits_init(const uint8_t* nb, uint64_t* rb, uint32_t P, uint32_t nwords) {
+    for (uint32_t jb = blockIdx.x * TPB; jb < nwords * 64u; jb += gridDim.x * TPB) {
+        const uint32_t j = jb + threadIdx.x;
+        const bool bit = j < P && (nb[j] & DIR_MASK) == DIR_RANDOM;
+        const unsigned long long bits = __ballot(bit);
+        if ((threadIdx.x & 63) == 0) rb[j >> 6] = bits;
+    }
+}
+
+uint32_t round_tiles(uint32_t P) { return (P + TILE - 1) / TILE; }
+// 64-bit words the ballot stores of one round touch (whole tiles) plus slack.
+uint32_t rbits_words_for(uint32_t P) { return round_tiles(P) * (TILE / 64) + 16u; }
+
+RoundArgs make_round_args(const DevState& S, uint32_t round) {
+    const int cur = round & 1;
+    RoundArgs a;
+    a.swc = S.sw[cur];
+    a.swn = S.sw[cur ^ 1];
+    a.nbc = S.nb[cur];
+    a.nbn = S.nb[cur ^ 1];
+    a.rbc = S.rbits[cur];
+    a.rbn = S.rbits[cur ^ 1];
+    a.in_off = S.in_off;
+    a.in_src = S.in_src;
+    a.c = S.c;
+    a.ctl = S.ctl;
+    a.G = S.G;
+    a.k0 = S.k0;
+    a.k1 = S.k1;
+    a.seed_node = S.seed_node;
+    a.ntiles = round_tiles(S.G.P);
+    return a;
+}
+
+hipError_t launch_round_tile(const DevState& S, uint32_t round, int grid, hipStream_t st) {
+    const RoundArgs a = make_round_args(S, round);
+    const dim3 g(grid), b(TPB);
+    if (S.alg == PUSHSUM) {
+        switch (S.topo) {
+            case LINE: hipLaunchKernelGGL(k_ps_tile<LINE>, g, b, 0, st, a, round); break;
+            case GRID3D: hipLaunchKernelGGL(k_ps_tile<GRID3D>, g, b, 0, st, a, round); break;
+            default: hipLaunchKernelGGL(k_ps_tile<IMP3D>, g, b, 0, st, a, round); break;
+        }
+    } else {
+        switch (S.topo) {
+            case LINE: hipLaunchKernelGGL(k_gossip_tile<LINE>, g, b, 0, st, a, round); break;
+            case GRID3D: hipLaunchKernelGGL(k_gossip_tile<GRID3D>, g, b, 0, st, a, round); break;
+            default: hipLaunchKernelGGL(k_gossip_tile<IMP3D>, g, b, 0, st, a, round); break;
+        }
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_rbits_init(const DevState& S, int grid, hipStream_t st) {
+    hipLaunchKernelGGL(k_rbits_init, dim3(grid), dim3(TPB), 0, st, S.nb[0], S.rbits[0], S.G.P, S.rbits_words);
+    return hipGetLastError();
+}
+
+}  // namespace gp

@@ -3,9 +3,10 @@
     python tools/ablate.py build            # CPU: compile variants into build/ablate/
     python tools/ablate.py run [n]           # GPU: time each variant (steady state from round 0)
 
-Each variant compiles gp_kernels.hip / gp_api.hip with -DGP_ABLATE=<mask>
-(switch meanings at the top of gp_kernels.hip); results are wrong by design,
-only the time per round matters.
+Each variant compiles gp_round.hip with -DGP_NPT=<n> -DGP_ABLATE=<mask>
+(switch meanings at the top of gp_round.hip); ablated results are wrong by
+design, only the steady-state time per round matters (the activation pre-roll
+uses the variant itself, so heavily ablated variants may activate slowly).
 """
 import os
 import subprocess
@@ -14,9 +15,13 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "gossipprotocol_amd", "csrc")
 OUT = os.path.join(ROOT, "build", "ablate")
+# name -> (GP_NPT, GP_ABLATE mask) for gp_round.hip (mask bits at the top of gp_round.hip)
 VARIANTS = {
-    "base": 1, "no_inlist": 1 | 2, "no_rgather": 1 | 4, "no_lattice": 1 | 8, "no_nextdir": 1 | 16,
-    "no_ratio": 1 | 32, "lattice_only": 1 | 2 | 16 | 32, "stream_only": 1 | 2 | 8 | 16 | 32,
+    "base_npt4": (4, 0), "npt2": (2, 0), "npt8": (8, 0),
+    "no_rgather": (4, 1), "no_lgather": (4, 2), "no_inlist": (4, 4), "no_nextdir": (4, 8),
+    "no_ephilox": (4, 16), "no_gathers": (4, 1 | 2), "stream_only": (4, 2 | 4 | 8),
+    "bitmap_only": (4, 32), "no_ratio": (4, 64),
+    "minb6": (4, 0, 6), "minb8": (4, 0, 8),
 }
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off"]
 
@@ -25,49 +30,60 @@ def build():
     os.makedirs(OUT, exist_ok=True)
     sort_obj = os.path.join(ROOT, "build", "obj", "gp_sort.o")
     procs = []
-    for name, mask in VARIANTS.items():
-        for src in ("gp_api", "gp_kernels"):
-            obj = os.path.join(OUT, f"{src}_{name}.o")
-            cmd = ["/opt/rocm/bin/hipcc", *FLAGS, f"-DGP_ABLATE={mask}", "-c", "-o", obj,
-                   os.path.join(CSRC, src + ".hip")]
-            procs.append(subprocess.Popen(cmd))
+    for name, v in VARIANTS.items():
+        npt, mask = v[0], v[1]
+        minb = v[2] if len(v) > 2 else 1
+        obj = os.path.join(OUT, f"gp_round_{name}.o")
+        cmd = ["/opt/rocm/bin/hipcc", *FLAGS, f"-DGP_NPT={npt}", f"-DGP_ABLATE={mask}", f"-DGP_MINB={minb}",
+               "-c", "-o", obj, os.path.join(CSRC, "gp_round.hip")]
+        procs.append(subprocess.Popen(cmd))
     for p in procs:
         assert p.wait() == 0
+    objdir = os.path.join(ROOT, "build", "obj")
     for name in VARIANTS:
         so = os.path.join(OUT, f"lib_{name}.so")
-        objs = [os.path.join(OUT, f"{src}_{name}.o") for src in ("gp_api", "gp_kernels")] + [sort_obj]
+        objs = [os.path.join(objdir, "gp_api.o"), os.path.join(objdir, "gp_kernels.o"),
+                os.path.join(OUT, f"gp_round_{name}.o"), sort_obj]
         subprocess.check_call(["/opt/rocm/bin/hipcc", *FLAGS, "-shared", "-o", so, *objs])
 
 
-def run(n):
+def run(n, only=None):
     import json
     res = {}
-    for name in VARIANTS:
-        so = os.path.join(OUT, f"lib_{name}.so")
+    for name in (only or VARIANTS):
+        so = os.path.join(OUT, f"lib_{name.split('@')[0]}.so")
         code = ("import sys,json; sys.path.insert(0,%r)\n"
                 "from gossipprotocol_amd import Simulation\n"
                 "s=Simulation(%d,'Imp3D','push-sum',kernel_timing=True)\n"
-                "s.step(3); s.sync(); s.kernel_stats(reset=True); s.step(10); s.sync()\n"
+                "P=s.population\n"
+                "pre=0\nwhile s.info().active < P and pre < 300: pre += len(s.step(8))\n"
+                "s.sync(); s.kernel_stats(reset=True); s.step(10); s.sync()\n"
                 "ms,k,_=s.kernel_stats(); print(json.dumps(ms/k))\n") % (ROOT, n)
-        env = dict(os.environ, GOSSIP_HIP_LIB_EXPERIMENT=so)
+        env = dict(os.environ, GOSSIP_HIP_LIB_EXPERIMENT=so, GP_GRID=os.environ.get("GP_GRID", "8192"))
+        if "@" in name:
+            name, grid = name.split("@")
+            so = os.path.join(OUT, f"lib_{name}.so")
+            env.update(GOSSIP_HIP_LIB_EXPERIMENT=so, GP_GRID=grid)
         out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
         if out.returncode:
             print(name, "FAILED", out.stderr[-500:], flush=True)
-            break
+            sys.exit(1)
         res[name] = float(out.stdout.strip().splitlines()[-1])
         print(f"{name:14s} {res[name]:8.2f} ms/round", flush=True)
-    for grid in (1024, 4096, 16384, 65536, (n + 255) // 256):
-        so = os.path.join(OUT, "lib_base.so")
+    for grid in ((1536, 3072, 8192, 16384, 65536) if not only else ()):
+        so = os.path.join(OUT, "lib_base_npt4.so")
         code = ("import sys,json; sys.path.insert(0,%r)\n"
                 "from gossipprotocol_amd import Simulation\n"
                 "s=Simulation(%d,'Imp3D','push-sum',kernel_timing=True)\n"
-                "s.step(3); s.sync(); s.kernel_stats(reset=True); s.step(10); s.sync()\n"
+                "P=s.population\n"
+                "pre=0\nwhile s.info().active < P and pre < 300: pre += len(s.step(8))\n"
+                "s.sync(); s.kernel_stats(reset=True); s.step(10); s.sync()\n"
                 "ms,k,_=s.kernel_stats(); print(json.dumps(ms/k))\n") % (ROOT, n)
         env = dict(os.environ, GOSSIP_HIP_LIB_EXPERIMENT=so, GP_GRID=str(grid))
         out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
         if out.returncode:
             print("grid", grid, "FAILED", out.stderr[-500:], flush=True)
-            break
+            sys.exit(1)
         print(f"base grid={grid:<9d} {float(out.stdout.strip().splitlines()[-1]):8.2f} ms/round", flush=True)
     return res
 
@@ -76,4 +92,4 @@ if __name__ == "__main__":
     if sys.argv[1] == "build":
         build()
     else:
-        run(int(sys.argv[2]) if len(sys.argv) > 2 else 10**9)
+        run(int(sys.argv[2]) if len(sys.argv) > 2 else 10**9, sys.argv[3].split(",") if len(sys.argv) > 3 else None)
