@@ -288,8 +288,35 @@ int gp_create(const gp_config* cfg, gp_sim** out) {
     // 64 workgroups per CU: measured best for the tiled round kernels (tools/ablate.py:
     // 2048 -> 27.5, 8192 -> 22.1, 16384 -> 21.2 ms/round at P = 1e9)
     int64_t cap = (int64_t)prop.multiProcessorCount * 64;
+    // round-kernel variant: column march for lattices with enough patches to fill
+    // the chip, the chunk kernel otherwise (line, small g); GP_KERNEL overrides
+    // (measured, profiles/r01: push-sum -> tiled; gossip on a large lattice -> column march)
+    int kernel = KERNEL_TILE;
+    const bool lattice = cfg->topology == GP_3D || cfg->topology == GP_IMP3D;
+    if (lattice && cfg->algorithm == GP_GOSSIP && g >= 200) kernel = KERNEL_COL;
+    if (const char* e = std::getenv("GP_KERNEL")) {
+        if (!std::strcmp(e, "tile")) kernel = KERNEL_TILE;
+        else if (!std::strcmp(e, "wave")) kernel = KERNEL_WAVE;
+        else if (!std::strcmp(e, "col") && lattice) kernel = KERNEL_COL;
+    }
+    uint32_t col_xsegs = 1;
+    if (cfg->topology != GP_FULL && kernel != KERNEL_TILE) {
+        // exactly the resident grid (a persistent sweep), a multiple of the 8 XCDs
+        const int bpc = kernel == KERNEL_COL ? col_blocks_per_cu(cfg->topology, cfg->algorithm)
+                                             : wave_blocks_per_cu(cfg->topology, cfg->algorithm);
+        cap = (int64_t)prop.multiProcessorCount * bpc;
+        if (kernel == KERNEL_COL) {
+            // x segments per patch: enough work items for every resident wave, >= 16 planes each
+            const int64_t patches = ((g + 63) / 64) * ((g + 3) / 4);
+            const int64_t waves = cap * (BULK_THREADS / 64);
+            int64_t xs = std::max<int64_t>(1, waves / std::max<int64_t>(1, patches));
+            xs = std::min<int64_t>(xs, std::max<int64_t>(1, g / 16));
+            col_xsegs = (uint32_t)xs;
+        }
+    }
     if (const char* e = std::getenv("GP_GRID")) cap = std::max<int64_t>(1, std::atoll(e));
-    s->grid = (int)std::max<int64_t>(1, std::min(blocks, cap));
+    if (const char* e = std::getenv("GP_XSEGS")) col_xsegs = (uint32_t)std::max(1, std::atoi(e));
+    s->grid = (int)std::max<int64_t>(1, std::min(kernel == KERNEL_COL ? cap : blocks, cap));
 
     DevState& S = s->S;
     S.topo = cfg->topology;
@@ -300,6 +327,15 @@ int gp_create(const gp_config* cfg, gp_sim** out) {
     S.G.g2 = (uint32_t)(g * g);
     S.G.div_g = make_fastdiv(S.G.g ? S.G.g : 1);
     S.G.div_g2 = make_fastdiv(S.G.g2 ? S.G.g2 : 1);
+    S.lo = 0;
+    S.nloc = (uint32_t)P;
+    S.base = 0;
+    S.rtag = nullptr;
+    S.rmsg = nullptr;
+    S.kernel = kernel;
+    S.col_xsegs = col_xsegs;
+    S.tile_walk = 0;
+    if (const char* e = std::getenv("GP_WALK")) S.tile_walk = (uint32_t)std::atoi(e);
     S.k0 = (uint32_t)cfg->seed;
     S.k1 = (uint32_t)(cfg->seed >> 32);
     // choice = Random().Next(0, nodes) (Program.fs:193,221,263)
@@ -345,7 +381,7 @@ int gp_create(const gp_config* cfg, gp_sim** out) {
         if ((rc = dev_alloc(s, &S.sort_tmp, tb))) return fail(rc);
     }
     if (S.topo == IMP3D) {
-        S.rbits_words = rbits_words_for(S.G.P);
+        S.rbits_words = S.kernel == KERNEL_COL ? col_rbits_words(S.nloc / S.G.g2, S.G.g) : rbits_words_for(S.G.P);
         if ((rc = dev_alloc_t(s, &S.rbits[0], S.rbits_words)) || (rc = dev_alloc_t(s, &S.rbits[1], S.rbits_words)))
             return fail(rc);
         if ((rc = build_imp3d(s))) return fail(rc);
@@ -364,7 +400,8 @@ int gp_create(const gp_config* cfg, gp_sim** out) {
         set_err("init launch failed");
         return fail(GP_EHIP);
     }
-    if (S.topo == IMP3D && launch_rbits_init(S, s->grid, s->stream) != hipSuccess) {
+    if (S.topo == IMP3D && (S.kernel == KERNEL_COL ? launch_col_rbits_init(S, s->stream)
+                                                   : launch_rbits_init(S, s->grid, s->stream)) != hipSuccess) {
         set_err("random-edge bitmap init failed");
         return fail(GP_EHIP);
     }

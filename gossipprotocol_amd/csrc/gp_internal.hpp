@@ -61,6 +61,18 @@ struct DevState {
     void* sort_tmp;
     size_t sort_tmp_bytes;
     uint32_t key_bits;
+    // slab of this rank (single GPU: lo = 0, nloc = P, base = 0): node ids
+    // [lo, lo + nloc) are owned; per-node arrays (sw, nb) start at id `base`
+    // (= lo - halo); c, in_off and rbits are indexed from lo
+    uint32_t lo, nloc, base;
+    // Imp3D random edges from senders on other ranks, per local in-edge:
+    // round tag (the round the message was delivered for) and the message
+    uint32_t* rtag;
+    double2* rmsg;
+    int kernel;  // KERNEL_* below
+    // column kernels: x segments per patch (set at create from the resident grid)
+    uint32_t col_xsegs;
+    uint32_t tile_walk;  // RoundArgs::walk
 };
 
 // Arguments of the tiled round kernels (gp_round.hip): only what they read.
@@ -77,7 +89,45 @@ struct RoundArgs {
     Ctl* ctl;
     Geom G;
     uint32_t k0, k1, seed_node, ntiles;
+    uint32_t walk;  // 0: XCD-contiguous eighths, 1: one global sweep (tile t -> block t % grid)
 };
+
+enum KernelVariant : int { KERNEL_WAVE = 0, KERNEL_TILE = 1, KERNEL_COL = 2 };
+
+// Arguments of the wave-autonomous round kernels (gp_wave.hip, gp_col.hip).
+struct WaveArgs {
+    const double2* swc;
+    double2* swn;
+    const uint8_t* nbc;
+    uint8_t* nbn;
+    const uint64_t* rbc;
+    uint64_t* rbn;
+    const uint32_t* in_off;
+    const uint32_t* in_src;
+    const uint32_t* rtag;
+    const double2* rmsg;
+    int32_t* c;
+    Ctl* ctl;
+    Geom G;
+    uint32_t k0, k1, seed_node;
+    uint32_t lo, nloc, base, nchunks;
+    // column kernels (gp_col.hip): planes [x_lo, x_hi) of this rank, patches of
+    // 64 z x 4 y rows, x split into segments of xs_len planes
+    uint32_t x_lo, x_hi, zsegs, yblocks, xs_len, nitems;
+};
+
+// ---- wave-autonomous round kernels (gp_wave.hip)
+uint32_t wave_chunks(uint32_t nloc);
+int wave_blocks_per_cu(int topo, int alg);
+hipError_t launch_round_wave(const WaveArgs& a, int topo, int alg, uint32_t round, int grid, hipStream_t st);
+WaveArgs make_wave_args(const DevState& S, uint32_t round);
+
+// ---- column-march round kernels (gp_col.hip): 3D / Imp3D
+hipError_t launch_round_col(const WaveArgs& a, int topo, int alg, uint32_t round, int grid, hipStream_t st);
+int col_blocks_per_cu(int topo, int alg);
+// random-edge bitmap words of the column layout (one 64-bit word per 64-node row segment)
+uint32_t col_rbits_words(uint32_t planes, uint32_t g);
+hipError_t launch_col_rbits_init(const DevState& S, hipStream_t st);
 
 // ---- tiled round kernels (gp_round.hip)
 uint32_t round_tiles(uint32_t P);

@@ -414,7 +414,11 @@ hipError_t launch_histogram(const uint32_t* keys, uint32_t n, uint32_t* counts, 
 
 hipError_t launch_bulk(const DevState& S, uint32_t round, int grid, hipStream_t st) {
     const dim3 g(grid), b(BULK_THREADS);
-    if (S.topo != FULL) return launch_round_tile(S, round, grid, st);
+    if (S.topo != FULL) {
+        if (S.kernel == KERNEL_TILE) return launch_round_tile(S, round, grid, st);
+        if (S.kernel == KERNEL_COL) return launch_round_col(make_wave_args(S, round), S.topo, S.alg, round, grid, st);
+        return launch_round_wave(make_wave_args(S, round), S.topo, S.alg, round, grid, st);
+    }
     if (S.alg == PUSHSUM) {
         hipLaunchKernelGGL(k_full_ps_recv, g, b, 0, st, S, round);
     } else {
@@ -425,11 +429,20 @@ hipError_t launch_bulk(const DevState& S, uint32_t round, int grid, hipStream_t 
 }
 
 const char* bulk_kernel_name(const DevState& S) {
-    static const char* ps[] = {"k_ps_tile<LINE>", "k_full_ps_send+sort+mark+recv", "k_ps_tile<GRID3D>",
-                               "k_ps_tile<IMP3D>"};
-    static const char* go[] = {"k_gossip_tile<LINE>", "k_full_gossip_send+recv", "k_gossip_tile<GRID3D>",
-                               "k_gossip_tile<IMP3D>"};
-    return S.alg == PUSHSUM ? ps[S.topo] : go[S.topo];
+    static const char* ps[3][4] = {{"k_ps_wave<LINE>", "k_full_ps_send+sort+mark+recv", "k_ps_wave<GRID3D>",
+                                    "k_ps_wave<IMP3D>"},
+                                   {"k_ps_tile<LINE>", "k_full_ps_send+sort+mark+recv", "k_ps_tile<GRID3D>",
+                                    "k_ps_tile<IMP3D>"},
+                                   {"k_ps_wave<LINE>", "k_full_ps_send+sort+mark+recv", "k_ps_col<GRID3D>",
+                                    "k_ps_col<IMP3D>"}};
+    static const char* go[3][4] = {{"k_gossip_wave<LINE>", "k_full_gossip_send+recv", "k_gossip_wave<GRID3D>",
+                                    "k_gossip_wave<IMP3D>"},
+                                   {"k_gossip_tile<LINE>", "k_full_gossip_send+recv", "k_gossip_tile<GRID3D>",
+                                    "k_gossip_tile<IMP3D>"},
+                                   {"k_gossip_wave<LINE>", "k_full_gossip_send+recv", "k_gossip_col<GRID3D>",
+                                    "k_gossip_col<IMP3D>"}};
+    const int v = S.kernel;
+    return S.alg == PUSHSUM ? ps[v][S.topo] : go[v][S.topo];
 }
 
 hipError_t launch_finalize(const DevState& S, uint32_t round_done, uint32_t round_next, hipStream_t st) {

@@ -63,7 +63,6 @@ struct TileLds {
     uint32_t sent[SRC_CAP / 4];  // gossip: byte per staged in-edge, sender used its random edge
     uint16_t pos[SRC_CAP];     // push-sum: slot of the edge's parked message (POS_NONE: not sent)
     double2 msg[MSG_CAP];      // push-sum: random-edge messages gathered by the flattened pass
-    uint32_t nmsg;
     uint32_t out[TILE / 4];    // next-round node bytes, stored as words
     uint32_t red[2][TPB / 64];
 };
@@ -94,9 +93,9 @@ __device__ __forceinline__ T ld_agent(const T* p) {
 // eighth of the tiles (speed only -- any placement is correct).
 struct TileWalk {
     uint32_t t, end, step;
-    __device__ TileWalk(uint32_t ntiles) {
+    __device__ TileWalk(uint32_t ntiles, uint32_t walk) {
         const uint32_t G = gridDim.x;
-        if (G >= 8 && (G & 7) == 0) {
+        if (walk == 0 && G >= 8 && (G & 7) == 0) {
             const uint32_t x = blockIdx.x & 7, k = blockIdx.x >> 3;
             const uint32_t lo = (uint32_t)((uint64_t)ntiles * x / 8);
             end = (uint32_t)((uint64_t)ntiles * (x + 1) / 8);
@@ -131,9 +130,16 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
     uint32_t alerts = 0, newly = 0;
     const int lane = threadIdx.x & 63;
 
-    for (TileWalk tw(a.ntiles); tw.t < tw.end; tw.t += tw.step) {
+    for (TileWalk tw(a.ntiles, a.walk); tw.t < tw.end; tw.t += tw.step) {
         const uint32_t j0 = tw.t * TILE;
         const uint32_t j1 = min(P, j0 + TILE);
+        // the tile's in-edge range first (two uniform loads), so the senders can be
+        // staged in the same phase as everything else
+        uint32_t e_lo = 0, e_hi = 0;
+        if (TOPO == IMP3D) {
+            e_lo = a.in_off[j0];
+            e_hi = a.in_off[j1];
+        }
         // own (s, w): issue first, consumed after staging
         double2 own[NPT];
 #pragma unroll
@@ -147,48 +153,68 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
             b_xm = stage_bytes(L.xm, a.nbc, (int64_t)j0 - G.g2, (int64_t)j1 - G.g2, P);
             b_xp = stage_bytes(L.xp, a.nbc, (int64_t)j0 + G.g2, (int64_t)j1 + G.g2, P);
         }
-        if (TOPO == IMP3D)
-            for (uint32_t q = threadIdx.x; q <= j1 - j0; q += TPB) L.off[q] = a.in_off[j0 + q];
-        __syncthreads();
-        uint32_t e_lo = 0;
-        bool staged = true;
+        const uint32_t cnt = e_hi - e_lo;
+        const bool staged = cnt <= (uint32_t)SRC_CAP;
         if (TOPO == IMP3D) {
-            e_lo = L.off[0];
-            const uint32_t cnt = L.off[j1 - j0] - e_lo;
-            staged = cnt <= (uint32_t)SRC_CAP;
-            if (threadIdx.x == 0) L.nmsg = 0;
+            for (uint32_t q = threadIdx.x; q <= j1 - j0; q += TPB) L.off[q] = a.in_off[j0 + q];
             if (staged)
                 for (uint32_t q = threadIdx.x; q < cnt; q += TPB) L.src[q] = in_src[e_lo + q];
-            __syncthreads();
+        }
+        __syncthreads();
+        if (TOPO == IMP3D) {
             if (staged) {
                 // Flattened, lane-balanced pass over the tile's in-edges: decide
                 // whether each sender used its random edge and gather its (s, w)
                 // into a compact LDS buffer, so the per-receiver loop below
                 // neither runs a wave's max in-degree of Philox draws nor waits
-                // on a random HBM read.  The LDS slot order is irrelevant: the
-                // fold walks edges in canonical (ascending sender) order.
-                for (uint32_t q = threadIdx.x; q < cnt; q += TPB) {
-                    const uint32_t i = L.src[q];
-                    bool sent;
-                    if (GP_ABLATE & ABL_NO_EPHILOX) {
-                        sent = false;
-                    } else if (all_active && !(GP_ABLATE & ABL_BITMAP_ONLY)) {
-                        const uint32_t di = popc6(present_mask<IMP3D>(i, G)) + 1u;
-                        sent = uniform(a.k0, a.k1, S_PUSHSUM, i, r, di) == di - 1u;
-                    } else {
-                        sent = (rbc[i >> 6] >> (i & 63)) & 1ull;
-                    }
-                    uint16_t p = POS_NONE;
-                    if (sent) {
-                        const uint32_t slot = atomicAdd(&L.nmsg, 1u);
-                        if (slot < (uint32_t)MSG_CAP) {
-                            L.msg[slot] = (GP_ABLATE & ABL_NO_RGATHER) ? make_double2((double)i, 1.0) : ld_sw(swc + i);
-                            p = (uint16_t)slot;
+                // on a random HBM read.  All FU decisions of a thread are
+                // independent (ILP across the Philox chains), then all gathers
+                // are issued together; slots come from a per-wave ballot prefix
+                // into the wave's own quarter of the buffer.  The slot order is
+                // irrelevant: the fold walks edges in canonical order.
+                constexpr int FU = SRC_CAP / TPB;
+                constexpr uint32_t WCAP = MSG_CAP / (TPB / 64);
+                uint32_t isrc[FU];
+                bool snt[FU];
+#pragma unroll
+                for (int m = 0; m < FU; ++m) {
+                    const uint32_t q = threadIdx.x + m * TPB;
+                    isrc[m] = q < cnt ? L.src[q] : 0u;
+                }
+#pragma unroll
+                for (int m = 0; m < FU; ++m) {
+                    const uint32_t q = threadIdx.x + m * TPB;
+                    const uint32_t i = isrc[m];
+                    bool sent = false;
+                    if (q < cnt) {
+                        if (GP_ABLATE & ABL_NO_EPHILOX) {
+                            sent = false;
+                        } else if (all_active && !(GP_ABLATE & ABL_BITMAP_ONLY)) {
+                            const uint32_t di = popc6(present_mask<IMP3D>(i, G)) + 1u;
+                            sent = uniform(a.k0, a.k1, S_PUSHSUM, i, r, di) == di - 1u;
                         } else {
-                            p = POS_GLOBAL;
+                            sent = (rbc[i >> 6] >> (i & 63)) & 1ull;
                         }
                     }
-                    L.pos[q] = p;
+                    snt[m] = sent;
+                }
+                double2 v[FU];
+#pragma unroll
+                for (int m = 0; m < FU; ++m) {
+                    v[m] = make_double2(0.0, 0.0);
+                    if (snt[m]) v[m] = (GP_ABLATE & ABL_NO_RGATHER) ? make_double2((double)isrc[m], 1.0) : ld_sw(swc + isrc[m]);
+                }
+                const uint32_t wbase = (threadIdx.x >> 6) * WCAP;
+                uint32_t wn = 0;
+#pragma unroll
+                for (int m = 0; m < FU; ++m) {
+                    const uint32_t q = threadIdx.x + m * TPB;
+                    const unsigned long long bal = __ballot(snt[m]);
+                    const uint32_t slot = wn + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                    wn += (uint32_t)__popcll(bal);
+                    if (q < cnt) L.pos[q] = !snt[m] ? POS_NONE : (slot < WCAP ? (uint16_t)(wbase + slot) : POS_GLOBAL);
+                    if (snt[m] && slot < WCAP) L.msg[wbase + slot] = v[m];
                 }
             }
             __syncthreads();
@@ -337,9 +363,14 @@ __global__ __launch_bounds__(TPB) void k_gossip_tile(RoundArgs a, uint32_t r) {
     uint32_t alerts = 0;
     const int lane = threadIdx.x & 63;
 
-    for (TileWalk tw(a.ntiles); tw.t < tw.end; tw.t += tw.step) {
+    for (TileWalk tw(a.ntiles, a.walk); tw.t < tw.end; tw.t += tw.step) {
         const uint32_t j0 = tw.t * TILE;
         const uint32_t j1 = min(P, j0 + TILE);
+        uint32_t e_lo = 0, e_hi = 0;
+        if (TOPO == IMP3D) {
+            e_lo = a.in_off[j0];
+            e_hi = a.in_off[j1];
+        }
         int32_t c0[NPT];
 #pragma unroll
         for (int k = 0; k < NPT; ++k) {
@@ -352,23 +383,33 @@ __global__ __launch_bounds__(TPB) void k_gossip_tile(RoundArgs a, uint32_t r) {
             b_xm = stage_bytes(L.xm, a.nbc, (int64_t)j0 - G.g2, (int64_t)j1 - G.g2, P);
             b_xp = stage_bytes(L.xp, a.nbc, (int64_t)j0 + G.g2, (int64_t)j1 + G.g2, P);
         }
-        if (TOPO == IMP3D)
-            for (uint32_t q = threadIdx.x; q <= j1 - j0; q += TPB) L.off[q] = a.in_off[j0 + q];
-        __syncthreads();
-        uint32_t e_lo = 0;
-        bool staged = true;
+        const uint32_t cnt = e_hi - e_lo;
+        const bool staged = cnt <= (uint32_t)SRC_CAP;
         if (TOPO == IMP3D) {
-            e_lo = L.off[0];
-            const uint32_t cnt = L.off[j1 - j0] - e_lo;
-            staged = cnt <= (uint32_t)SRC_CAP;
+            for (uint32_t q = threadIdx.x; q <= j1 - j0; q += TPB) L.off[q] = a.in_off[j0 + q];
             if (staged) {
-                for (uint32_t q = threadIdx.x; q < cnt; q += TPB) {
-                    const uint32_t i = a.in_src[e_lo + q];
-                    reinterpret_cast<uint8_t*>(L.sent)[q] = (uint8_t)((a.rbc[i >> 6] >> (i & 63)) & 1ull);
+                // all sender loads, then all bitmap loads, in flight together
+                constexpr int FU = SRC_CAP / TPB;
+                uint32_t isrc[FU];
+#pragma unroll
+                for (int m = 0; m < FU; ++m) {
+                    const uint32_t q = threadIdx.x + m * TPB;
+                    isrc[m] = q < cnt ? a.in_src[e_lo + q] : 0u;
+                }
+                unsigned long long wv[FU];
+#pragma unroll
+                for (int m = 0; m < FU; ++m) {
+                    const uint32_t q = threadIdx.x + m * TPB;
+                    wv[m] = q < cnt ? a.rbc[isrc[m] >> 6] : 0ull;
+                }
+#pragma unroll
+                for (int m = 0; m < FU; ++m) {
+                    const uint32_t q = threadIdx.x + m * TPB;
+                    if (q < cnt) reinterpret_cast<uint8_t*>(L.sent)[q] = (uint8_t)((wv[m] >> (isrc[m] & 63)) & 1ull);
                 }
             }
-            __syncthreads();
         }
+        __syncthreads();
 #pragma unroll
         for (int k = 0; k < NPT; ++k) {
             const uint32_t jl = k * TPB + threadIdx.x;
@@ -469,6 +510,7 @@ RoundArgs make_round_args(const DevState& S, uint32_t round) {
     a.k1 = S.k1;
     a.seed_node = S.seed_node;
     a.ntiles = round_tiles(S.G.P);
+    a.walk = S.tile_walk;
     return a;
 }
 

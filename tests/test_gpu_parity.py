@@ -161,3 +161,32 @@ def test_full_size_imp3d_pushsum_1e9_properties():
     sim2.step(40)
     assert hashlib.sha256(sim2.state(0, chunk)["s"].tobytes()).hexdigest() == h.hexdigest()
     sim2.close()
+
+
+KERNEL_CASES = [  # (num_nodes, topology, algorithm, seed, rounds, checkpoint, x-segments)
+    (64000, "Imp3D", "push-sum", 5, 400, 97, "3"),
+    (125000, "Imp3D", "gossip", 7, 300, 101, "2"),
+    (216000, "3D", "push-sum", 9, 200, 75, "1"),
+    (27000, "3D", "gossip", 4, 600, 150, "4"),
+    (343000, "Imp3D", "push-sum", 11, 120, 60, "1"),
+]
+
+
+@pytest.mark.parametrize("kernel", ["wave", "col", "tile"])
+@pytest.mark.parametrize("n,topo,alg,seed,rounds,chk,xsegs", KERNEL_CASES, ids=lambda v: str(v))
+def test_kernel_variant_parity(kernel, n, topo, alg, seed, rounds, chk, xsegs, monkeypatch):
+    """Every round-kernel variant (chunk / column march / tiled) bit-exact vs the oracle,
+    the column march also with its x-segmentation forced."""
+    monkeypatch.setenv("GP_KERNEL", kernel)
+    monkeypatch.setenv("GP_XSEGS", xsegs)
+    sim, orc = Sim(n, topo, alg, seed=seed), Oracle(n, topo, alg, seed)
+    done = 0
+    while done < rounds:
+        k = min(chk, rounds - done)
+        ga, oa = sim.step(k), orc.step(k)
+        assert ga == oa, f"alerts differ in rounds {done}..{done + k}"
+        assert_same_state(alg, sim.state(), orc.state())
+        done += k
+        if len(ga) < k:
+            break
+    sim.close()
