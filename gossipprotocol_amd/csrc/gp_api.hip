@@ -330,6 +330,8 @@ int gp_create(const gp_config* cfg, gp_sim** out) {
     S.lo = 0;
     S.nloc = (uint32_t)P;
     S.base = 0;
+    S.ext_lo = 0;
+    S.ext_hi = (uint32_t)P;
     S.rtag = nullptr;
     S.rmsg = nullptr;
     S.kernel = kernel;
@@ -381,7 +383,7 @@ int gp_create(const gp_config* cfg, gp_sim** out) {
         if ((rc = dev_alloc(s, &S.sort_tmp, tb))) return fail(rc);
     }
     if (S.topo == IMP3D) {
-        S.rbits_words = S.kernel == KERNEL_COL ? col_rbits_words(S.nloc / S.G.g2, S.G.g) : rbits_words_for(S.G.P);
+        S.rbits_words = S.kernel == KERNEL_COL ? col_rbits_words(S.nloc / S.G.g2, S.G.g) : rbits_words_for(S.lo, S.nloc);
         if ((rc = dev_alloc_t(s, &S.rbits[0], S.rbits_words)) || (rc = dev_alloc_t(s, &S.rbits[1], S.rbits_words)))
             return fail(rc);
         if ((rc = build_imp3d(s))) return fail(rc);

@@ -65,6 +65,7 @@ struct DevState {
     // [lo, lo + nloc) are owned; per-node arrays (sw, nb) start at id `base`
     // (= lo - halo); c, in_off and rbits are indexed from lo
     uint32_t lo, nloc, base;
+    uint32_t ext_lo, ext_hi;  // ids the node arrays hold: [lo - halo, lo + nloc + halo) within [0, P)
     // Imp3D random edges from senders on other ranks, per local in-edge:
     // round tag (the round the message was delivered for) and the message
     uint32_t* rtag;
@@ -83,12 +84,15 @@ struct RoundArgs {
     uint8_t* nbn;
     const uint64_t* rbc;
     uint64_t* rbn;
-    const uint32_t* in_off;
+    const uint32_t* in_off;  // indexed by global id
     const uint32_t* in_src;
-    int32_t* c;
+    const uint32_t* rtag;    // per local in-edge: round of the delivered remote message
+    const double2* rmsg;
+    int32_t* c;              // indexed by global id
     Ctl* ctl;
     Geom G;
     uint32_t k0, k1, seed_node, ntiles;
+    uint32_t lo, nloc, ext_lo, ext_hi;  // owned ids [lo, lo + nloc); arrays hold [ext_lo, ext_hi)
     uint32_t walk;  // 0: XCD-contiguous eighths, 1: one global sweep (tile t -> block t % grid)
 };
 
@@ -117,7 +121,7 @@ struct WaveArgs {
 };
 
 // ---- wave-autonomous round kernels (gp_wave.hip)
-uint32_t wave_chunks(uint32_t nloc);
+uint32_t wave_chunks(uint32_t lo, uint32_t nloc);
 int wave_blocks_per_cu(int topo, int alg);
 hipError_t launch_round_wave(const WaveArgs& a, int topo, int alg, uint32_t round, int grid, hipStream_t st);
 WaveArgs make_wave_args(const DevState& S, uint32_t round);
@@ -131,7 +135,7 @@ hipError_t launch_col_rbits_init(const DevState& S, hipStream_t st);
 
 // ---- tiled round kernels (gp_round.hip)
 uint32_t round_tiles(uint32_t P);
-uint32_t rbits_words_for(uint32_t P);
+uint32_t rbits_words_for(uint32_t lo, uint32_t nloc);
 hipError_t launch_round_tile(const DevState& S, uint32_t round, int grid, hipStream_t st);
 hipError_t launch_rbits_init(const DevState& S, int grid, hipStream_t st);
 

@@ -71,12 +71,14 @@ __device__ __forceinline__ uint32_t lds_byte(const uint32_t* w, uint32_t idx) {
     return reinterpret_cast<const uint8_t*>(w)[idx];
 }
 
-// Copy the bytes of nb[lo, hi) (clamped to [0, P)) into LDS words; returns the
-// node id of LDS byte 0.  Reads at most 3 bytes past hi (allocations are padded).
+// Copy the bytes of nb[lo, hi) (clamped to the ids [ext_lo, ext_hi) the slab's
+// arrays hold, halos included) into LDS words; returns the node id of LDS byte
+// 0.  `nb` is indexed by global id; reads at most 3 bytes either side of the
+// range (allocations are padded and start 4-aligned).
 __device__ __forceinline__ uint32_t stage_bytes(uint32_t* lds, const uint8_t* nb, int64_t lo, int64_t hi,
-                                                uint32_t P) {
-    if (lo < 0) lo = 0;
-    if (hi > (int64_t)P) hi = P;
+                                                uint32_t ext_lo, uint32_t ext_hi) {
+    if (lo < (int64_t)ext_lo) lo = ext_lo;
+    if (hi > (int64_t)ext_hi) hi = ext_hi;
     const uint32_t ws = (uint32_t)lo & ~3u;
     const int nw = hi > lo ? (int)(((uint32_t)hi + 3u - ws) >> 2) : 0;
     const uint32_t* src = reinterpret_cast<const uint32_t*>(nb + ws);
@@ -125,14 +127,16 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
     const uint64_t* __restrict__ rbc = a.rbc;
     const uint32_t* __restrict__ in_src = a.in_src;
     const Geom G = a.G;
-    const uint32_t P = G.P;
     const uint32_t H = TOPO == LINE ? 1u : G.g;
     uint32_t alerts = 0, newly = 0;
     const int lane = threadIdx.x & 63;
 
     for (TileWalk tw(a.ntiles, a.walk); tw.t < tw.end; tw.t += tw.step) {
-        const uint32_t j0 = tw.t * TILE;
-        const uint32_t j1 = min(P, j0 + TILE);
+        // tiles sit on global multiples of TILE (4-aligned word I/O, 64-aligned
+        // ballot words); the slab's first and last tile may be partial
+        const uint32_t T = (a.lo / TILE + tw.t) * TILE;
+        const uint32_t j0 = max(a.lo, T);
+        const uint32_t j1 = min(a.lo + a.nloc, T + TILE);
         // the tile's in-edge range first (two uniform loads), so the senders can be
         // staged in the same phase as everything else
         uint32_t e_lo = 0, e_hi = 0;
@@ -144,19 +148,19 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
         double2 own[NPT];
 #pragma unroll
         for (int k = 0; k < NPT; ++k) {
-            const uint32_t j = j0 + k * TPB + threadIdx.x;
-            own[k] = j < j1 ? swc[j] : make_double2(0.0, 1.0);
+            const uint32_t j = T + k * TPB + threadIdx.x;
+            own[k] = (j >= j0 && j < j1) ? swc[j] : make_double2(0.0, 1.0);
         }
-        const uint32_t b_rows = stage_bytes(L.rows, a.nbc, (int64_t)j0 - H, (int64_t)j1 + H, P);
+        const uint32_t b_rows = stage_bytes(L.rows, a.nbc, (int64_t)j0 - H, (int64_t)j1 + H, a.ext_lo, a.ext_hi);
         uint32_t b_xm = 0, b_xp = 0;
         if (TOPO != LINE) {
-            b_xm = stage_bytes(L.xm, a.nbc, (int64_t)j0 - G.g2, (int64_t)j1 - G.g2, P);
-            b_xp = stage_bytes(L.xp, a.nbc, (int64_t)j0 + G.g2, (int64_t)j1 + G.g2, P);
+            b_xm = stage_bytes(L.xm, a.nbc, (int64_t)j0 - G.g2, (int64_t)j1 - G.g2, a.ext_lo, a.ext_hi);
+            b_xp = stage_bytes(L.xp, a.nbc, (int64_t)j0 + G.g2, (int64_t)j1 + G.g2, a.ext_lo, a.ext_hi);
         }
         const uint32_t cnt = e_hi - e_lo;
         const bool staged = cnt <= (uint32_t)SRC_CAP;
         if (TOPO == IMP3D) {
-            for (uint32_t q = threadIdx.x; q <= j1 - j0; q += TPB) L.off[q] = a.in_off[j0 + q];
+            for (uint32_t q = j0 - T + threadIdx.x; q <= j1 - T; q += TPB) L.off[q] = a.in_off[T + q];
             if (staged)
                 for (uint32_t q = threadIdx.x; q < cnt; q += TPB) L.src[q] = in_src[e_lo + q];
         }
@@ -187,13 +191,15 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                     const uint32_t i = isrc[m];
                     bool sent = false;
                     if (q < cnt) {
-                        if (GP_ABLATE & ABL_NO_EPHILOX) {
+                        if (i - a.lo >= a.nloc) {  // sender on another rank: the exchange tagged its message
+                            sent = a.rtag[e_lo + q] == r;
+                        } else if (GP_ABLATE & ABL_NO_EPHILOX) {
                             sent = false;
                         } else if (all_active && !(GP_ABLATE & ABL_BITMAP_ONLY)) {
                             const uint32_t di = popc6(present_mask<IMP3D>(i, G)) + 1u;
                             sent = uniform(a.k0, a.k1, S_PUSHSUM, i, r, di) == di - 1u;
                         } else {
-                            sent = (rbc[i >> 6] >> (i & 63)) & 1ull;
+                            sent = (rbc[(i >> 6) - (a.lo >> 6)] >> (i & 63)) & 1ull;
                         }
                     }
                     snt[m] = sent;
@@ -202,7 +208,11 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
 #pragma unroll
                 for (int m = 0; m < FU; ++m) {
                     v[m] = make_double2(0.0, 0.0);
-                    if (snt[m]) v[m] = (GP_ABLATE & ABL_NO_RGATHER) ? make_double2((double)isrc[m], 1.0) : ld_sw(swc + isrc[m]);
+                    if (snt[m]) {
+                        const uint32_t q = threadIdx.x + m * TPB;
+                        v[m] = (GP_ABLATE & ABL_NO_RGATHER) ? make_double2((double)isrc[m], 1.0)
+                               : (isrc[m] - a.lo >= a.nloc) ? a.rmsg[e_lo + q] : ld_sw(swc + isrc[m]);
+                    }
                 }
                 const uint32_t wbase = (threadIdx.x >> 6) * WCAP;
                 uint32_t wn = 0;
@@ -223,8 +233,8 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
 #pragma unroll
         for (int k = 0; k < NPT; ++k) {
             const uint32_t jl = k * TPB + threadIdx.x;
-            const uint32_t j = j0 + jl;
-            const bool valid = j < j1;
+            const uint32_t j = T + jl;
+            const bool valid = j >= j0 && j < j1;
             uint32_t dir = DIR_NONE;
             if (valid) {
                 const uint32_t b = lds_byte(L.rows, j - b_rows);
@@ -271,16 +281,24 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                             const uint16_t p = L.pos[e - e_lo];
                             sent = p != POS_NONE;
                             if (p < (uint16_t)MSG_CAP) mi = L.msg[p];
-                            else if (p == POS_GLOBAL) mi = ld_sw(swc + L.src[e - e_lo]);
+                            else if (p == POS_GLOBAL) {
+                                const uint32_t i = L.src[e - e_lo];
+                                mi = (i - a.lo >= a.nloc) ? a.rmsg[e] : ld_sw(swc + i);
+                            }
                         } else {  // rare: tile in-degree above SRC_CAP
                             const uint32_t i = in_src[e];
-                            if (all_active) {
-                                const uint32_t di = popc6(present_mask<IMP3D>(i, G)) + 1u;
-                                sent = uniform(a.k0, a.k1, S_PUSHSUM, i, r, di) == di - 1u;
+                            if (i - a.lo >= a.nloc) {
+                                sent = a.rtag[e] == r;
+                                if (sent) mi = a.rmsg[e];
                             } else {
-                                sent = (rbc[i >> 6] >> (i & 63)) & 1ull;
+                                if (all_active) {
+                                    const uint32_t di = popc6(present_mask<IMP3D>(i, G)) + 1u;
+                                    sent = uniform(a.k0, a.k1, S_PUSHSUM, i, r, di) == di - 1u;
+                                } else {
+                                    sent = (rbc[(i >> 6) - (a.lo >> 6)] >> (i & 63)) & 1ull;
+                                }
+                                if (sent) mi = ld_sw(swc + i);
                             }
-                            if (sent) mi = ld_sw(swc + i);
                         }
                         if (sent) {
                             acc_s = acc_s + mi.x * 0.5;
@@ -315,13 +333,20 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
             }
             if (TOPO == IMP3D) {
                 const unsigned long long bits = __ballot(valid && dir == DIR_RANDOM);
-                if (lane == 0) a.rbn[(j0 + k * TPB + (threadIdx.x & ~63u)) >> 6] = bits;
+                if (lane == 0) a.rbn[((T + k * TPB + (threadIdx.x & ~63u)) >> 6) - (a.lo >> 6)] = bits;
             }
         }
         __syncthreads();
         // node bytes out as words (allocations are padded past P)
-        for (uint32_t w = threadIdx.x; w < (uint32_t)(TILE / 4) && j0 + w * 4 < j1; w += TPB)
-            reinterpret_cast<uint32_t*>(a.nbn)[(j0 >> 2) + w] = L.out[w];
+        for (uint32_t w = threadIdx.x; w < (uint32_t)(TILE / 4); w += TPB) {
+            const uint32_t jw = T + w * 4;
+            if (jw >= j0 && jw + 4 <= j1) {
+                reinterpret_cast<uint32_t*>(a.nbn + T)[w] = L.out[w];
+            } else {
+                for (uint32_t b = 0; b < 4; ++b)
+                    if (jw + b >= j0 && jw + b < j1) a.nbn[jw + b] = reinterpret_cast<const uint8_t*>(L.out)[w * 4 + b];
+            }
+        }
         __syncthreads();
     }
     // block reduction of alerts / newly active
@@ -358,14 +383,16 @@ __global__ __launch_bounds__(TPB) void k_gossip_tile(RoundArgs a, uint32_t r) {
     if (ld_agent(&ctl->done)) return;
     const long long inj = ld_agent(&ctl->inj_target);
     const Geom G = a.G;
-    const uint32_t P = G.P;
     const uint32_t H = TOPO == LINE ? 1u : G.g;
     uint32_t alerts = 0;
     const int lane = threadIdx.x & 63;
 
     for (TileWalk tw(a.ntiles, a.walk); tw.t < tw.end; tw.t += tw.step) {
-        const uint32_t j0 = tw.t * TILE;
-        const uint32_t j1 = min(P, j0 + TILE);
+        // tiles sit on global multiples of TILE (4-aligned word I/O, 64-aligned
+        // ballot words); the slab's first and last tile may be partial
+        const uint32_t T = (a.lo / TILE + tw.t) * TILE;
+        const uint32_t j0 = max(a.lo, T);
+        const uint32_t j1 = min(a.lo + a.nloc, T + TILE);
         uint32_t e_lo = 0, e_hi = 0;
         if (TOPO == IMP3D) {
             e_lo = a.in_off[j0];
@@ -374,19 +401,19 @@ __global__ __launch_bounds__(TPB) void k_gossip_tile(RoundArgs a, uint32_t r) {
         int32_t c0[NPT];
 #pragma unroll
         for (int k = 0; k < NPT; ++k) {
-            const uint32_t j = j0 + k * TPB + threadIdx.x;
-            c0[k] = j < j1 ? a.c[j] : (int32_t)GOSSIP_DONE;
+            const uint32_t j = T + k * TPB + threadIdx.x;
+            c0[k] = (j >= j0 && j < j1) ? a.c[j] : (int32_t)GOSSIP_DONE;
         }
-        const uint32_t b_rows = stage_bytes(L.rows, a.nbc, (int64_t)j0 - H, (int64_t)j1 + H, P);
+        const uint32_t b_rows = stage_bytes(L.rows, a.nbc, (int64_t)j0 - H, (int64_t)j1 + H, a.ext_lo, a.ext_hi);
         uint32_t b_xm = 0, b_xp = 0;
         if (TOPO != LINE) {
-            b_xm = stage_bytes(L.xm, a.nbc, (int64_t)j0 - G.g2, (int64_t)j1 - G.g2, P);
-            b_xp = stage_bytes(L.xp, a.nbc, (int64_t)j0 + G.g2, (int64_t)j1 + G.g2, P);
+            b_xm = stage_bytes(L.xm, a.nbc, (int64_t)j0 - G.g2, (int64_t)j1 - G.g2, a.ext_lo, a.ext_hi);
+            b_xp = stage_bytes(L.xp, a.nbc, (int64_t)j0 + G.g2, (int64_t)j1 + G.g2, a.ext_lo, a.ext_hi);
         }
         const uint32_t cnt = e_hi - e_lo;
         const bool staged = cnt <= (uint32_t)SRC_CAP;
         if (TOPO == IMP3D) {
-            for (uint32_t q = threadIdx.x; q <= j1 - j0; q += TPB) L.off[q] = a.in_off[j0 + q];
+            for (uint32_t q = j0 - T + threadIdx.x; q <= j1 - T; q += TPB) L.off[q] = a.in_off[T + q];
             if (staged) {
                 // all sender loads, then all bitmap loads, in flight together
                 constexpr int FU = SRC_CAP / TPB;
@@ -400,12 +427,16 @@ __global__ __launch_bounds__(TPB) void k_gossip_tile(RoundArgs a, uint32_t r) {
 #pragma unroll
                 for (int m = 0; m < FU; ++m) {
                     const uint32_t q = threadIdx.x + m * TPB;
-                    wv[m] = q < cnt ? a.rbc[isrc[m] >> 6] : 0ull;
+                    const uint32_t li = isrc[m] - a.lo;
+                    wv[m] = q >= cnt ? 0ull
+                            : li < a.nloc ? a.rbc[(isrc[m] >> 6) - (a.lo >> 6)]
+                                          : (a.rtag[e_lo + q] == r ? ~0ull : 0ull);
                 }
 #pragma unroll
                 for (int m = 0; m < FU; ++m) {
                     const uint32_t q = threadIdx.x + m * TPB;
-                    if (q < cnt) reinterpret_cast<uint8_t*>(L.sent)[q] = (uint8_t)((wv[m] >> (isrc[m] & 63)) & 1ull);
+                    if (q < cnt)
+                        reinterpret_cast<uint8_t*>(L.sent)[q] = (uint8_t)((wv[m] >> (isrc[m] & 63)) & 1ull);
                 }
             }
         }
@@ -413,8 +444,8 @@ __global__ __launch_bounds__(TPB) void k_gossip_tile(RoundArgs a, uint32_t r) {
 #pragma unroll
         for (int k = 0; k < NPT; ++k) {
             const uint32_t jl = k * TPB + threadIdx.x;
-            const uint32_t j = j0 + jl;
-            const bool valid = j < j1;
+            const uint32_t j = T + jl;
+            const bool valid = j >= j0 && j < j1;
             uint32_t dir = DIR_NONE;
             if (valid) {
                 const uint32_t mask = present_mask<TOPO>(j, G);
@@ -439,7 +470,9 @@ __global__ __launch_bounds__(TPB) void k_gossip_tile(RoundArgs a, uint32_t r) {
                         } else {
                             for (uint32_t e = e_b; e < e_e; ++e) {
                                 const uint32_t i = a.in_src[e];
-                                inc += (uint32_t)((a.rbc[i >> 6] >> (i & 63)) & 1ull);
+                                const uint32_t li = i - a.lo;
+                                inc += li < a.nloc ? (uint32_t)((a.rbc[(i >> 6) - (a.lo >> 6)] >> (i & 63)) & 1ull)
+                                                   : (a.rtag[e] == r ? 1u : 0u);
                             }
                         }
                     }
@@ -458,12 +491,19 @@ __global__ __launch_bounds__(TPB) void k_gossip_tile(RoundArgs a, uint32_t r) {
             }
             if (TOPO == IMP3D) {
                 const unsigned long long bits = __ballot(valid && dir == DIR_RANDOM);
-                if (lane == 0) a.rbn[(j0 + k * TPB + (threadIdx.x & ~63u)) >> 6] = bits;
+                if (lane == 0) a.rbn[((T + k * TPB + (threadIdx.x & ~63u)) >> 6) - (a.lo >> 6)] = bits;
             }
         }
         __syncthreads();
-        for (uint32_t w = threadIdx.x; w < (uint32_t)(TILE / 4) && j0 + w * 4 < j1; w += TPB)
-            reinterpret_cast<uint32_t*>(a.nbn)[(j0 >> 2) + w] = L.out[w];
+        for (uint32_t w = threadIdx.x; w < (uint32_t)(TILE / 4); w += TPB) {
+            const uint32_t jw = T + w * 4;
+            if (jw >= j0 && jw + 4 <= j1) {
+                reinterpret_cast<uint32_t*>(a.nbn + T)[w] = L.out[w];
+            } else {
+                for (uint32_t b = 0; b < 4; ++b)
+                    if (jw + b >= j0 && jw + b < j1) a.nbn[jw + b] = reinterpret_cast<const uint8_t*>(L.out)[w * 4 + b];
+            }
+        }
         __syncthreads();
     }
     uint32_t x = alerts;
@@ -479,37 +519,50 @@ __global__ __launch_bounds__(TPB) void k_gossip_tile(RoundArgs a, uint32_t r) {
 }
 
 // Random-edge bits of round 0 (only the seed can be sending).
-__global__ __launch_bounds__(TPB) void k_rbits_init(const uint8_t* nb, uint64_t* rb, uint32_t P, uint32_t nwords) {
+// nb indexed by global id; bit (j - lo) of rb for the slab's nodes.
+// Word w holds ids [64 (w + lo/64), +64) (global 64-alignment, as the round kernels).
+__global__ __launch_bounds__(TPB) void k_rbits_init(const uint8_t* nb, uint64_t* rb, uint32_t lo, uint32_t nloc,
+                                                    uint32_t nwords) {
+    const uint32_t j00 = lo & ~63u;
     for (uint32_t jb = blockIdx.x * TPB; jb < nwords * 64u; jb += gridDim.x * TPB) {
-        const uint32_t j = jb + threadIdx.x;
-        const bool bit = j < P && (nb[j] & DIR_MASK) == DIR_RANDOM;
+        const uint32_t j = j00 + jb + threadIdx.x;
+        const bool bit = j >= lo && j - lo < nloc && (nb[j] & DIR_MASK) == DIR_RANDOM;
         const unsigned long long bits = __ballot(bit);
-        if ((threadIdx.x & 63) == 0) rb[j >> 6] = bits;
+        if ((threadIdx.x & 63) == 0) rb[(j >> 6) - (lo >> 6)] = bits;
     }
 }
 
 uint32_t round_tiles(uint32_t P) { return (P + TILE - 1) / TILE; }
 // 64-bit words the ballot stores of one round touch (whole tiles) plus slack.
-uint32_t rbits_words_for(uint32_t P) { return round_tiles(P) * (TILE / 64) + 16u; }
+uint32_t rbits_words_for(uint32_t lo, uint32_t nloc) {
+    return ((lo + nloc + TILE - 1) / TILE - lo / TILE) * (TILE / 64) + 16u;
+}
 
 RoundArgs make_round_args(const DevState& S, uint32_t round) {
     const int cur = round & 1;
     RoundArgs a;
-    a.swc = S.sw[cur];
-    a.swn = S.sw[cur ^ 1];
-    a.nbc = S.nb[cur];
-    a.nbn = S.nb[cur ^ 1];
+    // node arrays indexed by global id: pointers offset by the slab's first id
+    a.swc = S.sw[cur] ? S.sw[cur] - S.base : nullptr;
+    a.swn = S.sw[cur ^ 1] ? S.sw[cur ^ 1] - S.base : nullptr;
+    a.nbc = S.nb[cur] ? S.nb[cur] - S.base : nullptr;
+    a.nbn = S.nb[cur ^ 1] ? S.nb[cur ^ 1] - S.base : nullptr;
     a.rbc = S.rbits[cur];
     a.rbn = S.rbits[cur ^ 1];
-    a.in_off = S.in_off;
+    a.in_off = S.in_off ? S.in_off - S.lo : nullptr;
     a.in_src = S.in_src;
-    a.c = S.c;
+    a.rtag = S.rtag;
+    a.rmsg = S.rmsg;
+    a.c = S.c ? S.c - S.lo : nullptr;
+    a.lo = S.lo;
+    a.nloc = S.nloc;
+    a.ext_lo = S.ext_lo;
+    a.ext_hi = S.ext_hi;
     a.ctl = S.ctl;
     a.G = S.G;
     a.k0 = S.k0;
     a.k1 = S.k1;
     a.seed_node = S.seed_node;
-    a.ntiles = round_tiles(S.G.P);
+    a.ntiles = (S.lo + S.nloc + TILE - 1) / TILE - S.lo / TILE;
     a.walk = S.tile_walk;
     return a;
 }
@@ -534,7 +587,8 @@ hipError_t launch_round_tile(const DevState& S, uint32_t round, int grid, hipStr
 }
 
 hipError_t launch_rbits_init(const DevState& S, int grid, hipStream_t st) {
-    hipLaunchKernelGGL(k_rbits_init, dim3(grid), dim3(TPB), 0, st, S.nb[0], S.rbits[0], S.G.P, S.rbits_words);
+    hipLaunchKernelGGL(k_rbits_init, dim3(grid), dim3(TPB), 0, st, S.nb[0] - S.base, S.rbits[0], S.lo, S.nloc,
+                       S.rbits_words);
     return hipGetLastError();
 }
 

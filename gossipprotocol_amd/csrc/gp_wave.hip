@@ -38,8 +38,7 @@ __device__ __forceinline__ bool local_sent_random(const WaveArgs& a, uint32_t i,
         const uint32_t di = popc6(present_mask<IMP3D>(i, a.G)) + 1u;
         return uniform(a.k0, a.k1, stream, i, r, di) == di - 1u;
     }
-    const uint32_t li = i - a.lo;
-    return (a.rbc[li >> 6] >> (li & 63)) & 1ull;
+    return (a.rbc[(i >> 6) - (a.lo >> 6)] >> (i & 63)) & 1ull;
 }
 
 }  // namespace
@@ -63,16 +62,19 @@ __global__ __launch_bounds__(BULK_THREADS) void k_ps_wave(WaveArgs a, uint32_t r
 
     const uint32_t wg = blockIdx.x * WPB + (threadIdx.x >> 6), wn = gridDim.x * WPB;
     for (uint32_t ch = wg; ch < a.nchunks; ch += wn) {
-        const uint32_t c0 = lo + ch * CH;                 // first node of the chunk (global id)
-        const uint32_t c1 = min(lo + nloc, c0 + CH);      // one past the last
+        // chunks sit on global multiples of CH (64-aligned ballot words); the
+        // slab's first and last chunk may be partial: valid ids [cv, c1)
+        const uint32_t c0 = ((lo / CH) + ch) * CH;
+        const uint32_t cv = max(lo, c0);
+        const uint32_t c1 = min(lo + nloc, c0 + CH);
         // ---- 1. loads that depend on nothing
         double2 own[WNPT];
         uint32_t bown[WNPT], from[WNPT], off[WNPT];
 #pragma unroll
         for (int k = 0; k < WNPT; ++k) {
             const uint32_t j = c0 + k * 64 + lane;
-            const bool valid = j < c1;
-            const uint32_t jl = (valid ? j : c0) - base;
+            const bool valid = j >= cv && j < c1;
+            const uint32_t jl = (valid ? j : cv) - base;
             own[k] = swc[jl];
             bown[k] = nbc[jl];
             const uint32_t mask = valid ? present_mask<TOPO>(j, G) : 0u;
@@ -80,12 +82,12 @@ __global__ __launch_bounds__(BULK_THREADS) void k_ps_wave(WaveArgs a, uint32_t r
 #pragma unroll
             for (uint32_t d = 0; d < ND; ++d) {
                 const bool has = (mask >> d) & 1u;
-                const uint32_t nl = (has ? nbr<TOPO>(j, d, G) : c0) - base;
+                const uint32_t nl = (has ? nbr<TOPO>(j, d, G) : cv) - base;
                 const uint32_t nbd = nbc[nl] & DIR_MASK;
                 f |= (has && nbd == (d ^ 1u)) ? (1u << d) : 0u;
             }
             from[k] = f;
-            if (TOPO == IMP3D) off[k] = a.in_off[min(j, c1) - lo];
+            if (TOPO == IMP3D) off[k] = a.in_off[min(max(j, cv), c1) - lo];
         }
         // ---- 2. Imp3D in-edges: flattened decide + gather, parked in LDS
         uint32_t e0 = 0, e1 = 0;
@@ -137,7 +139,7 @@ __global__ __launch_bounds__(BULK_THREADS) void k_ps_wave(WaveArgs a, uint32_t r
 #pragma unroll
         for (int k = 0; k < WNPT; ++k) {
             const uint32_t j = c0 + k * 64 + lane;
-            const bool valid = j < c1;
+            const bool valid = j >= cv && j < c1;
             const uint32_t mask = valid ? present_mask<TOPO>(j, G) : 0u;
             const uint32_t deg = popc6(mask) + (TOPO == IMP3D ? 1u : 0u);
             const uint32_t b = bown[k];
@@ -151,7 +153,7 @@ __global__ __launch_bounds__(BULK_THREADS) void k_ps_wave(WaveArgs a, uint32_t r
 #pragma unroll
             for (uint32_t d = 0; d < ND; ++d) {
                 const bool s = (f >> d) & 1u;
-                const uint32_t nl = (s ? nbr<TOPO>(j, d, G) : c0) - base;
+                const uint32_t nl = (s ? nbr<TOPO>(j, d, G) : cv) - base;
                 m[d] = s ? swc[nl] : make_double2(0.0, 0.0);
             }
 #pragma unroll
@@ -225,7 +227,7 @@ __global__ __launch_bounds__(BULK_THREADS) void k_ps_wave(WaveArgs a, uint32_t r
             }
             if (TOPO == IMP3D && !all_active) {
                 const unsigned long long bits = __ballot(valid && dir == DIR_RANDOM);
-                if (lane == 0) a.rbn[(c0 - lo + k * 64) >> 6] = bits;
+                if (lane == 0) a.rbn[((c0 + k * 64) >> 6) - (lo >> 6)] = bits;
             }
             __builtin_amdgcn_sched_barrier(0);  // one node's gathers live at a time (VGPR budget)
         }
@@ -254,25 +256,28 @@ __global__ __launch_bounds__(BULK_THREADS) void k_gossip_wave(WaveArgs a, uint32
 
     const uint32_t wg = blockIdx.x * WPB + (threadIdx.x >> 6), wn = gridDim.x * WPB;
     for (uint32_t ch = wg; ch < a.nchunks; ch += wn) {
-        const uint32_t c0 = lo + ch * CH;
+        // chunks sit on global multiples of CH (64-aligned ballot words); the
+        // slab's first and last chunk may be partial: valid ids [cv, c1)
+        const uint32_t c0 = ((lo / CH) + ch) * CH;
+        const uint32_t cv = max(lo, c0);
         const uint32_t c1 = min(lo + nloc, c0 + CH);
         int32_t c0v[WNPT];
         uint32_t inc[WNPT], off[WNPT];
 #pragma unroll
         for (int k = 0; k < WNPT; ++k) {
             const uint32_t j = c0 + k * 64 + lane;
-            const bool valid = j < c1;
-            c0v[k] = a.c[(valid ? j : c0) - lo];
+            const bool valid = j >= cv && j < c1;
+            c0v[k] = a.c[(valid ? j : cv) - lo];
             const uint32_t mask = valid ? present_mask<TOPO>(j, G) : 0u;
             uint32_t n = (valid && (long long)j == inj) ? 1u : 0u;
 #pragma unroll
             for (uint32_t d = 0; d < ND; ++d) {
                 const bool has = (mask >> d) & 1u;
-                const uint32_t nl = (has ? nbr<TOPO>(j, d, G) : c0) - base;
+                const uint32_t nl = (has ? nbr<TOPO>(j, d, G) : cv) - base;
                 n += (has && (nbc[nl] & DIR_MASK) == (d ^ 1u)) ? 1u : 0u;
             }
             inc[k] = n;
-            if (TOPO == IMP3D) off[k] = a.in_off[min(j, c1) - lo];
+            if (TOPO == IMP3D) off[k] = a.in_off[min(max(j, cv), c1) - lo];
         }
         uint32_t e0 = 0, e1 = 0;
         if (TOPO == IMP3D) {
@@ -303,7 +308,7 @@ __global__ __launch_bounds__(BULK_THREADS) void k_gossip_wave(WaveArgs a, uint32
 #pragma unroll
         for (int k = 0; k < WNPT; ++k) {
             const uint32_t j = c0 + k * 64 + lane;
-            const bool valid = j < c1;
+            const bool valid = j >= cv && j < c1;
             const uint32_t mask = valid ? present_mask<TOPO>(j, G) : 0u;
             uint32_t n = inc[k];
             if (TOPO == IMP3D) {
@@ -337,7 +342,7 @@ __global__ __launch_bounds__(BULK_THREADS) void k_gossip_wave(WaveArgs a, uint32
             if (valid) a.nbn[j - base] = (uint8_t)dir;
             if (TOPO == IMP3D) {
                 const unsigned long long bits = __ballot(valid && dir == DIR_RANDOM);
-                if (lane == 0) a.rbn[(c0 - lo + k * 64) >> 6] = bits;
+                if (lane == 0) a.rbn[((c0 + k * 64) >> 6) - (lo >> 6)] = bits;
             }
         }
         if (TOPO == IMP3D) wave_lds_sync();
@@ -345,7 +350,7 @@ __global__ __launch_bounds__(BULK_THREADS) void k_gossip_wave(WaveArgs a, uint32
     block_add2(alerts, 0u, &ctl->round_alerts, nullptr);
 }
 
-uint32_t wave_chunks(uint32_t nloc) { return (nloc + CH - 1) / CH; }
+uint32_t wave_chunks(uint32_t lo, uint32_t nloc) { return (lo + nloc + CH - 1) / CH - lo / CH; }
 
 // Resident 256-thread blocks per CU of the round kernel (grid = this x CUs: one
 // continuous sweep, so the x-1 plane a chunk gathers from was just streamed).
@@ -384,7 +389,7 @@ WaveArgs make_wave_args(const DevState& S, uint32_t round) {
     a.lo = S.lo;
     a.nloc = S.nloc;
     a.base = S.base;
-    a.nchunks = wave_chunks(S.nloc);
+    a.nchunks = wave_chunks(S.lo, S.nloc);
     a.x_lo = a.x_hi = a.zsegs = a.yblocks = a.xs_len = a.nitems = 0;
     if (S.G.g2) {  // column kernels (3D / Imp3D)
         const uint32_t g = S.G.g;
