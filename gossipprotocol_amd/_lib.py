@@ -17,6 +17,7 @@ GP_LINE, GP_FULL, GP_3D, GP_IMP3D = 0, 1, 2, 3
 GP_GOSSIP, GP_PUSHSUM = 0, 1
 GP_STATUS_CONVERGED, GP_STATUS_MAX_ROUNDS = 0, 1
 GP_FLAG_KERNEL_TIMING = 1
+GP_FLAG_VIRTUAL_RANKS = 2
 ERRORS = {-1: "GP_EINVAL", -2: "GP_ENOMEM", -3: "GP_EHIP", -4: "GP_ENCCL", -5: "GP_ESTATE", -6: "GP_ENODEV"}
 
 

@@ -1,24 +1,39 @@
 // gp_api.hip -- C-ABI of libgossip_hip.so (include/gossip_hip.h) and the host
-// orchestrator of the synchronous round loop.
+// orchestrator of the synchronous round loop, on one GPU or sharded over ranks.
 //
 // Replaces, in /root/reference/Project2/Program.fs:
 //   * actor population + topology build (Program.fs:169-176,180-191,209-216,238-261)
-//     -> gp_create: SoA device state, implicit neighbours, Imp3D in-lists;
+//     -> gp_create / gp_create_rank: SoA device state per slab, implicit
+//     neighbours, Imp3D receiver-sorted in-lists;
 //   * message loop + scheduler (Program.fs:41-61,84-131,141-163) -> gp_step / gp_run:
-//     per round one bulk kernel + one finalize kernel, queued in batches with one
-//     host synchronisation per batch (never per round).
+//     per round the bulk round kernel, the inter-rank exchange and the
+//     finalize kernel(s), queued in batches with one host synchronisation per
+//     batch (never per round).
+//
+// Sharding: contiguous node-id slabs, plane-aligned for 3D /
+// Imp3D.  Each slab's node arrays carry one halo plane (line: one node) per
+// neighbouring slab.  After every round the halos are refreshed from the
+// neighbours and the Imp3D random-edge messages are exchanged (gp_xchg.hip);
+// the round's alert / activation / injector counts are summed over ranks.
+// Two transports: RCCL between processes (one process per GPU, gp_create_rank),
+// and in-process "virtual ranks" on one device (gp_config.flags
+// GP_FLAG_VIRTUAL_RANKS), which run the same kernels and exchange plan with
+// device copies -- the single-GPU test bed of the multi-GPU path.
 #include <algorithm>
 #include <chrono>
 #include <cmath>
-#include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
 
+#include <rccl/rccl.h>
+
 #include "../../include/gossip_hip.h"
 #include "gp_internal.hpp"
+#include "gp_xchg.hpp"
 
 using namespace gp;
 
@@ -44,22 +59,70 @@ void set_err(const char* fmt, ...) {
         }                                                                               \
     } while (0)
 
+#define NCCL_TRY(expr)                                                                  \
+    do {                                                                                \
+        ncclResult_t r_ = (expr);                                                       \
+        if (r_ != ncclSuccess) {                                                        \
+            set_err("%s failed: %s (%s:%d)", #expr, ncclGetErrorString(r_), __FILE__, __LINE__); \
+            return GP_ENCCL;                                                            \
+        }                                                                               \
+    } while (0)
+
 constexpr int64_t BATCH = 1024;  // rounds queued per host synchronisation (<= HIST)
 static_assert(BATCH <= HIST, "alert ring must cover a batch");
+
+enum Mode { MODE_SINGLE = 0, MODE_VIRTUAL = 1, MODE_RCCL = 2 };
+
+// One rank's share of the network.
+struct Slab {
+    DevState S{};
+    int rank = 0;
+    uint32_t hi = 0;  // one past the last owned id
+    // Imp3D random-edge exchange (W > 1)
+    uint32_t* pos = nullptr;
+    uint8_t* xsend = nullptr;
+    uint8_t* xrecv = nullptr;
+    uint32_t nedges = 0;
+    std::vector<uint32_t> cap_out, cap_in;
+    std::vector<size_t> soff, sbytes, roff, rbytes;
+    unsigned int* overflow = nullptr;  // device flag
+};
+
+size_t xbuf_bytes(uint32_t cap, bool push) {
+    if (!cap) return 0;
+    const size_t slots = ((size_t)cap * 4 + 15) & ~(size_t)15;
+    return 16 + slots + (push ? (size_t)cap * 16 : 0);
+}
+
+XPeer xpeer(uint8_t* buf, size_t off, uint32_t cap) {
+    XPeer p{};
+    if (!cap) return p;
+    uint8_t* b = buf + off;
+    p.cnt = reinterpret_cast<uint32_t*>(b);
+    p.slots = reinterpret_cast<uint32_t*>(b + 16);
+    p.vals = reinterpret_cast<double2*>(b + 16 + (((size_t)cap * 4 + 15) & ~(size_t)15));
+    p.cap = cap;
+    return p;
+}
 
 }  // namespace
 
 struct gp_sim {
     gp_config cfg{};
-    DevState S{};
     int device = 0;
     hipStream_t stream = nullptr;
     int grid = 1;
     int64_t P = 0, T = 0, g = 0;
+    int mode = MODE_SINGLE;
+    int world = 1, rank = 0;  // ranks sharing the population; this process's rank (RCCL)
+    std::vector<uint32_t> bounds;  // world + 1 slab boundaries (global ids)
+    uint32_t halo = 0;             // ids per halo side
+    std::vector<Slab> slab;        // MODE_VIRTUAL: all ranks; otherwise this rank's
+    ncclComm_t comm = nullptr;
     int64_t rounds_done = 0;
     int64_t alerts_total = 0;
     bool done = false;
-    Ctl* host_ctl = nullptr;  // pinned mirror of the device control block
+    Ctl* host_ctl = nullptr;  // pinned mirror of slab 0's control block (global bookkeeping)
     std::vector<void*> allocs;
     // kernel timing
     bool timing = false;
@@ -71,7 +134,7 @@ struct gp_sim {
 namespace {
 
 int dev_alloc(gp_sim* s, void** p, size_t bytes) {
-    if (bytes == 0) bytes = 4;
+    if (bytes == 0) bytes = 16;
     hipError_t e = hipMalloc(p, bytes);
     if (e != hipSuccess) {
         set_err("hipMalloc(%zu bytes) failed: %s", bytes, hipGetErrorString(e));
@@ -100,44 +163,6 @@ uint32_t bits_for(uint64_t maxval) {
     return b;
 }
 
-// Imp3D: draw rnd[] (Program.fs:258-260), then build the receiver-sorted
-// in-lists: a stable sort of (rnd[i], i) by rnd keeps every receiver's
-// senders in ascending id order; in_off = exclusive scan of the in-degrees.
-int build_imp3d(gp_sim* s) {
-    DevState& S = s->S;
-    const uint32_t P = S.G.P;
-    int rc;
-    if ((rc = dev_alloc_t(s, &S.rnd, P)) || (rc = dev_alloc_t(s, &S.in_off, (size_t)P + 1)) ||
-        (rc = dev_alloc_t(s, &S.in_src, P)))
-        return rc;
-    uint32_t *iota = nullptr, *keys_sorted = nullptr, *counts = nullptr;
-    HIP_TRY(hipMalloc(&iota, sizeof(uint32_t) * P));
-    HIP_TRY(hipMalloc(&keys_sorted, sizeof(uint32_t) * P));
-    HIP_TRY(hipMalloc(&counts, sizeof(uint32_t) * ((size_t)P + 1)));
-    HIP_TRY(launch_topo_rnd(S, s->grid, s->stream));
-    HIP_TRY(launch_iota(iota, P, s->grid, s->stream));
-    const uint32_t bits = bits_for(P > 1 ? P - 2 : 0);
-    size_t tmp_bytes = 0;
-    HIP_TRY(sort_pairs(nullptr, tmp_bytes, S.rnd, keys_sorted, iota, S.in_src, P, bits, s->stream));
-    void* tmp = nullptr;
-    HIP_TRY(hipMalloc(&tmp, tmp_bytes ? tmp_bytes : 4));
-    HIP_TRY(sort_pairs(tmp, tmp_bytes, S.rnd, keys_sorted, iota, S.in_src, P, bits, s->stream));
-    HIP_TRY(hipMemsetAsync(counts, 0, sizeof(uint32_t) * ((size_t)P + 1), s->stream));
-    HIP_TRY(launch_histogram(S.rnd, P, counts, s->grid, s->stream));
-    size_t scan_bytes = 0;
-    HIP_TRY(exclusive_scan_u32(nullptr, scan_bytes, counts, S.in_off, P + 1, s->stream));
-    void* scan_tmp = nullptr;
-    HIP_TRY(hipMalloc(&scan_tmp, scan_bytes ? scan_bytes : 4));
-    HIP_TRY(exclusive_scan_u32(scan_tmp, scan_bytes, counts, S.in_off, P + 1, s->stream));
-    HIP_TRY(hipStreamSynchronize(s->stream));
-    HIP_TRY(hipFree(scan_tmp));
-    HIP_TRY(hipFree(tmp));
-    HIP_TRY(hipFree(counts));
-    HIP_TRY(hipFree(keys_sorted));
-    HIP_TRY(hipFree(iota));
-    return GP_OK;
-}
-
 int check_device(int device) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
@@ -157,25 +182,424 @@ int check_device(int device) {
     return GP_OK;
 }
 
-// One synchronous round r (bulk kernel[s]) followed by the finalize kernel.
-int launch_round(gp_sim* s, uint32_t r, hipEvent_t e0, hipEvent_t e1) {
-    DevState& S = s->S;
-    if (e0) HIP_TRY(hipEventRecord(e0, s->stream));
-    if (S.topo == FULL && S.alg == PUSHSUM) {
-        HIP_TRY(launch_full_pushsum_send(S, r, s->grid, s->stream));
-        HIP_TRY(sort_pairs(S.sort_tmp, S.sort_tmp_bytes, S.key[0], S.key[1], S.val[0], S.val[1], S.G.P, S.key_bits,
-                           s->stream));
-        HIP_TRY(hipMemsetAsync(S.head, 0xFF, sizeof(uint32_t) * S.G.P, s->stream));
-        HIP_TRY(launch_full_pushsum_mark(S, s->grid, s->stream));
+// Slab boundaries: 3D / Imp3D whole x-planes (Program.fs:246-257 id = x g^2 + y g + z),
+// line contiguous ids; full topology is single-rank.
+int make_bounds(gp_sim* s) {
+    const int W = s->world;
+    s->bounds.assign(W + 1, 0);
+    const int topo = s->cfg.topology;
+    if (W == 1) {
+        s->bounds[1] = (uint32_t)s->P;
+        s->halo = 0;
+        return GP_OK;
     }
-    HIP_TRY(launch_bulk(S, r, s->grid, s->stream));
-    if (e1) HIP_TRY(hipEventRecord(e1, s->stream));
-    HIP_TRY(launch_finalize(S, r, r + 1, s->stream));
+    if (W > XMAXW) {
+        set_err("at most %d ranks are supported (got %d)", XMAXW, W);
+        return GP_EINVAL;
+    }
+    if (topo == GP_FULL) {
+        set_err("the full topology runs on one GPU in this release (num_gpus = 1)");
+        return GP_EINVAL;
+    }
+    if (topo == GP_LINE) {
+        if (s->P < W) {
+            set_err("line with %lld nodes cannot be split over %d ranks", (long long)s->P, W);
+            return GP_EINVAL;
+        }
+        for (int w = 0; w <= W; ++w) s->bounds[w] = (uint32_t)(s->P * w / W);
+        s->halo = 1;
+    } else {
+        if (s->g < W) {
+            set_err("a %lld^3 lattice has fewer planes than ranks (%d)", (long long)s->g, W);
+            return GP_EINVAL;
+        }
+        for (int w = 0; w <= W; ++w) s->bounds[w] = (uint32_t)((s->g * w / W) * s->g * s->g);
+        s->halo = (uint32_t)(s->g * s->g);
+    }
     return GP_OK;
 }
 
+// Device state of slab `r` (rank r): ids [bounds[r], bounds[r+1]) plus halos.
+int alloc_slab(gp_sim* s, Slab& sl, int r) {
+    DevState& S = sl.S;
+    const int W = s->world;
+    sl.rank = r;
+    const uint32_t lo = s->bounds[r], hi = s->bounds[r + 1];
+    sl.hi = hi;
+    S.topo = s->cfg.topology;
+    S.alg = s->cfg.algorithm;
+    S.G.P = (uint32_t)s->P;
+    S.G.T = (uint32_t)s->T;
+    S.G.g = (uint32_t)s->g;
+    S.G.g2 = (uint32_t)(s->g * s->g);
+    S.G.div_g = make_fastdiv(S.G.g ? S.G.g : 1);
+    S.G.div_g2 = make_fastdiv(S.G.g2 ? S.G.g2 : 1);
+    S.k0 = (uint32_t)s->cfg.seed;
+    S.k1 = (uint32_t)(s->cfg.seed >> 32);
+    // choice = Random().Next(0, nodes) (Program.fs:193,221,263)
+    S.seed_node = uniform(S.k0, S.k1, S_START, 0, 0, (uint32_t)s->T);
+    S.lo = lo;
+    S.nloc = hi - lo;
+    S.ext_lo = r > 0 ? lo - s->halo : lo;
+    S.ext_hi = r < W - 1 ? hi + s->halo : hi;
+    S.base = S.ext_lo & ~3u;  // 4-aligned: the tile kernels move node bytes as words
+    S.rtag = nullptr;
+    S.rmsg = nullptr;
+    int rc;
+    const size_t next = (size_t)(S.ext_hi - S.base) + 1024;  // node arrays (+ word-I/O padding)
+    const size_t nl = S.nloc;
+    if ((rc = dev_alloc_t(s, &S.ctl, 1))) return rc;
+    if (S.alg == PUSHSUM) {
+        if ((rc = dev_alloc_t(s, &S.sw[0], next)) || (rc = dev_alloc_t(s, &S.sw[1], next)) ||
+            (rc = dev_alloc_t(s, &S.nb[0], next)))
+            return rc;
+        if (S.topo != FULL && (rc = dev_alloc_t(s, &S.nb[1], next))) return rc;
+    } else {
+        if ((rc = dev_alloc_t(s, &S.c, nl))) return rc;
+        if (S.topo == FULL) {
+            if ((rc = dev_alloc_t(s, &S.inc, nl))) return rc;
+        } else {
+            if ((rc = dev_alloc_t(s, &S.nb[0], next)) || (rc = dev_alloc_t(s, &S.nb[1], next))) return rc;
+            S.nchunks = (uint32_t)((s->T + INJ_CHUNK - 1) / INJ_CHUNK);
+            if ((rc = dev_alloc_t(s, &S.live_bits, (size_t)S.nchunks * (INJ_CHUNK / 32))) ||
+                (rc = dev_alloc_t(s, &S.chunk_live, S.nchunks)))
+                return rc;
+        }
+    }
+    if (S.topo == FULL && S.alg == PUSHSUM) {
+        const uint32_t P = S.G.P;
+        if ((rc = dev_alloc_t(s, &S.key[0], P)) || (rc = dev_alloc_t(s, &S.key[1], P)) ||
+            (rc = dev_alloc_t(s, &S.val[0], P)) || (rc = dev_alloc_t(s, &S.val[1], P)) ||
+            (rc = dev_alloc_t(s, &S.head, P)))
+            return rc;
+        S.key_bits = bits_for((uint64_t)P);
+        HIP_TRY(launch_iota(S.val[0], P, s->grid, s->stream));
+        size_t tb = 0;
+        HIP_TRY(sort_pairs(nullptr, tb, S.key[0], S.key[1], S.val[0], S.val[1], P, S.key_bits, s->stream));
+        S.sort_tmp_bytes = tb;
+        if ((rc = dev_alloc(s, &S.sort_tmp, tb))) return rc;
+    }
+    if (S.topo == IMP3D) {
+        S.rbits_words = S.kernel == KERNEL_COL ? col_rbits_words(S.nloc / S.G.g2, S.G.g)
+                                               : rbits_words_for(S.lo, S.nloc);
+        if ((rc = dev_alloc_t(s, &S.rbits[0], S.rbits_words)) || (rc = dev_alloc_t(s, &S.rbits[1], S.rbits_words)))
+            return rc;
+    }
+    return GP_OK;
+}
+
+// Imp3D: draw rnd[] for every node (Program.fs:258-260), then a stable sort of
+// (rnd[i], i) by rnd gives every receiver's senders in ascending id order and
+// in_off = exclusive scan of the in-degrees.  Every rank builds the global
+// order (it is deterministic) and keeps its receivers' slice; with several
+// ranks, each local sender also learns the position of its message in the
+// destination's in-edge array (pos).
+int build_imp3d(gp_sim* s) {
+    const uint32_t P = (uint32_t)s->P;
+    const int W = s->world;
+    DevState& S0 = s->slab[0].S;
+    uint32_t *rnd_all = nullptr, *iota = nullptr, *keys_sorted = nullptr, *src_sorted = nullptr, *counts = nullptr,
+             *off_all = nullptr, *inv = nullptr;
+    HIP_TRY(hipMalloc(&rnd_all, sizeof(uint32_t) * P));
+    HIP_TRY(hipMalloc(&iota, sizeof(uint32_t) * P));
+    HIP_TRY(hipMalloc(&keys_sorted, sizeof(uint32_t) * P));
+    HIP_TRY(hipMalloc(&src_sorted, sizeof(uint32_t) * P));
+    HIP_TRY(hipMalloc(&counts, sizeof(uint32_t) * ((size_t)P + 1)));
+    HIP_TRY(hipMalloc(&off_all, sizeof(uint32_t) * ((size_t)P + 1)));
+    HIP_TRY(launch_topo_rnd_range(S0.k0, S0.k1, P, 0, P, rnd_all, s->grid, s->stream));
+    HIP_TRY(launch_iota(iota, P, s->grid, s->stream));
+    const uint32_t bits = bits_for(P > 1 ? P - 2 : 0);
+    size_t tmp_bytes = 0;
+    HIP_TRY(sort_pairs(nullptr, tmp_bytes, rnd_all, keys_sorted, iota, src_sorted, P, bits, s->stream));
+    void* tmp = nullptr;
+    HIP_TRY(hipMalloc(&tmp, tmp_bytes ? tmp_bytes : 4));
+    HIP_TRY(sort_pairs(tmp, tmp_bytes, rnd_all, keys_sorted, iota, src_sorted, P, bits, s->stream));
+    HIP_TRY(hipMemsetAsync(counts, 0, sizeof(uint32_t) * ((size_t)P + 1), s->stream));
+    HIP_TRY(launch_histogram(rnd_all, P, counts, s->grid, s->stream));
+    size_t scan_bytes = 0;
+    HIP_TRY(exclusive_scan_u32(nullptr, scan_bytes, counts, off_all, P + 1, s->stream));
+    void* scan_tmp = nullptr;
+    HIP_TRY(hipMalloc(&scan_tmp, scan_bytes ? scan_bytes : 4));
+    HIP_TRY(exclusive_scan_u32(scan_tmp, scan_bytes, counts, off_all, P + 1, s->stream));
+    if (W > 1) {
+        HIP_TRY(hipMalloc(&inv, sizeof(uint32_t) * P));
+        HIP_TRY(launch_inverse(src_sorted, P, inv, s->grid, s->stream));
+    }
+    // first global edge of every rank
+    std::vector<uint32_t> edge0(W + 1);
+    for (int w = 0; w <= W; ++w)
+        HIP_TRY(hipMemcpyAsync(&edge0[w], off_all + s->bounds[w], sizeof(uint32_t), hipMemcpyDeviceToHost,
+                               s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    int rc;
+    for (Slab& sl : s->slab) {
+        DevState& S = sl.S;
+        const int r = sl.rank;
+        const uint32_t ne = edge0[r + 1] - edge0[r];
+        sl.nedges = ne;
+        if ((rc = dev_alloc_t(s, &S.rnd, S.nloc)) || (rc = dev_alloc_t(s, &S.in_off, (size_t)S.nloc + 1)) ||
+            (rc = dev_alloc_t(s, &S.in_src, ne)))
+            return rc;
+        HIP_TRY(hipMemcpyAsync(S.rnd, rnd_all + S.lo, sizeof(uint32_t) * S.nloc, hipMemcpyDeviceToDevice, s->stream));
+        HIP_TRY(hipMemcpyAsync(S.in_off, off_all + S.lo, sizeof(uint32_t) * ((size_t)S.nloc + 1),
+                               hipMemcpyDeviceToDevice, s->stream));
+        HIP_TRY(launch_sub(S.in_off, S.nloc + 1, edge0[r], s->grid, s->stream));
+        if (ne)
+            HIP_TRY(hipMemcpyAsync(S.in_src, src_sorted + edge0[r], sizeof(uint32_t) * ne, hipMemcpyDeviceToDevice,
+                                   s->stream));
+        if (W > 1) {
+            if ((rc = dev_alloc_t(s, &sl.pos, S.nloc)) || (rc = dev_alloc_t(s, &S.rtag, ne)) ||
+                (S.alg == PUSHSUM && (rc = dev_alloc_t(s, &S.rmsg, ne))))
+                return rc;
+            HIP_TRY(hipMemsetAsync(S.rtag, 0xFF, sizeof(uint32_t) * (ne ? ne : 1), s->stream));
+            PosArgs pa{};
+            pa.rnd = S.rnd;
+            pa.inv = inv;
+            pa.pos = sl.pos;
+            pa.lo = S.lo;
+            pa.nloc = S.nloc;
+            pa.W = W;
+            pa.me = r;
+            for (int w = 0; w <= W; ++w) pa.bounds[w] = s->bounds[w];
+            for (int w = 0; w < W; ++w) pa.edge0[w] = edge0[w];
+            HIP_TRY(launch_make_pos(pa, s->grid, s->stream));
+        }
+    }
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    HIP_TRY(hipFree(scan_tmp));
+    HIP_TRY(hipFree(tmp));
+    if (inv) HIP_TRY(hipFree(inv));
+    HIP_TRY(hipFree(off_all));
+    HIP_TRY(hipFree(counts));
+    HIP_TRY(hipFree(src_sorted));
+    HIP_TRY(hipFree(keys_sorted));
+    HIP_TRY(hipFree(iota));
+    HIP_TRY(hipFree(rnd_all));
+    return GP_OK;
+}
+
+// Fixed-capacity exchange buffers per rank pair: capacity = expected messages
+// per round + 12 sigma + 64 (never more than the pair's random edges).
+int setup_exchange(gp_sim* s) {
+    const int W = s->world;
+    const bool push = s->cfg.algorithm == GP_PUSHSUM;
+    std::vector<uint32_t> caps((size_t)W * W, 0);  // caps[a * W + b]: a -> b
+    double* mu = nullptr;
+    unsigned long long* n = nullptr;
+    HIP_TRY(hipMalloc(&mu, sizeof(double) * XMAXW));
+    HIP_TRY(hipMalloc(&n, sizeof(unsigned long long) * XMAXW));
+    for (Slab& sl : s->slab) {
+        DevState& S = sl.S;
+        HIP_TRY(hipMemsetAsync(mu, 0, sizeof(double) * XMAXW, s->stream));
+        HIP_TRY(hipMemsetAsync(n, 0, sizeof(unsigned long long) * XMAXW, s->stream));
+        ExpectArgs ea{};
+        ea.rnd = S.rnd;
+        ea.lo = S.lo;
+        ea.nloc = S.nloc;
+        ea.W = W;
+        ea.me = sl.rank;
+        for (int w = 0; w <= W; ++w) ea.bounds[w] = s->bounds[w];
+        ea.G = S.G;
+        ea.mu = mu;
+        ea.n = n;
+        HIP_TRY(launch_expect(ea, s->grid, s->stream));
+        double hmu[XMAXW];
+        unsigned long long hn[XMAXW];
+        HIP_TRY(hipMemcpyAsync(hmu, mu, sizeof hmu, hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(hipMemcpyAsync(hn, n, sizeof hn, hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(hipStreamSynchronize(s->stream));
+        for (int b = 0; b < W; ++b) {
+            if (b == sl.rank || hn[b] == 0) continue;
+            const double c = std::ceil(hmu[b] + 12.0 * std::sqrt(hmu[b]) + 64.0);
+            caps[(size_t)sl.rank * W + b] = (uint32_t)std::min<double>(c, (double)hn[b]);
+        }
+    }
+    HIP_TRY(hipFree(mu));
+    HIP_TRY(hipFree(n));
+    if (s->mode == MODE_RCCL) {
+        // every rank learns the capacities of the buffers it will receive
+        uint32_t* d = nullptr;
+        HIP_TRY(hipMalloc(&d, sizeof(uint32_t) * W * W));
+        HIP_TRY(hipMemcpyAsync(d + (size_t)s->rank * W, caps.data() + (size_t)s->rank * W, sizeof(uint32_t) * W,
+                               hipMemcpyHostToDevice, s->stream));
+        NCCL_TRY(ncclAllGather(d + (size_t)s->rank * W, d, W, ncclUint32, s->comm, s->stream));
+        HIP_TRY(hipMemcpyAsync(caps.data(), d, sizeof(uint32_t) * W * W, hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(hipStreamSynchronize(s->stream));
+        HIP_TRY(hipFree(d));
+    }
+    int rc;
+    for (Slab& sl : s->slab) {
+        const int a = sl.rank;
+        sl.cap_out.assign(W, 0);
+        sl.cap_in.assign(W, 0);
+        sl.soff.assign(W, 0);
+        sl.sbytes.assign(W, 0);
+        sl.roff.assign(W, 0);
+        sl.rbytes.assign(W, 0);
+        size_t so = 0, ro = 0;
+        for (int b = 0; b < W; ++b) {
+            sl.cap_out[b] = caps[(size_t)a * W + b];
+            sl.cap_in[b] = caps[(size_t)b * W + a];
+            sl.soff[b] = so;
+            sl.sbytes[b] = xbuf_bytes(sl.cap_out[b], push);
+            so += sl.sbytes[b];
+            sl.roff[b] = ro;
+            sl.rbytes[b] = xbuf_bytes(sl.cap_in[b], push);
+            ro += sl.rbytes[b];
+        }
+        if ((rc = dev_alloc_t(s, &sl.xsend, so)) || (rc = dev_alloc_t(s, &sl.xrecv, ro))) return rc;
+        HIP_TRY(hipMemsetAsync(sl.xsend, 0, so ? so : 16, s->stream));
+        HIP_TRY(hipMemsetAsync(sl.xrecv, 0, ro ? ro : 16, s->stream));
+        sl.overflow = &sl.S.ctl->overflow;
+    }
+    return GP_OK;
+}
+
+// Halo refresh + Imp3D random-edge exchange for round `rn`, whose state the
+// previous round kernel has just written to buffers rn & 1.
+int exchange(gp_sim* s, uint32_t rn) {
+    const int W = s->world;
+    if (W == 1) return GP_OK;
+    const int b = rn & 1;
+    const bool push = s->cfg.algorithm == GP_PUSHSUM;
+    const bool imp = s->cfg.topology == GP_IMP3D;
+    if (imp) {
+        for (Slab& sl : s->slab) {
+            DevState& S = sl.S;
+            ZeroArgs z{};
+            PackArgs pa{};
+            pa.nbn = S.nb[b];
+            pa.swn = push ? S.sw[b] : nullptr;
+            pa.rnd = S.rnd;
+            pa.pos = sl.pos;
+            pa.lo = S.lo;
+            pa.nloc = S.nloc;
+            pa.base = S.base;
+            pa.W = W;
+            pa.me = sl.rank;
+            pa.push = push ? 1 : 0;
+            for (int w = 0; w <= W; ++w) pa.bounds[w] = s->bounds[w];
+            for (int p = 0; p < W; ++p) {
+                pa.peer[p] = xpeer(sl.xsend, sl.soff[p], sl.cap_out[p]);
+                z.cnt[p] = pa.peer[p].cnt;
+            }
+            z.n = W;
+            pa.overflow = sl.overflow;
+            HIP_TRY(launch_zero_counts(z, s->stream));
+            HIP_TRY(launch_pack(pa, s->grid, s->stream));
+        }
+    }
+    const size_t H = s->halo;
+    if (s->mode == MODE_VIRTUAL) {
+        for (int r = 0; r + 1 < W; ++r) {
+            DevState& A = s->slab[r].S;  // lower slab
+            DevState& B = s->slab[r + 1].S;
+            const uint32_t edge = B.lo;  // A's hi
+            // A's last H ids -> B's lower halo; B's first H ids -> A's upper halo
+            HIP_TRY(hipMemcpyAsync(B.nb[b] + (edge - H - B.base), A.nb[b] + (edge - H - A.base), H,
+                                   hipMemcpyDeviceToDevice, s->stream));
+            HIP_TRY(hipMemcpyAsync(A.nb[b] + (edge - A.base), B.nb[b] + (edge - B.base), H, hipMemcpyDeviceToDevice,
+                                   s->stream));
+            if (push) {
+                HIP_TRY(hipMemcpyAsync(B.sw[b] + (edge - H - B.base), A.sw[b] + (edge - H - A.base), H * 16,
+                                       hipMemcpyDeviceToDevice, s->stream));
+                HIP_TRY(hipMemcpyAsync(A.sw[b] + (edge - A.base), B.sw[b] + (edge - B.base), H * 16,
+                                       hipMemcpyDeviceToDevice, s->stream));
+            }
+        }
+        if (imp)
+            for (Slab& a : s->slab)
+                for (Slab& d : s->slab)
+                    if (&a != &d && a.sbytes[d.rank])
+                        HIP_TRY(hipMemcpyAsync(d.xrecv + d.roff[a.rank], a.xsend + a.soff[d.rank], a.sbytes[d.rank],
+                                               hipMemcpyDeviceToDevice, s->stream));
+    } else {
+        Slab& sl = s->slab[0];
+        DevState& S = sl.S;
+        const int r = sl.rank;
+        NCCL_TRY(ncclGroupStart());
+        if (r > 0) {  // my first H ids <-> lower neighbour's last H ids
+            NCCL_TRY(ncclSend(S.nb[b] + (S.lo - S.base), H, ncclUint8, r - 1, s->comm, s->stream));
+            NCCL_TRY(ncclRecv(S.nb[b] + (S.lo - H - S.base), H, ncclUint8, r - 1, s->comm, s->stream));
+            if (push) {
+                NCCL_TRY(ncclSend(S.sw[b] + (S.lo - S.base), H * 16, ncclUint8, r - 1, s->comm, s->stream));
+                NCCL_TRY(ncclRecv(S.sw[b] + (S.lo - H - S.base), H * 16, ncclUint8, r - 1, s->comm, s->stream));
+            }
+        }
+        if (r < W - 1) {  // my last H ids <-> upper neighbour's first H ids
+            NCCL_TRY(ncclSend(S.nb[b] + (sl.hi - H - S.base), H, ncclUint8, r + 1, s->comm, s->stream));
+            NCCL_TRY(ncclRecv(S.nb[b] + (sl.hi - S.base), H, ncclUint8, r + 1, s->comm, s->stream));
+            if (push) {
+                NCCL_TRY(ncclSend(S.sw[b] + (sl.hi - H - S.base), H * 16, ncclUint8, r + 1, s->comm, s->stream));
+                NCCL_TRY(ncclRecv(S.sw[b] + (sl.hi - S.base), H * 16, ncclUint8, r + 1, s->comm, s->stream));
+            }
+        }
+        if (imp)
+            for (int p = 0; p < W; ++p) {
+                if (p == r) continue;
+                if (sl.sbytes[p]) NCCL_TRY(ncclSend(sl.xsend + sl.soff[p], sl.sbytes[p], ncclUint8, p, s->comm, s->stream));
+                if (sl.rbytes[p]) NCCL_TRY(ncclRecv(sl.xrecv + sl.roff[p], sl.rbytes[p], ncclUint8, p, s->comm, s->stream));
+            }
+        NCCL_TRY(ncclGroupEnd());
+    }
+    if (imp) {
+        for (Slab& sl : s->slab) {
+            UnpackArgs ua{};
+            ua.rtag = sl.S.rtag;
+            ua.rmsg = sl.S.rmsg;
+            ua.nedges = sl.nedges;
+            ua.W = W;
+            ua.me = sl.rank;
+            ua.push = push ? 1 : 0;
+            for (int p = 0; p < W; ++p) ua.peer[p] = xpeer(sl.xrecv, sl.roff[p], sl.cap_in[p]);
+            HIP_TRY(launch_unpack(ua, rn, std::max(1, s->grid / 8), s->stream));
+        }
+    }
+    return GP_OK;
+}
+
+// Close round `round_done` (if round_next > 0) and prepare round `round_next`.
+int finalize(gp_sim* s, uint32_t round_done, uint32_t round_next) {
+    if (s->world == 1) {
+        HIP_TRY(launch_finalize(s->slab[0].S, round_done, round_next, s->stream));
+        return GP_OK;
+    }
+    for (Slab& sl : s->slab) HIP_TRY(launch_finalize_pre(sl.S, round_next, s->stream));
+    if (s->mode == MODE_VIRTUAL) {
+        SumArgs sa{};
+        sa.W = (int)s->slab.size();
+        for (int w = 0; w < sa.W; ++w) sa.ctl[w] = s->slab[w].S.ctl;
+        HIP_TRY(launch_sum_xchg(sa, s->stream));
+    } else {
+        Ctl* c = s->slab[0].S.ctl;
+        NCCL_TRY(ncclAllReduce(c->xchg, c->xchg, 4, ncclUint64, ncclSum, s->comm, s->stream));
+    }
+    for (Slab& sl : s->slab) HIP_TRY(launch_finalize_post(sl.S, round_done, round_next, s->stream));
+    return GP_OK;
+}
+
+// One synchronous round r: round kernel(s), exchange, finalize.
+int launch_round(gp_sim* s, uint32_t r, hipEvent_t e0, hipEvent_t e1) {
+    for (size_t q = 0; q < s->slab.size(); ++q) {
+        DevState& S = s->slab[q].S;
+        if (q == 0 && e0) HIP_TRY(hipEventRecord(e0, s->stream));
+        if (S.topo == FULL && S.alg == PUSHSUM) {
+            HIP_TRY(launch_full_pushsum_send(S, r, s->grid, s->stream));
+            HIP_TRY(sort_pairs(S.sort_tmp, S.sort_tmp_bytes, S.key[0], S.key[1], S.val[0], S.val[1], S.G.P,
+                               S.key_bits, s->stream));
+            HIP_TRY(hipMemsetAsync(S.head, 0xFF, sizeof(uint32_t) * S.G.P, s->stream));
+            HIP_TRY(launch_full_pushsum_mark(S, s->grid, s->stream));
+        }
+        HIP_TRY(launch_bulk(S, r, s->grid, s->stream));
+        if (q == 0 && e1) HIP_TRY(hipEventRecord(e1, s->stream));
+    }
+    int rc;
+    if ((rc = exchange(s, r + 1))) return rc;
+    return finalize(s, r, r + 1);
+}
+
 double alg_bytes(const gp_sim* s) {
-    const DevState& S = s->S;
+    const DevState& S = s->slab[0].S;
     if (S.alg == PUSHSUM) {
         // sw r+w 32, node byte r+w 2 (+ Imp3D in-list: offset 4 + sender 4)
         if (S.topo == IMP3D) return 42.0;
@@ -189,6 +613,158 @@ double alg_bytes(const gp_sim* s) {
     if (S.topo == IMP3D) return 18.0;
     if (S.topo != FULL) return 10.0;
     return 4.0 + 8.0 + 8.0 + 8.0;  // send: c + atomic RMW; recv: inc r+w, c r+w
+}
+
+// Kernel variant and grid for this run (measured defaults, GP_KERNEL / GP_GRID /
+// GP_XSEGS / GP_WALK override for experiments).
+void choose_kernel(gp_sim* s, int64_t nloc_max, int& kernel, uint32_t& col_xsegs, uint32_t& walk) {
+    hipDeviceProp_t prop;
+    (void)hipGetDeviceProperties(&prop, s->device);
+    const gp_config* cfg = &s->cfg;
+    const int64_t g = s->g;
+    const int64_t blocks = (nloc_max + BULK_THREADS - 1) / BULK_THREADS;
+    // 64 workgroups per CU: measured best for the tiled round kernels (tools/ablate.py:
+    // 2048 -> 27.5, 8192 -> 22.1, 16384 -> 21.2 ms/round at P = 1e9)
+    int64_t cap = (int64_t)prop.multiProcessorCount * 64;
+    // (measured, profiles/r01: push-sum -> tiled; gossip on a large lattice -> column march)
+    kernel = KERNEL_TILE;
+    const bool lattice = cfg->topology == GP_3D || cfg->topology == GP_IMP3D;
+    if (lattice && cfg->algorithm == GP_GOSSIP && g >= 200) kernel = KERNEL_COL;
+    if (const char* e = std::getenv("GP_KERNEL")) {
+        if (!std::strcmp(e, "tile")) kernel = KERNEL_TILE;
+        else if (!std::strcmp(e, "wave")) kernel = KERNEL_WAVE;
+        else if (!std::strcmp(e, "col") && lattice) kernel = KERNEL_COL;
+    }
+    col_xsegs = 1;
+    if (cfg->topology != GP_FULL && kernel != KERNEL_TILE) {
+        // exactly the resident grid (a persistent sweep), a multiple of the 8 XCDs
+        const int bpc = kernel == KERNEL_COL ? col_blocks_per_cu(cfg->topology, cfg->algorithm)
+                                             : wave_blocks_per_cu(cfg->topology, cfg->algorithm);
+        cap = (int64_t)prop.multiProcessorCount * bpc;
+        if (kernel == KERNEL_COL) {
+            // x segments per patch: enough work items for every resident wave, >= 16 planes each
+            const int64_t patches = ((g + 63) / 64) * ((g + 3) / 4);
+            const int64_t waves = cap * (BULK_THREADS / 64);
+            const int64_t planes = std::max<int64_t>(1, g / s->world);
+            int64_t xs = std::max<int64_t>(1, waves / std::max<int64_t>(1, patches));
+            xs = std::min<int64_t>(xs, std::max<int64_t>(1, planes / 16));
+            col_xsegs = (uint32_t)xs;
+        }
+    }
+    if (const char* e = std::getenv("GP_GRID")) cap = std::max<int64_t>(1, std::atoll(e));
+    if (const char* e = std::getenv("GP_XSEGS")) col_xsegs = (uint32_t)std::max(1, std::atoi(e));
+    s->grid = (int)std::max<int64_t>(1, std::min(kernel == KERNEL_COL ? cap : blocks, cap));
+    walk = 0;
+    if (const char* e = std::getenv("GP_WALK")) walk = (uint32_t)std::atoi(e);
+}
+
+// Everything after the handle exists: slabs, topology, initial state, round 0.
+int build_sim(gp_sim* s) {
+    int rc;
+    if ((rc = make_bounds(s))) return rc;
+    int64_t nloc_max = 0;
+    for (int w = 0; w < s->world; ++w) nloc_max = std::max<int64_t>(nloc_max, s->bounds[w + 1] - s->bounds[w]);
+    int kernel;
+    uint32_t col_xsegs, walk;
+    choose_kernel(s, nloc_max, kernel, col_xsegs, walk);
+    if (s->mode == MODE_VIRTUAL) {
+        s->slab.resize(s->world);
+        for (int w = 0; w < s->world; ++w) s->slab[w].rank = w;
+    } else {
+        s->slab.resize(1);
+        s->slab[0].rank = s->rank;
+    }
+    for (Slab& sl : s->slab) {
+        sl.S.kernel = kernel;
+        sl.S.col_xsegs = col_xsegs;
+        sl.S.tile_walk = walk;
+        if ((rc = alloc_slab(s, sl, sl.rank))) return rc;
+    }
+    if (s->cfg.topology == GP_IMP3D) {
+        if ((rc = build_imp3d(s))) return rc;
+        if (s->world > 1 && (rc = setup_exchange(s))) return rc;
+    }
+    if (hipHostMalloc((void**)&s->host_ctl, sizeof(Ctl), hipHostMallocDefault) != hipSuccess) {
+        set_err("hipHostMalloc failed");
+        return GP_ENOMEM;
+    }
+    Ctl& init = *s->host_ctl;
+    std::memset(&init, 0, sizeof init);
+    init.active_total = 1;  // the seed
+    init.all_active = s->P <= 1 ? 1u : 0u;
+    init.inj_target = -1;
+    init.inj_pick = -1;
+    for (Slab& sl : s->slab) {
+        DevState& S = sl.S;
+        HIP_TRY(hipMemcpyAsync(S.ctl, &init, sizeof(Ctl), hipMemcpyHostToDevice, s->stream));
+        HIP_TRY(launch_init(S, s->grid, s->stream));
+        if (S.topo == IMP3D)
+            HIP_TRY(S.kernel == KERNEL_COL ? launch_col_rbits_init(S, s->stream)
+                                           : launch_rbits_init(S, s->grid, s->stream));
+        if (S.alg == GOSSIP && S.topo != FULL) HIP_TRY(launch_injector_init(S, s->grid, s->stream));
+    }
+    if ((rc = exchange(s, 0))) return rc;     // halos and random edges of round 0
+    if ((rc = finalize(s, 0, 0))) return rc;  // prepare round 0
+    hipError_t e = hipStreamSynchronize(s->stream);
+    if (e != hipSuccess) {
+        set_err("initialisation failed: %s", hipGetErrorString(e));
+        return GP_EHIP;
+    }
+    if (s->timing) {
+        s->ev.resize(2 * BATCH);
+        for (auto& x : s->ev) HIP_TRY(hipEventCreate(&x));
+    }
+    return GP_OK;
+}
+
+int create_common(const gp_config* cfg, int mode, int world, int rank, const uint8_t* uid, gp_sim** out) {
+    if (!cfg || !out) {
+        set_err("gp_create: null argument");
+        return GP_EINVAL;
+    }
+    *out = nullptr;
+    if (cfg->algorithm != GP_GOSSIP && cfg->algorithm != GP_PUSHSUM) {
+        set_err("option invalid: algorithm id %d", cfg->algorithm);
+        return GP_EINVAL;
+    }
+    int64_t P, T, g;
+    int rc = gp_resolve(cfg->num_nodes, cfg->topology, &P, &T, &g);
+    if (rc) return rc;
+    if ((rc = check_device(cfg->device))) return rc;
+    gp_sim* s = new gp_sim();
+    s->cfg = *cfg;
+    s->device = cfg->device;
+    s->P = P;
+    s->T = T;
+    s->g = g;
+    s->mode = mode;
+    s->world = world;
+    s->rank = rank;
+    s->timing = (cfg->flags & GP_FLAG_KERNEL_TIMING) != 0;
+    if (hipSetDevice(s->device) != hipSuccess || hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
+        set_err("hipSetDevice/hipStreamCreate failed on device %d", s->device);
+        gp_destroy(s);
+        return GP_EHIP;
+    }
+    if (mode == MODE_RCCL) {
+        ncclUniqueId id;
+        std::memcpy(id.internal, uid, NCCL_UNIQUE_ID_BYTES);
+        ncclResult_t r = ncclCommInitRank(&s->comm, world, id, rank);
+        if (r != ncclSuccess) {
+            set_err("ncclCommInitRank(rank %d of %d) failed: %s", rank, world, ncclGetErrorString(r));
+            s->comm = nullptr;
+            gp_destroy(s);
+            return GP_ENCCL;
+        }
+    }
+    if ((rc = build_sim(s))) {
+        const std::string msg = g_err;
+        gp_destroy(s);
+        g_err = msg;
+        return rc;
+    }
+    *out = s;
+    return GP_OK;
 }
 
 }  // namespace
@@ -253,196 +829,37 @@ int gp_create(const gp_config* cfg, gp_sim** out) {
         set_err("gp_create: null argument");
         return GP_EINVAL;
     }
-    *out = nullptr;
-    if (cfg->algorithm != GP_GOSSIP && cfg->algorithm != GP_PUSHSUM) {
-        set_err("option invalid: algorithm id %d", cfg->algorithm);
-        return GP_EINVAL;
-    }
     if (cfg->num_gpus > 1) {
-        set_err("num_gpus > 1: run one process per GPU and use gp_create_rank");
+        if (cfg->flags & GP_FLAG_VIRTUAL_RANKS) return create_common(cfg, MODE_VIRTUAL, cfg->num_gpus, 0, nullptr, out);
+        set_err("num_gpus > 1: run one process per GPU and use gp_create_rank (or GP_FLAG_VIRTUAL_RANKS)");
         return GP_EINVAL;
     }
-    int64_t P, T, g;
-    int rc = gp_resolve(cfg->num_nodes, cfg->topology, &P, &T, &g);
-    if (rc) return rc;
-    if ((rc = check_device(cfg->device))) return rc;
-
-    gp_sim* s = new gp_sim();
-    s->cfg = *cfg;
-    s->device = cfg->device;
-    s->P = P;
-    s->T = T;
-    s->g = g;
-    s->timing = (cfg->flags & GP_FLAG_KERNEL_TIMING) != 0;
-    auto fail = [&](int code) {
-        gp_destroy(s);
-        return code;
-    };
-    if (hipSetDevice(s->device) != hipSuccess || hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
-        set_err("hipSetDevice/hipStreamCreate failed on device %d", s->device);
-        return fail(GP_EHIP);
-    }
-    hipDeviceProp_t prop;
-    (void)hipGetDeviceProperties(&prop, s->device);
-    const int64_t blocks = (P + BULK_THREADS - 1) / BULK_THREADS;
-    // 64 workgroups per CU: measured best for the tiled round kernels (tools/ablate.py:
-    // 2048 -> 27.5, 8192 -> 22.1, 16384 -> 21.2 ms/round at P = 1e9)
-    int64_t cap = (int64_t)prop.multiProcessorCount * 64;
-    // round-kernel variant: column march for lattices with enough patches to fill
-    // the chip, the chunk kernel otherwise (line, small g); GP_KERNEL overrides
-    // (measured, profiles/r01: push-sum -> tiled; gossip on a large lattice -> column march)
-    int kernel = KERNEL_TILE;
-    const bool lattice = cfg->topology == GP_3D || cfg->topology == GP_IMP3D;
-    if (lattice && cfg->algorithm == GP_GOSSIP && g >= 200) kernel = KERNEL_COL;
-    if (const char* e = std::getenv("GP_KERNEL")) {
-        if (!std::strcmp(e, "tile")) kernel = KERNEL_TILE;
-        else if (!std::strcmp(e, "wave")) kernel = KERNEL_WAVE;
-        else if (!std::strcmp(e, "col") && lattice) kernel = KERNEL_COL;
-    }
-    uint32_t col_xsegs = 1;
-    if (cfg->topology != GP_FULL && kernel != KERNEL_TILE) {
-        // exactly the resident grid (a persistent sweep), a multiple of the 8 XCDs
-        const int bpc = kernel == KERNEL_COL ? col_blocks_per_cu(cfg->topology, cfg->algorithm)
-                                             : wave_blocks_per_cu(cfg->topology, cfg->algorithm);
-        cap = (int64_t)prop.multiProcessorCount * bpc;
-        if (kernel == KERNEL_COL) {
-            // x segments per patch: enough work items for every resident wave, >= 16 planes each
-            const int64_t patches = ((g + 63) / 64) * ((g + 3) / 4);
-            const int64_t waves = cap * (BULK_THREADS / 64);
-            int64_t xs = std::max<int64_t>(1, waves / std::max<int64_t>(1, patches));
-            xs = std::min<int64_t>(xs, std::max<int64_t>(1, g / 16));
-            col_xsegs = (uint32_t)xs;
-        }
-    }
-    if (const char* e = std::getenv("GP_GRID")) cap = std::max<int64_t>(1, std::atoll(e));
-    if (const char* e = std::getenv("GP_XSEGS")) col_xsegs = (uint32_t)std::max(1, std::atoi(e));
-    s->grid = (int)std::max<int64_t>(1, std::min(kernel == KERNEL_COL ? cap : blocks, cap));
-
-    DevState& S = s->S;
-    S.topo = cfg->topology;
-    S.alg = cfg->algorithm;
-    S.G.P = (uint32_t)P;
-    S.G.T = (uint32_t)T;
-    S.G.g = (uint32_t)g;
-    S.G.g2 = (uint32_t)(g * g);
-    S.G.div_g = make_fastdiv(S.G.g ? S.G.g : 1);
-    S.G.div_g2 = make_fastdiv(S.G.g2 ? S.G.g2 : 1);
-    S.lo = 0;
-    S.nloc = (uint32_t)P;
-    S.base = 0;
-    S.ext_lo = 0;
-    S.ext_hi = (uint32_t)P;
-    S.rtag = nullptr;
-    S.rmsg = nullptr;
-    S.kernel = kernel;
-    S.col_xsegs = col_xsegs;
-    S.tile_walk = 0;
-    if (const char* e = std::getenv("GP_WALK")) S.tile_walk = (uint32_t)std::atoi(e);
-    S.k0 = (uint32_t)cfg->seed;
-    S.k1 = (uint32_t)(cfg->seed >> 32);
-    // choice = Random().Next(0, nodes) (Program.fs:193,221,263)
-    S.seed_node = uniform(S.k0, S.k1, S_START, 0, 0, (uint32_t)T);
-
-    const size_t Pn = (size_t)P;
-    if ((rc = dev_alloc_t(s, &S.ctl, 1))) return fail(rc);
-    const size_t Pnb = Pn + 1024;  // node-byte arrays: tiles read/write whole words past P
-    if (S.alg == PUSHSUM) {
-        if ((rc = dev_alloc_t(s, &S.sw[0], Pn)) || (rc = dev_alloc_t(s, &S.sw[1], Pn)) ||
-            (rc = dev_alloc_t(s, &S.nb[0], Pnb)))
-            return fail(rc);
-        if (S.topo != FULL && (rc = dev_alloc_t(s, &S.nb[1], Pnb))) return fail(rc);
-    } else {
-        if ((rc = dev_alloc_t(s, &S.c, Pn))) return fail(rc);
-        if (S.topo == FULL) {
-            if ((rc = dev_alloc_t(s, &S.inc, Pn))) return fail(rc);
-        } else {
-            if ((rc = dev_alloc_t(s, &S.nb[0], Pnb)) || (rc = dev_alloc_t(s, &S.nb[1], Pnb))) return fail(rc);
-            S.nchunks = (uint32_t)((T + INJ_CHUNK - 1) / INJ_CHUNK);
-            if ((rc = dev_alloc_t(s, &S.live_bits, (size_t)S.nchunks * (INJ_CHUNK / 32))) ||
-                (rc = dev_alloc_t(s, &S.chunk_live, S.nchunks)))
-                return fail(rc);
-        }
-    }
-    if (S.topo == FULL && S.alg == PUSHSUM) {
-        if ((rc = dev_alloc_t(s, &S.key[0], Pn)) || (rc = dev_alloc_t(s, &S.key[1], Pn)) ||
-            (rc = dev_alloc_t(s, &S.val[0], Pn)) || (rc = dev_alloc_t(s, &S.val[1], Pn)) ||
-            (rc = dev_alloc_t(s, &S.head, Pn)))
-            return fail(rc);
-        S.key_bits = bits_for((uint64_t)P);
-        if (launch_iota(S.val[0], S.G.P, s->grid, s->stream) != hipSuccess) {
-            set_err("iota launch failed");
-            return fail(GP_EHIP);
-        }
-        size_t tb = 0;
-        if (sort_pairs(nullptr, tb, S.key[0], S.key[1], S.val[0], S.val[1], S.G.P, S.key_bits, s->stream) !=
-            hipSuccess) {
-            set_err("rocprim sort sizing failed");
-            return fail(GP_EHIP);
-        }
-        S.sort_tmp_bytes = tb;
-        if ((rc = dev_alloc(s, &S.sort_tmp, tb))) return fail(rc);
-    }
-    if (S.topo == IMP3D) {
-        S.rbits_words = S.kernel == KERNEL_COL ? col_rbits_words(S.nloc / S.G.g2, S.G.g) : rbits_words_for(S.lo, S.nloc);
-        if ((rc = dev_alloc_t(s, &S.rbits[0], S.rbits_words)) || (rc = dev_alloc_t(s, &S.rbits[1], S.rbits_words)))
-            return fail(rc);
-        if ((rc = build_imp3d(s))) return fail(rc);
-    }
-
-    if (hipHostMalloc((void**)&s->host_ctl, sizeof(Ctl), hipHostMallocDefault) != hipSuccess) {
-        set_err("hipHostMalloc failed");
-        return fail(GP_ENOMEM);
-    }
-    std::memset(s->host_ctl, 0, sizeof(Ctl));
-    s->host_ctl->active_total = 1;  // the seed
-    s->host_ctl->all_active = P <= 1 ? 1u : 0u;
-    s->host_ctl->inj_target = -1;
-    if (hipMemcpyAsync(S.ctl, s->host_ctl, sizeof(Ctl), hipMemcpyHostToDevice, s->stream) != hipSuccess ||
-        launch_init(S, s->grid, s->stream) != hipSuccess) {
-        set_err("init launch failed");
-        return fail(GP_EHIP);
-    }
-    if (S.topo == IMP3D && (S.kernel == KERNEL_COL ? launch_col_rbits_init(S, s->stream)
-                                                   : launch_rbits_init(S, s->grid, s->stream)) != hipSuccess) {
-        set_err("random-edge bitmap init failed");
-        return fail(GP_EHIP);
-    }
-    if (S.alg == GOSSIP && S.topo != FULL && launch_injector_init(S, s->grid, s->stream) != hipSuccess) {
-        set_err("injector init launch failed");
-        return fail(GP_EHIP);
-    }
-    if (launch_finalize(S, 0, 0, s->stream) != hipSuccess) {  // prepare round 0
-        set_err("finalize launch failed");
-        return fail(GP_EHIP);
-    }
-    hipError_t e = hipStreamSynchronize(s->stream);
-    if (e != hipSuccess) {
-        set_err("initialisation failed: %s", hipGetErrorString(e));
-        return fail(GP_EHIP);
-    }
-    if (s->timing) {
-        s->ev.resize(2 * BATCH);
-        for (auto& x : s->ev)
-            if (hipEventCreate(&x) != hipSuccess) {
-                set_err("hipEventCreate failed");
-                return fail(GP_EHIP);
-            }
-    }
-    *out = s;
-    return GP_OK;
+    return create_common(cfg, MODE_SINGLE, 1, 0, nullptr, out);
 }
 
 int gp_get_unique_id(uint8_t unique_id[128]) {
-    (void)unique_id;
-    set_err("multi-GPU ranks are not available in this build");
-    return GP_ESTATE;
+    if (!unique_id) {
+        set_err("gp_get_unique_id: null buffer");
+        return GP_EINVAL;
+    }
+    static_assert(NCCL_UNIQUE_ID_BYTES == 128, "RCCL unique id size");
+    ncclUniqueId id;
+    NCCL_TRY(ncclGetUniqueId(&id));
+    std::memcpy(unique_id, id.internal, NCCL_UNIQUE_ID_BYTES);
+    return GP_OK;
 }
 
 int gp_create_rank(const gp_config* cfg, int32_t rank, int32_t world, const uint8_t unique_id[128], gp_sim** out) {
-    (void)unique_id;
-    if (world == 1 && rank == 0) return gp_create(cfg, out);
-    set_err("multi-GPU ranks are not available in this build");
-    return GP_ESTATE;
+    if (!cfg || !out || world < 1 || rank < 0 || rank >= world) {
+        set_err("gp_create_rank: bad argument (rank %d, world %d)", rank, world);
+        return GP_EINVAL;
+    }
+    if (world == 1) return create_common(cfg, MODE_SINGLE, 1, 0, nullptr, out);
+    if (!unique_id) {
+        set_err("gp_create_rank: null unique id");
+        return GP_EINVAL;
+    }
+    return create_common(cfg, MODE_RCCL, world, rank, unique_id, out);
 }
 
 int64_t gp_step(gp_sim* s, int64_t nrounds, int64_t* alerts_out) {
@@ -470,9 +887,14 @@ int64_t gp_step(gp_sim* s, int64_t nrounds, int64_t* alerts_out) {
             int rc = launch_round(s, r, e0, e1);
             if (rc) return rc;
         }
-        HIP_TRY(hipMemcpyAsync(s->host_ctl, s->S.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(hipMemcpyAsync(s->host_ctl, s->slab[0].S.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, s->stream));
         HIP_TRY(hipStreamSynchronize(s->stream));
         const Ctl& hc = *s->host_ctl;
+        if (hc.overflow) {
+            set_err("random-edge exchange buffer overflow (capacity = expected + 12 sigma was exceeded); "
+                    "the rounds of this batch are invalid");
+            return GP_ESTATE;
+        }
         int64_t cum = s->alerts_total, ex = 0;
         for (int64_t k = 0; k < batch; ++k) {
             const int64_t r = s->rounds_done + k;
@@ -544,37 +966,51 @@ int gp_read_state(gp_sim* s, int64_t first, int64_t count, int32_t* c, double* s
         return GP_EINVAL;
     }
     if (count == 0) return GP_OK;
+    if (s->mode == MODE_RCCL) {
+        const Slab& sl = s->slab[0];
+        if (first < sl.S.lo || first + count > sl.hi) {
+            set_err("gp_read_state: range [%lld, %lld) outside this rank's slab [%u, %u)", (long long)first,
+                    (long long)(first + count), sl.S.lo, sl.hi);
+            return GP_EINVAL;
+        }
+    }
     HIP_TRY(hipSetDevice(s->device));
     HIP_TRY(hipStreamSynchronize(s->stream));
-    const DevState& S = s->S;
     const int cur = (int)(s->rounds_done & 1);
-    if (S.alg == PUSHSUM) {
-        std::vector<double2> sw((size_t)count);
-        std::vector<uint8_t> nb((size_t)count);
-        HIP_TRY(hipMemcpy(sw.data(), S.sw[cur] + first, sizeof(double2) * count, hipMemcpyDeviceToHost));
-        const uint8_t* nbsrc = S.topo == FULL ? S.nb[0] : S.nb[cur];
-        HIP_TRY(hipMemcpy(nb.data(), nbsrc + first, count, hipMemcpyDeviceToHost));
-        for (int64_t q = 0; q < count; ++q) {
-            if (c) c[q] = 0;
-            if (sv) sv[q] = sw[q].x;
-            if (wv) wv[q] = sw[q].y;
-            if (flags) {
-                const uint8_t b = nb[q];
-                flags[q] = (uint8_t)(((b & B_ACTIVE) ? 1 : 0) | ((b & B_CONV) ? 2 : 0) | (((b >> CNT_SHIFT) & 3) << 2));
+    for (const Slab& sl : s->slab) {
+        const DevState& S = sl.S;
+        const int64_t a = std::max<int64_t>(first, S.lo), b = std::min<int64_t>(first + count, sl.hi);
+        if (a >= b) continue;
+        const int64_t n = b - a, q0 = a - first;
+        if (S.alg == PUSHSUM) {
+            std::vector<double2> sw((size_t)n);
+            std::vector<uint8_t> nb((size_t)n);
+            HIP_TRY(hipMemcpy(sw.data(), S.sw[cur] + (a - S.base), sizeof(double2) * n, hipMemcpyDeviceToHost));
+            const uint8_t* nbsrc = S.topo == FULL ? S.nb[0] : S.nb[cur];
+            HIP_TRY(hipMemcpy(nb.data(), nbsrc + (a - S.base), n, hipMemcpyDeviceToHost));
+            for (int64_t q = 0; q < n; ++q) {
+                if (c) c[q0 + q] = 0;
+                if (sv) sv[q0 + q] = sw[q].x;
+                if (wv) wv[q0 + q] = sw[q].y;
+                if (flags) {
+                    const uint8_t bb = nb[q];
+                    flags[q0 + q] = (uint8_t)(((bb & B_ACTIVE) ? 1 : 0) | ((bb & B_CONV) ? 2 : 0) |
+                                              (((bb >> CNT_SHIFT) & 3) << 2));
+                }
             }
-        }
-    } else {
-        std::vector<int32_t> cc((size_t)count);
-        HIP_TRY(hipMemcpy(cc.data(), S.c + first, sizeof(int32_t) * count, hipMemcpyDeviceToHost));
-        for (int64_t q = 0; q < count; ++q) {
-            const int64_t i = first + q;
-            const int32_t ci = cc[q];
-            if (c) c[q] = ci;
-            if (sv) sv[q] = 0.0;
-            if (wv) wv[q] = 0.0;
-            if (flags) {
-                const bool act = (i == (int64_t)S.seed_node || ci >= 1) && ci <= 10;
-                flags[q] = (uint8_t)((act ? 1 : 0) | (ci >= 11 ? 2 : 0));
+        } else {
+            std::vector<int32_t> cc((size_t)n);
+            HIP_TRY(hipMemcpy(cc.data(), S.c + (a - S.lo), sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+            for (int64_t q = 0; q < n; ++q) {
+                const int64_t i = a + q;
+                const int32_t ci = cc[q];
+                if (c) c[q0 + q] = ci;
+                if (sv) sv[q0 + q] = 0.0;
+                if (wv) wv[q0 + q] = 0.0;
+                if (flags) {
+                    const bool act = (i == (int64_t)S.seed_node || ci >= 1) && ci <= 10;
+                    flags[q0 + q] = (uint8_t)((act ? 1 : 0) | (ci >= 11 ? 2 : 0));
+                }
             }
         }
     }
@@ -586,7 +1022,7 @@ int gp_neighbors(gp_sim* s, int64_t node, int64_t* out, int64_t cap) {
         set_err("gp_neighbors: bad handle or node");
         return GP_EINVAL;
     }
-    const DevState& S = s->S;
+    const DevState& S = s->slab[0].S;
     const uint32_t j = (uint32_t)node;
     std::vector<int64_t> nb;
     if (S.topo == FULL) {
@@ -597,13 +1033,7 @@ int gp_neighbors(gp_sim* s, int64_t node, int64_t* out, int64_t cap) {
     uint32_t mask = S.topo == LINE ? present_mask<LINE>(j, S.G) : present_mask<GRID3D>(j, S.G);
     for (uint32_t d = 0; d < 6; ++d)
         if (mask & (1u << d)) nb.push_back(S.topo == LINE ? nbr<LINE>(j, d, S.G) : nbr<GRID3D>(j, d, S.G));
-    if (S.topo == IMP3D) {
-        uint32_t r = 0;
-        HIP_TRY(hipSetDevice(s->device));
-        HIP_TRY(hipStreamSynchronize(s->stream));
-        HIP_TRY(hipMemcpy(&r, S.rnd + j, sizeof r, hipMemcpyDeviceToHost));
-        nb.push_back(r);
-    }
+    if (S.topo == IMP3D) nb.push_back(uniform(S.k0, S.k1, S_TOPO, j, 0, S.G.P - 1));  // Program.fs:259
     for (int64_t k = 0; k < std::min<int64_t>((int64_t)nb.size(), cap); ++k) out[k] = nb[(size_t)k];
     return (int)nb.size();
 }
@@ -614,21 +1044,26 @@ int gp_get_info(gp_sim* s, gp_info* o) {
         return GP_EINVAL;
     }
     HIP_TRY(hipSetDevice(s->device));
-    HIP_TRY(hipMemcpyAsync(s->host_ctl, s->S.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipMemcpyAsync(s->host_ctl, s->slab[0].S.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
     o->population = s->P;
     o->threshold = s->T;
     o->grid = s->g;
-    o->seed_node = s->S.seed_node;
+    o->seed_node = s->slab[0].S.seed_node;
     o->rounds = s->rounds_done;
     o->alerts_total = s->alerts_total;
-    o->active = s->S.alg == PUSHSUM ? (int64_t)s->host_ctl->active_total : -1;
-    o->topology = s->S.topo;
-    o->algorithm = s->S.alg;
+    o->active = s->slab[0].S.alg == PUSHSUM ? (int64_t)s->host_ctl->active_total : -1;
+    o->topology = s->cfg.topology;
+    o->algorithm = s->cfg.algorithm;
     o->device = s->device;
-    o->num_gpus = 1;
-    o->slab_first = 0;
-    o->slab_count = s->P;
+    o->num_gpus = s->world;
+    if (s->mode == MODE_RCCL) {
+        o->slab_first = s->slab[0].S.lo;
+        o->slab_count = s->slab[0].S.nloc;
+    } else {
+        o->slab_first = 0;
+        o->slab_count = s->P;
+    }
     return GP_OK;
 }
 
@@ -649,9 +1084,7 @@ int gp_kernel_stats(gp_sim* s, double* total_ms, int64_t* launches, char* name, 
     }
     if (total_ms) *total_ms = s->kernel_ms;
     if (launches) *launches = s->launches;
-    if (name && name_cap > 0) {
-        std::snprintf(name, (size_t)name_cap, "%s", bulk_kernel_name(s->S));
-    }
+    if (name && name_cap > 0) std::snprintf(name, (size_t)name_cap, "%s", bulk_kernel_name(s->slab[0].S));
     if (reset) {
         s->kernel_ms = 0.0;
         s->launches = 0;
@@ -666,6 +1099,7 @@ void gp_destroy(gp_sim* s) {
     (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     for (auto& e : s->ev) (void)hipEventDestroy(e);
+    if (s->comm) (void)ncclCommDestroy(s->comm);
     free_all(s);
     if (s->host_ctl) (void)hipHostFree(s->host_ctl);
     if (s->stream) (void)hipStreamDestroy(s->stream);

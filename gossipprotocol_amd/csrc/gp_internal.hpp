@@ -26,6 +26,10 @@ struct Ctl {
     long long inj_target;             // node the injector delivers to this round, -1 none
     unsigned int done;                // cumulative alerts reached T (Program.fs:53)
     unsigned int all_active;          // every node active at round start (push-sum)
+    unsigned long long xchg[4];       // multi-rank: {alerts, newly active, injector pick converged, 0}, summed over ranks
+    long long inj_pick;               // multi-rank: the injector's pick for the next round (-1 none)
+    unsigned int overflow;            // multi-rank: a random-edge exchange buffer overflowed (run is invalid)
+    unsigned int pad_;
     unsigned long long hist[HIST];    // alerts of round r at hist[r % HIST]
 };
 
@@ -141,10 +145,11 @@ hipError_t launch_rbits_init(const DevState& S, int grid, hipStream_t st);
 
 // ---- kernels (gp_kernels.hip)
 hipError_t launch_init(const DevState& S, int grid, hipStream_t st);
-hipError_t launch_topo_rnd(const DevState& S, int grid, hipStream_t st);
 hipError_t launch_injector_init(const DevState& S, int grid, hipStream_t st);
 hipError_t launch_bulk(const DevState& S, uint32_t round, int grid, hipStream_t st);
 hipError_t launch_finalize(const DevState& S, uint32_t round_done, uint32_t round_next, hipStream_t st);
+hipError_t launch_finalize_pre(const DevState& S, uint32_t round_next, hipStream_t st);
+hipError_t launch_finalize_post(const DevState& S, uint32_t round_done, uint32_t round_next, hipStream_t st);
 hipError_t launch_full_pushsum_send(const DevState& S, uint32_t round, int grid, hipStream_t st);
 hipError_t launch_full_pushsum_mark(const DevState& S, int grid, hipStream_t st);
 hipError_t launch_full_pushsum_recv(const DevState& S, uint32_t round, int grid, hipStream_t st);

@@ -71,10 +71,12 @@ __device__ __forceinline__ uint32_t draw_dir(const DevState& S, uint32_t stream,
 // ---------------------------------------------------------------- init
 // InitialSum x / weight 1.0 / count 1 / rumours 0 (Program.fs:67-71,78,174);
 // only the seed (Program.fs:193) is active in round 0.
+// Slab-aware: the rank's nodes [lo, lo + nloc); node arrays at id - base.
 template <int TOPO, int ALG>
 __global__ __launch_bounds__(BULK_THREADS) void k_init(DevState S) {
-    const uint32_t P = S.G.P;
-    for (uint32_t j = blockIdx.x * BULK_THREADS + threadIdx.x; j < P; j += gridDim.x * BULK_THREADS) {
+    for (uint32_t lj = blockIdx.x * BULK_THREADS + threadIdx.x; lj < S.nloc; lj += gridDim.x * BULK_THREADS) {
+        const uint32_t j = S.lo + lj;
+        const uint32_t jb = j - S.base;
         const bool seed = j == S.seed_node;
         uint32_t dir = DIR_NONE;
         if (TOPO != FULL && seed) {
@@ -82,21 +84,14 @@ __global__ __launch_bounds__(BULK_THREADS) void k_init(DevState S) {
             dir = draw_dir<TOPO>(S, ALG == GOSSIP ? S_GOSSIP : S_PUSHSUM, j, mask, 0);
         }
         if (ALG == PUSHSUM) {
-            S.sw[0][j] = make_double2((double)j, 1.0);
-            S.nb[0][j] = (uint8_t)((1u << CNT_SHIFT) | (seed ? B_ACTIVE : 0u) | dir);
+            S.sw[0][jb] = make_double2((double)j, 1.0);
+            S.nb[0][jb] = (uint8_t)((1u << CNT_SHIFT) | (seed ? B_ACTIVE : 0u) | dir);
         } else {
-            S.c[j] = 0;
-            if (TOPO != FULL) S.nb[0][j] = (uint8_t)dir;
-            else S.inc[j] = 0;
+            S.c[lj] = 0;
+            if (TOPO != FULL) S.nb[0][jb] = (uint8_t)dir;
+            else S.inc[lj] = 0;
         }
     }
-}
-
-// Imp3D random neighbour Random().Next(0, nodes-1) in [0, P-2] (Program.fs:259).
-__global__ __launch_bounds__(BULK_THREADS) void k_topo_rnd(DevState S) {
-    const uint32_t P = S.G.P;
-    for (uint32_t i = blockIdx.x * BULK_THREADS + threadIdx.x; i < P; i += gridDim.x * BULK_THREADS)
-        S.rnd[i] = uniform(S.k0, S.k1, S_TOPO, i, 0, P - 1);
 }
 
 __global__ __launch_bounds__(BULK_THREADS) void k_iota(uint32_t* v, uint32_t n) {
@@ -263,46 +258,18 @@ __device__ uint32_t block_incl_scan(uint32_t v, uint32_t* lds) {
     return v;
 }
 
-// Closes round `round_done` (if has_done) and prepares round `round_next`:
-// scheduler bookkeeping (Program.fs:51-56) and, for gossip on line / 3D /
-// Imp3D, one injector step (Program.fs:150-159): k = U(|L|), t = k-th live id;
-// if t converged remove it, else deliver one rumour to t in round_next.
-__global__ __launch_bounds__(FIN_THREADS) void k_finalize(DevState S, uint32_t round_done, uint32_t round_next,
-                                                          int has_done, int injector) {
+// The injector's list L (Program.fs:147-148) is a bitmap over ids 0..T-1 plus
+// per-chunk live counts, replicated on every rank.  inj_find: the id of the
+// k-th live element (block-wide two-level search), or -1.
+__device__ long long inj_find(const DevState& S, uint32_t k) {
     __shared__ uint32_t lds[FIN_THREADS / 64];
-    __shared__ int sh_skip;
     __shared__ uint32_t sh_chunk, sh_k;
-    __shared__ long long sh_target;
-    Ctl* ctl = S.ctl;
+    __shared__ long long sh_id;
     if (threadIdx.x == 0) {
-        int skip = (int)ld_agent(&ctl->done);
-        if (!skip && has_done) {
-            const unsigned long long a = atomicExch(&ctl->round_alerts, 0ull);
-            const unsigned long long na = atomicExch(&ctl->round_active, 0ull);
-            const unsigned long long tot = ld_agent(&ctl->alerts_total) + a;
-            st_agent(&ctl->alerts_total, tot);
-            ctl->hist[round_done % HIST] = a;
-            const unsigned long long act = ld_agent(&ctl->active_total) + na;
-            st_agent(&ctl->active_total, act);
-            if (act >= S.G.P) st_agent(&ctl->all_active, 1u);
-            if (tot >= S.G.T) {
-                st_agent(&ctl->done, 1u);
-                skip = 1;
-            }
-        }
-        sh_skip = skip;
-        sh_target = -1;
         sh_chunk = 0xFFFFFFFFu;
+        sh_id = -1;
     }
     __syncthreads();
-    if (sh_skip || !injector) return;
-
-    const uint32_t live = (uint32_t)ld_agent(&ctl->live);
-    if (live == 0) {
-        if (threadIdx.x == 0) st_agent(&ctl->inj_target, -1ll);
-        return;
-    }
-    const uint32_t k = uniform(S.k0, S.k1, S_INJECT, 0, round_next, live);
     // phase A: which chunk holds the k-th live id
     const uint32_t nch = S.nchunks;
     const uint32_t per = (nch + FIN_THREADS - 1) / FIN_THREADS;
@@ -325,10 +292,7 @@ __global__ __launch_bounds__(FIN_THREADS) void k_finalize(DevState S, uint32_t r
         }
     }
     __syncthreads();
-    if (sh_chunk >= nch) {  // unreachable when chunk_live sums to live; never index past the bitmap
-        if (threadIdx.x == 0) st_agent(&ctl->inj_target, -1ll);
-        return;
-    }
+    if (sh_chunk >= nch) return -1;  // unreachable when chunk_live sums to live
     // phase B: which bit of the chunk's 2048 words
     const uint32_t chunk = sh_chunk, kk = sh_k;
     constexpr uint32_t WPT = (INJ_CHUNK / 32) / FIN_THREADS;  // words per thread (2)
@@ -351,23 +315,110 @@ __global__ __launch_bounds__(FIN_THREADS) void k_finalize(DevState S, uint32_t r
                 uint32_t m = wv[q];
                 for (uint32_t z = 0; z < rem; ++z) m &= m - 1;  // drop `rem` lowest set bits
                 const uint32_t bit = (uint32_t)__ffs(m) - 1;
-                const uint32_t word = threadIdx.x * WPT + q;
-                const uint32_t id = chunk * INJ_CHUNK + word * 32 + bit;
-                if (S.c[id] >= (int32_t)GOSSIP_DONE) {  // converged: remove (Program.fs:158)
-                    S.live_bits[(size_t)chunk * (INJ_CHUNK / 32) + word] = wv[q] & ~(1u << bit);
-                    S.chunk_live[chunk] -= 1;
-                    st_agent(&ctl->live, (unsigned long long)(live - 1));
-                    sh_target = -1;
-                } else {
-                    sh_target = id;  // Process2 to the pick (Program.fs:155)
-                }
+                sh_id = (long long)chunk * INJ_CHUNK + (threadIdx.x * WPT + q) * 32 + bit;
                 break;
             }
             rem -= pc;
         }
     }
     __syncthreads();
-    if (threadIdx.x == 0) st_agent(&ctl->inj_target, sh_target);
+    return sh_id;
+}
+
+// Remove id from L (Program.fs:158); one thread.
+__device__ void inj_remove(const DevState& S, long long id, uint32_t live) {
+    const uint32_t chunk = (uint32_t)(id / INJ_CHUNK);
+    const uint32_t word = (uint32_t)((id % INJ_CHUNK) / 32), bit = (uint32_t)(id % 32);
+    uint32_t* w = S.live_bits + (size_t)chunk * (INJ_CHUNK / 32) + word;
+    *w = *w & ~(1u << bit);
+    S.chunk_live[chunk] -= 1;
+    st_agent(&S.ctl->live, (unsigned long long)(live - 1));
+}
+
+// Scheduler bookkeeping of round `round_done` from this round's global counts
+// (Program.fs:51-56); returns 1 when the run is over.  One thread.
+__device__ int close_round(const DevState& S, uint32_t round_done, unsigned long long a, unsigned long long na) {
+    Ctl* ctl = S.ctl;
+    const unsigned long long tot = ld_agent(&ctl->alerts_total) + a;
+    st_agent(&ctl->alerts_total, tot);
+    ctl->hist[round_done % HIST] = a;
+    const unsigned long long act = ld_agent(&ctl->active_total) + na;
+    st_agent(&ctl->active_total, act);
+    if (act >= S.G.P) st_agent(&ctl->all_active, 1u);
+    if (tot >= S.G.T) {
+        st_agent(&ctl->done, 1u);
+        return 1;
+    }
+    return 0;
+}
+
+// Single rank: closes round `round_done` (if has_done) and prepares round
+// `round_next`: scheduler bookkeeping and, for gossip on line / 3D / Imp3D, one
+// injector step (Program.fs:150-159): k = U(|L|), t = k-th live id; if t
+// converged remove it, else deliver one rumour to t in round_next.
+__global__ __launch_bounds__(FIN_THREADS) void k_finalize(DevState S, uint32_t round_done, uint32_t round_next,
+                                                          int has_done, int injector) {
+    __shared__ int sh_skip;
+    Ctl* ctl = S.ctl;
+    if (threadIdx.x == 0) {
+        int skip = (int)ld_agent(&ctl->done);
+        if (!skip && has_done)
+            skip = close_round(S, round_done, atomicExch(&ctl->round_alerts, 0ull),
+                               atomicExch(&ctl->round_active, 0ull));
+        sh_skip = skip;
+    }
+    __syncthreads();
+    if (sh_skip || !injector) return;
+    const uint32_t live = (uint32_t)ld_agent(&ctl->live);
+    long long target = -1;
+    if (live) {
+        const long long id = inj_find(S, uniform(S.k0, S.k1, S_INJECT, 0, round_next, live));
+        if (threadIdx.x == 0 && id >= 0) {
+            if (S.c[id - S.lo] >= (int32_t)GOSSIP_DONE) inj_remove(S, id, live);  // converged: remove
+            else target = id;                                                    // Process2 to the pick
+        }
+    }
+    if (threadIdx.x == 0) st_agent(&ctl->inj_target, target);
+}
+
+// Multi-rank, part 1: this rank's counts of round `round_done` go to xchg[0..1];
+// the injector pick for round_next (identical on every rank: L is replicated)
+// goes to inj_pick and xchg[2] = 1 iff this rank owns it and it has converged.
+// xchg is then summed over ranks (RCCL all-reduce) before part 2.
+__global__ __launch_bounds__(FIN_THREADS) void k_finalize_pre(DevState S, uint32_t round_next, int injector) {
+    Ctl* ctl = S.ctl;
+    const int skip = (int)ld_agent(&ctl->done);
+    if (threadIdx.x == 0) {
+        ctl->xchg[0] = skip ? 0ull : atomicExch(&ctl->round_alerts, 0ull);
+        ctl->xchg[1] = skip ? 0ull : atomicExch(&ctl->round_active, 0ull);
+        ctl->xchg[2] = 0ull;
+        ctl->xchg[3] = 0ull;
+        ctl->inj_pick = -1;
+    }
+    if (skip || !injector) return;
+    const uint32_t live = (uint32_t)ld_agent(&ctl->live);
+    if (!live) return;
+    const long long id = inj_find(S, uniform(S.k0, S.k1, S_INJECT, 0, round_next, live));
+    if (threadIdx.x == 0 && id >= 0) {
+        ctl->inj_pick = id;
+        if ((uint64_t)(id - S.lo) < S.nloc && S.c[id - S.lo] >= (int32_t)GOSSIP_DONE) ctl->xchg[2] = 1ull;
+    }
+}
+
+// Multi-rank, part 2: global bookkeeping from the summed xchg, then apply the
+// injector pick (remove from the replicated L if converged, else deliver).
+__global__ void k_finalize_post(DevState S, uint32_t round_done, int has_done, int injector) {
+    Ctl* ctl = S.ctl;
+    if (threadIdx.x != 0) return;
+    if (ld_agent(&ctl->done)) return;
+    if (has_done && close_round(S, round_done, ctl->xchg[0], ctl->xchg[1])) return;
+    long long target = -1;
+    const long long id = ctl->inj_pick;
+    if (injector && id >= 0) {
+        if (ctl->xchg[2]) inj_remove(S, id, (uint32_t)ld_agent(&ctl->live));
+        else target = id;
+    }
+    st_agent(&ctl->inj_target, target);
 }
 
 // ---------------------------------------------------------------- launchers
@@ -389,11 +440,6 @@ hipError_t launch_init(const DevState& S, int grid, hipStream_t st) {
         }
     }
 #undef GP_INIT
-    return hipGetLastError();
-}
-
-hipError_t launch_topo_rnd(const DevState& S, int grid, hipStream_t st) {
-    hipLaunchKernelGGL(k_topo_rnd, dim3(grid), dim3(BULK_THREADS), 0, st, S);
     return hipGetLastError();
 }
 
@@ -443,6 +489,19 @@ const char* bulk_kernel_name(const DevState& S) {
                                     "k_gossip_col<IMP3D>"}};
     const int v = S.kernel;
     return S.alg == PUSHSUM ? ps[v][S.topo] : go[v][S.topo];
+}
+
+hipError_t launch_finalize_pre(const DevState& S, uint32_t round_next, hipStream_t st) {
+    const int injector = (S.alg == GOSSIP && S.topo != FULL) ? 1 : 0;
+    hipLaunchKernelGGL(k_finalize_pre, dim3(1), dim3(FIN_THREADS), 0, st, S, round_next, injector);
+    return hipGetLastError();
+}
+
+hipError_t launch_finalize_post(const DevState& S, uint32_t round_done, uint32_t round_next, hipStream_t st) {
+    const int has_done = round_next > 0;
+    const int injector = (S.alg == GOSSIP && S.topo != FULL) ? 1 : 0;
+    hipLaunchKernelGGL(k_finalize_post, dim3(1), dim3(64), 0, st, S, round_done, has_done, injector);
+    return hipGetLastError();
 }
 
 hipError_t launch_finalize(const DevState& S, uint32_t round_done, uint32_t round_next, hipStream_t st) {

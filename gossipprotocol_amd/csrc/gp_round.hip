@@ -333,7 +333,10 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
             }
             if (TOPO == IMP3D) {
                 const unsigned long long bits = __ballot(valid && dir == DIR_RANDOM);
-                if (lane == 0) a.rbn[((T + k * TPB + (threadIdx.x & ~63u)) >> 6) - (a.lo >> 6)] = bits;
+                if (lane == 0) {  // the slab's first tile may start below lo: no word there
+                    const int64_t wi = (int64_t)((T + k * TPB + (threadIdx.x & ~63u)) >> 6) - (int64_t)(a.lo >> 6);
+                    if (wi >= 0) a.rbn[wi] = bits;
+                }
             }
         }
         __syncthreads();
@@ -491,7 +494,10 @@ __global__ __launch_bounds__(TPB) void k_gossip_tile(RoundArgs a, uint32_t r) {
             }
             if (TOPO == IMP3D) {
                 const unsigned long long bits = __ballot(valid && dir == DIR_RANDOM);
-                if (lane == 0) a.rbn[((T + k * TPB + (threadIdx.x & ~63u)) >> 6) - (a.lo >> 6)] = bits;
+                if (lane == 0) {  // the slab's first tile may start below lo: no word there
+                    const int64_t wi = (int64_t)((T + k * TPB + (threadIdx.x & ~63u)) >> 6) - (int64_t)(a.lo >> 6);
+                    if (wi >= 0) a.rbn[wi] = bits;
+                }
             }
         }
         __syncthreads();

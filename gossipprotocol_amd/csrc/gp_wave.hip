@@ -227,7 +227,10 @@ __global__ __launch_bounds__(BULK_THREADS) void k_ps_wave(WaveArgs a, uint32_t r
             }
             if (TOPO == IMP3D && !all_active) {
                 const unsigned long long bits = __ballot(valid && dir == DIR_RANDOM);
-                if (lane == 0) a.rbn[((c0 + k * 64) >> 6) - (lo >> 6)] = bits;
+                if (lane == 0) {  // the slab's first chunk may start below lo: no word there
+                    const int64_t wi = (int64_t)((c0 + k * 64) >> 6) - (int64_t)(lo >> 6);
+                    if (wi >= 0) a.rbn[wi] = bits;
+                }
             }
             __builtin_amdgcn_sched_barrier(0);  // one node's gathers live at a time (VGPR budget)
         }
@@ -342,7 +345,10 @@ __global__ __launch_bounds__(BULK_THREADS) void k_gossip_wave(WaveArgs a, uint32
             if (valid) a.nbn[j - base] = (uint8_t)dir;
             if (TOPO == IMP3D) {
                 const unsigned long long bits = __ballot(valid && dir == DIR_RANDOM);
-                if (lane == 0) a.rbn[((c0 + k * 64) >> 6) - (lo >> 6)] = bits;
+                if (lane == 0) {  // the slab's first chunk may start below lo: no word there
+                    const int64_t wi = (int64_t)((c0 + k * 64) >> 6) - (int64_t)(lo >> 6);
+                    if (wi >= 0) a.rbn[wi] = bits;
+                }
             }
         }
         if (TOPO == IMP3D) wave_lds_sync();

@@ -41,16 +41,21 @@ class Simulation:
 
     def __init__(self, num_nodes: int, topology: str, algorithm: str, seed: int = 1,
                  max_rounds: int = 0, device: int = 0, kernel_timing: bool = False,
-                 rank: int = 0, world: int = 1, dist=None):
+                 rank: int = 0, world: int = 1, dist=None, virtual_ranks: int = 1):
+        """world > 1: this process is rank `rank` of a one-process-per-GPU run
+        (RCCL; `dist` is a torch.distributed group used once to share the RCCL
+        id).  virtual_ranks > 1: that many slabs in this process on `device`,
+        exchanging through device copies (the multi-GPU path on one GPU)."""
         cfg = L.GpConfig()
         cfg.num_nodes = num_nodes
         cfg.topology = parse_topology(topology)
         cfg.algorithm = parse_algorithm(algorithm)
         cfg.seed = seed
-        cfg.num_gpus = 1
+        cfg.num_gpus = max(1, virtual_ranks)
         cfg.device = device
         cfg.max_rounds = max_rounds
-        cfg.flags = L.GP_FLAG_KERNEL_TIMING if kernel_timing else 0
+        cfg.flags = (L.GP_FLAG_KERNEL_TIMING if kernel_timing else 0) | \
+            (L.GP_FLAG_VIRTUAL_RANKS if virtual_ranks > 1 else 0)
         self.topology, self.algorithm = topology, algorithm
         h = C.c_void_p()
         if world > 1:

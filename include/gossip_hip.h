@@ -48,7 +48,9 @@ enum {
 };
 /* gp_config.flags */
 enum {
-    GP_FLAG_KERNEL_TIMING = 1 /* bracket every round kernel with HIP events (gp_kernel_stats) */
+    GP_FLAG_KERNEL_TIMING = 1, /* bracket every round kernel with HIP events (gp_kernel_stats) */
+    GP_FLAG_VIRTUAL_RANKS = 2  /* num_gpus > 1 slabs in this process on `device` (the multi-GPU
+                                  exchange with device copies instead of RCCL; for testing) */
 };
 
 typedef struct gp_sim gp_sim;
@@ -59,7 +61,8 @@ typedef struct gp_config {
     int32_t topology;    /* GP_LINE .. GP_IMP3D (argv[1], Program.fs:33) */
     int32_t algorithm;   /* GP_GOSSIP | GP_PUSHSUM (argv[2], Program.fs:34) */
     uint64_t seed;       /* Philox key; replaces `new Random()` (Program.fs:86 et al.) */
-    int32_t num_gpus;    /* GPUs driven by this process; 1 in this release (multi-GPU: one process per GPU, gp_create_rank) */
+    int32_t num_gpus;    /* 1; multi-GPU runs one process per GPU (gp_create_rank), or num_gpus
+                            in-process slabs with GP_FLAG_VIRTUAL_RANKS */
     int32_t device;      /* HIP device ordinal for num_gpus == 1 */
     int64_t max_rounds;  /* cap; <= 0 means unlimited (the reference blocks forever, Program.fs:282) */
     int32_t flags;       /* GP_FLAG_* */
