@@ -560,7 +560,7 @@ int exchange(gp_sim* s, uint32_t rn) {
 
 // Close round `round_done` (if round_next > 0) and prepare round `round_next`.
 int finalize(gp_sim* s, uint32_t round_done, uint32_t round_next) {
-    if (s->world == 1) {
+    if (s->mode == MODE_SINGLE) {
         HIP_TRY(launch_finalize(s->slab[0].S, round_done, round_next, s->stream));
         return GP_OK;
     }
@@ -854,7 +854,10 @@ int gp_create_rank(const gp_config* cfg, int32_t rank, int32_t world, const uint
         set_err("gp_create_rank: bad argument (rank %d, world %d)", rank, world);
         return GP_EINVAL;
     }
-    if (world == 1) return create_common(cfg, MODE_SINGLE, 1, 0, nullptr, out);
+    // GP_FORCE_RCCL=1: a one-rank RCCL communicator (smoke test of the RCCL
+    // transport on a single GPU: init, bookkeeping all-reduce, teardown)
+    const char* force = std::getenv("GP_FORCE_RCCL");
+    if (world == 1 && !(force && force[0] == '1')) return create_common(cfg, MODE_SINGLE, 1, 0, nullptr, out);
     if (!unique_id) {
         set_err("gp_create_rank: null unique id");
         return GP_EINVAL;

@@ -11,6 +11,7 @@ tests.  Every call goes to libgossip_hip.so; there is no CPU path here.
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -58,7 +59,7 @@ class Simulation:
             (L.GP_FLAG_VIRTUAL_RANKS if virtual_ranks > 1 else 0)
         self.topology, self.algorithm = topology, algorithm
         h = C.c_void_p()
-        if world > 1:
+        if world > 1 or (world == 1 and dist is not None and os.environ.get("GP_FORCE_RCCL") == "1"):
             # one process per GPU: rank 0 makes the RCCL id, the caller's process
             # group (gloo is enough) broadcasts it, every rank joins its slab
             uid = C.create_string_buffer(128)

@@ -1,0 +1,369 @@
+"""CPU emulation of the multi-rank exchange protocol of libgossip_hip.so.
+
+TEST INFRASTRUCTURE ONLY (tests/test_multirank_gloo.py).  Each torch.distributed
+(gloo) rank owns the slab of node ids the library would give it
+(gp_api.hip make_bounds: whole x-planes for 3D / Imp3D, contiguous ids for
+line) and runs SRS v1 rounds for its slab with numpy, talking to the other
+ranks only through the library's exchange plan:
+
+  * halo refresh: after every round the boundary plane (line: node) of node
+    bytes -- here the direction / active fields -- and (s, w) goes to the
+    neighbouring rank (gp_api.hip exchange, halo part);
+  * random-edge messages: every sender whose next direction is its random edge
+    and whose target lives on another rank sends {slot, s, w} with `slot` =
+    the message's position in the destination's receiver-sorted in-edge array,
+    computed from the global stable sort exactly like build_imp3d / k_make_pos;
+    the receiver tags rtag[slot] = round (gp_xchg.hip k_pack / k_unpack);
+  * bookkeeping: {alerts, newly active, injector pick converged} summed over
+    ranks (k_finalize_pre / all-reduce / k_finalize_post); the gossip
+    injector's live list is replicated on every rank.
+
+It never calls the HIP library: it checks the decomposition itself (slab
+plan, slot arithmetic, fold order with remote messages, replicated injector)
+against the single-process CPU oracle.  Vectorised Philox4x32-10 follows
+oracle/srs_py.py (itself pinned by the Random123 known-answer vectors).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+M0, M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
+MASK = np.uint64(0xFFFFFFFF)
+S_TOPO, S_START, S_GOSSIP, S_PUSHSUM, S_INJECT = 0, 1, 2, 3, 4
+DIR_NONE, DIR_RANDOM = 7, 6
+
+
+def uniform(seed, stream, node, rnd, m):
+    """U(m) for arrays of node ids (ctr = (node, round, stream, 0), key = seed)."""
+    node = np.asarray(node, dtype=np.uint64)
+    c0 = node & MASK
+    c1 = np.full_like(node, np.uint64(rnd) & MASK)
+    c2 = np.full_like(node, np.uint64(stream))
+    c3 = node >> np.uint64(32)
+    k0, k1 = seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF
+    for r in range(10):
+        if r:
+            k0 = (k0 + 0x9E3779B9) & 0xFFFFFFFF
+            k1 = (k1 + 0xBB67AE85) & 0xFFFFFFFF
+        p0 = M0 * c0
+        p1 = M1 * c2
+        c0, c1, c2, c3 = ((p1 >> np.uint64(32)) ^ c1 ^ np.uint64(k0)) & MASK, p1 & MASK, \
+            ((p0 >> np.uint64(32)) ^ c3 ^ np.uint64(k1)) & MASK, p0 & MASK
+    m = np.asarray(m, dtype=np.uint64)
+    lo = c0 * m
+    hi = c1 * m + (lo >> np.uint64(32))
+    return (hi >> np.uint64(32)).astype(np.int64)
+
+
+def resolve(n, topo):
+    if topo in ("line", "full"):
+        return n + 1, n, 0
+    g = int(round(n ** (1 / 3)))
+    while g > 0 and g ** 3 >= n:
+        g -= 1
+    while g ** 3 < n:
+        g += 1
+    return g ** 3, g ** 3, g
+
+
+class Geometry:
+    """Implicit neighbours in the reference's slot order (Program.fs:182-191,246-260)."""
+
+    def __init__(self, P, g, topo, seed):
+        self.P, self.g, self.topo, self.seed = P, g, topo, seed
+        self.ND = 2 if topo == "line" else 6
+
+    def nbr(self, j, d):
+        """Neighbour of ids j in direction d, or -1 if absent."""
+        j = np.asarray(j, dtype=np.int64)
+        if self.topo == "line":
+            out = j - 1 if d == 0 else j + 1
+            return np.where((out >= 0) & (out < self.P), out, -1)
+        g, g2 = self.g, self.g * self.g
+        x, y, z = j // g2, (j // g) % g, j % g
+        off, ok = [(-g2, x > 0), (g2, x < g - 1), (g, y < g - 1), (-g, y > 0), (1, z < g - 1), (-1, z > 0)][d]
+        return np.where(ok, j + off, -1)
+
+    def mask(self, j):
+        m = np.zeros(len(j), dtype=np.int64)
+        for d in range(self.ND):
+            m |= (self.nbr(j, d) >= 0).astype(np.int64) << d
+        return m
+
+    def degree(self, j):
+        deg = np.zeros(len(j), dtype=np.int64)
+        for d in range(self.ND):
+            deg += self.nbr(j, d) >= 0
+        return deg + (1 if self.topo == "Imp3D" else 0)
+
+    def draw_dir(self, j, stream, rnd):
+        """Direction each id in j sends in during round rnd (slot order -> direction)."""
+        mask = self.mask(j)
+        deg = self.degree(j)
+        k = uniform(self.seed, stream, j, rnd, np.maximum(deg, 1))
+        out = np.full(len(j), DIR_NONE, dtype=np.int64)
+        for d in range(self.ND):              # slot k -> k-th present direction
+            has = (mask >> d) & 1 == 1
+            take = has & (k == 0) & (out == DIR_NONE)
+            out[take] = d
+            k = np.where(has & (out == DIR_NONE), k - 1, k)
+        if self.topo == "Imp3D":
+            out[(out == DIR_NONE) & (deg > 0)] = DIR_RANDOM
+        out[deg == 0] = DIR_NONE
+        return out
+
+
+def slab_bounds(P, g, topo, W):
+    """gp_api.hip make_bounds."""
+    if topo == "line":
+        return [P * w // W for w in range(W + 1)], 1
+    return [(g * w // W) * g * g for w in range(W + 1)], g * g
+
+
+class RankSim:
+    """One rank's slab, advanced in synchronous rounds through the exchange plan."""
+
+    def __init__(self, n, topo, alg, seed, rank, world, dist):
+        self.topo, self.alg, self.seed, self.rank, self.W, self.dist = topo, alg, seed, rank, world, dist
+        self.P, self.T, self.g = resolve(n, topo)
+        self.G = Geometry(self.P, self.g, topo, seed)
+        self.bounds, self.H = slab_bounds(self.P, self.g, topo, world)
+        self.lo, self.hi = self.bounds[rank], self.bounds[rank + 1]
+        self.ext_lo = self.lo - self.H if rank > 0 else self.lo
+        self.ext_hi = self.hi + self.H if rank < world - 1 else self.hi
+        self.ids = np.arange(self.lo, self.hi, dtype=np.int64)
+        self.seed_node = int(uniform(seed, S_START, np.array([0]), 0, self.T)[0])
+        n_ext = self.ext_hi - self.ext_lo
+        self.dir = np.full(n_ext, DIR_NONE, dtype=np.int64)      # direction of the current round (ext)
+        self.round = 0
+        self.alerts_total = 0
+        self.done = False
+        if topo == "Imp3D":
+            self._build_inlists()
+        if alg == "push-sum":
+            self.s = np.arange(self.ext_lo, self.ext_hi, dtype=np.float64)
+            self.w = np.ones(n_ext)
+            self.active = np.zeros(n_ext, dtype=bool)
+            self.cnt = np.ones(self.hi - self.lo, dtype=np.int64)
+            self.conv = np.zeros(self.hi - self.lo, dtype=bool)
+            if self.lo <= self.seed_node < self.hi:
+                self.active[self.seed_node - self.ext_lo] = True
+                self.dir[self.seed_node - self.ext_lo] = self.G.draw_dir(np.array([self.seed_node]), S_PUSHSUM, 0)[0]
+            self.active_total = 1
+        else:
+            self.c = np.zeros(self.hi - self.lo, dtype=np.int64)
+            if self.lo <= self.seed_node < self.hi:
+                self.dir[self.seed_node - self.ext_lo] = self.G.draw_dir(np.array([self.seed_node]), S_GOSSIP, 0)[0]
+            self.live = list(range(self.T)) if topo != "full" else None
+        self._exchange(0)
+        if alg == "gossip":
+            self._prepare_injector(0)
+
+    # ---------------------------------------------------------------- topology
+    def _build_inlists(self):
+        P = self.P
+        rnd_all = uniform(self.seed, S_TOPO, np.arange(P), 0, P - 1)   # Program.fs:259
+        order = np.argsort(rnd_all, kind="stable")                     # senders ascending per receiver
+        off_all = np.zeros(P + 1, dtype=np.int64)
+        np.add.at(off_all, rnd_all + 1, 1)
+        off_all = np.cumsum(off_all)
+        inv = np.empty(P, dtype=np.int64)
+        inv[order] = np.arange(P)
+        edge0 = off_all[self.bounds]
+        self.in_off = off_all[self.lo:self.hi + 1] - edge0[self.rank]
+        self.in_src = order[edge0[self.rank]:edge0[self.rank + 1]]
+        self.rnd = rnd_all[self.lo:self.hi]
+        self.owner = np.searchsorted(np.array(self.bounds[1:-1]), self.rnd, side="right")
+        # slot of each local sender's message in its target owner's in-edge array (k_make_pos)
+        self.pos = inv[self.lo:self.hi] - edge0[self.owner]
+        ne = len(self.in_src)
+        self.rtag = np.full(ne, -1, dtype=np.int64)
+        self.rmsg = np.zeros((ne, 2))
+
+    def _local(self, ids):
+        return ids - self.ext_lo
+
+    # ---------------------------------------------------------------- exchange
+    def _exchange(self, rn):
+        """Halo refresh + random-edge messages for round rn (state already in place)."""
+        import torch
+        d = self.dist
+        fields = [self.dir] + ([self.s, self.w, self.active.astype(np.float64)] if self.alg == "push-sum" else [])
+        H = self.H
+        if self.W > 1:
+            lo_l, hi_l = self.lo - self.ext_lo, self.hi - self.ext_lo
+            out = {}
+            if self.rank > 0:
+                out[self.rank - 1] = [f[lo_l:lo_l + H].astype(np.float64) for f in fields]
+            if self.rank < self.W - 1:
+                out[self.rank + 1] = [f[hi_l - H:hi_l].astype(np.float64) for f in fields]
+            got = [None] * self.W
+            d.all_gather_object(got, out)
+            for src, payload in enumerate(got):
+                if self.rank not in payload:
+                    continue
+                for f, v in zip(fields, payload[self.rank]):
+                    if src == self.rank - 1:
+                        f[:H] = v.astype(f.dtype)
+                    else:
+                        f[hi_l:hi_l + H] = v.astype(f.dtype)
+            if self.alg == "push-sum":
+                self.active = fields[3].astype(bool)
+        if self.topo == "Imp3D" and self.W > 1:
+            mydir = self.dir[self._local(self.ids)]
+            send = (mydir == DIR_RANDOM) & (self.owner != self.rank)
+            packets = {}
+            for p in range(self.W):
+                sel = send & (self.owner == p)
+                if self.alg == "push-sum":
+                    li = self._local(self.ids[sel])
+                    packets[p] = (self.pos[sel], self.s[li], self.w[li])
+                else:
+                    packets[p] = (self.pos[sel],)
+            got = [None] * self.W
+            d.all_gather_object(got, packets)
+            for src, pk in enumerate(got):
+                if src == self.rank:
+                    continue
+                msg = pk[self.rank]
+                self.rtag[msg[0]] = rn
+                if self.alg == "push-sum":
+                    self.rmsg[msg[0], 0] = msg[1]
+                    self.rmsg[msg[0], 1] = msg[2]
+        _ = torch  # gloo transport via torch.distributed
+
+    def _allreduce(self, vals):
+        import torch
+        t = torch.tensor(vals, dtype=torch.int64)
+        if self.W > 1:
+            self.dist.all_reduce(t)
+        return [int(v) for v in t.tolist()]
+
+    # ---------------------------------------------------------------- rounds
+    def _random_in(self, r):
+        """Per local in-edge: did the sender use its random edge in round r?"""
+        src = self.in_src
+        local = (src >= self.lo) & (src < self.hi)
+        sent = np.zeros(len(src), dtype=bool)
+        sent[local] = self.dir[self._local(src[local])] == DIR_RANDOM
+        sent[~local] = self.rtag[~local] == r
+        return sent, local
+
+    def _pushsum_round(self):
+        r = self.round
+        j = self.ids
+        lj = self._local(j)
+        deg = self.G.degree(j)
+        act = self.active[lj]
+        halve = act & (deg > 0)
+        acc_s = np.where(halve, self.s[lj] * 0.5, self.s[lj])
+        acc_w = np.where(halve, self.w[lj] * 0.5, self.w[lj])
+        recv = np.zeros(len(j), dtype=bool)
+        for d in range(self.G.ND):            # lattice slots in the receiver's order
+            n = self.G.nbr(j, d)
+            ok = n >= 0
+            ln = self._local(np.where(ok, n, self.lo))
+            hit = ok & (self.dir[ln] == (d ^ 1))
+            acc_s = np.where(hit, acc_s + self.s[ln] * 0.5, acc_s)
+            acc_w = np.where(hit, acc_w + self.w[ln] * 0.5, acc_w)
+            recv |= hit
+        if self.topo == "Imp3D":              # random edges, ascending sender
+            sent, local = self._random_in(r)
+            val_s = np.zeros(len(sent))
+            val_w = np.zeros(len(sent))
+            ls = self._local(self.in_src[local])
+            val_s[local], val_w[local] = self.s[ls], self.w[ls]
+            val_s[~local], val_w[~local] = self.rmsg[~local, 0], self.rmsg[~local, 1]
+            indeg = np.diff(self.in_off)
+            for k in range(int(indeg.max()) if len(indeg) else 0):
+                has = indeg > k
+                e = np.where(has, self.in_off[:-1] + k, 0)
+                hit = has & sent[e]
+                acc_s = np.where(hit, acc_s + val_s[e] * 0.5, acc_s)
+                acc_w = np.where(hit, acc_w + val_w[e] * 0.5, acc_w)
+                recv |= hit
+        r_old = self.s[lj] / self.w[lj]
+        r_new = acc_s / acc_w
+        upd = recv & ~self.conv
+        self.cnt = np.where(upd, np.where(np.abs(r_new - r_old) > 1e-10, 0, self.cnt + 1), self.cnt)
+        newc = upd & (self.cnt == 3)
+        self.conv |= newc
+        newly = recv & ~act
+        self.active[lj] |= recv
+        self.s[lj], self.w[lj] = acc_s, acc_w
+        nd = self.G.draw_dir(j, S_PUSHSUM, r + 1)
+        self.dir[:] = DIR_NONE
+        self.dir[lj] = np.where(self.active[lj] & (deg > 0), nd, DIR_NONE)
+        self._exchange(r + 1)
+        alerts, na, _ = self._allreduce([int(newc.sum()), int(newly.sum()), 0])
+        self.active_total += na
+        return alerts
+
+    def _prepare_injector(self, rn):
+        """Injector pick for round rn on the replicated live list (Program.fs:150-159)."""
+        self.inj = -1
+        if self.live is None or not self.live:
+            self._allreduce([0, 0, 0])
+            return
+        t = self.live[int(uniform(self.seed, S_INJECT, np.array([0]), rn, len(self.live))[0])]
+        mine = self.lo <= t < self.hi and self.c[t - self.lo] >= 11
+        conv = self._allreduce([0, 0, int(mine)])[2]
+        if conv:
+            self.live.remove(t)
+        else:
+            self.inj = t
+
+    def _gossip_round(self):
+        r = self.round
+        j = self.ids
+        lj = self._local(j)
+        conv = self.c >= 11
+        inc = np.zeros(len(j), dtype=np.int64)
+        for d in range(self.G.ND):
+            n = self.G.nbr(j, d)
+            ok = n >= 0
+            ln = self._local(np.where(ok, n, self.lo))
+            inc += ok & (self.dir[ln] == (d ^ 1))
+        if self.topo == "Imp3D":
+            sent, _ = self._random_in(r)
+            indeg = np.diff(self.in_off)
+            for k in range(int(indeg.max()) if len(indeg) else 0):
+                has = indeg > k
+                e = np.where(has, self.in_off[:-1] + k, 0)
+                inc += has & sent[e]
+        if self.lo <= self.inj < self.hi:
+            inc[self.inj - self.lo] += 1
+        inc[conv] = 0                                   # dropped at converged receivers (Program.fs:87)
+        alerts_local = int(((self.c <= 10) & (self.c + inc > 10) & (inc > 0)).sum())
+        self.c += inc
+        active = ((j == self.seed_node) | (self.c >= 1)) & (self.c <= 10)
+        nd = self.G.draw_dir(j, S_GOSSIP, r + 1)
+        deg = self.G.degree(j)
+        self.dir[:] = DIR_NONE
+        self.dir[lj] = np.where(active & (deg > 0), nd, DIR_NONE)
+        self._exchange(r + 1)
+        alerts = self._allreduce([alerts_local, 0, 0])[0]
+        self._prepare_injector(r + 1)
+        return alerts
+
+    def step(self, nrounds):
+        out = []
+        while len(out) < nrounds and not self.done:
+            a = self._gossip_round() if self.alg == "gossip" else self._pushsum_round()
+            out.append(a)
+            self.alerts_total += a
+            self.round += 1
+            if self.alerts_total >= self.T:
+                self.done = True
+        return out
+
+    def state(self):
+        """This rank's slab: (lo, c or None, s, w, flags) in the library's flag encoding."""
+        lj = self._local(self.ids)
+        if self.alg == "gossip":
+            act = ((self.ids == self.seed_node) | (self.c >= 1)) & (self.c <= 10)
+            flags = act.astype(np.uint8) | ((self.c >= 11).astype(np.uint8) << 1)
+            return self.lo, self.c.astype(np.int32), None, None, flags
+        flags = self.active[lj].astype(np.uint8) | (self.conv.astype(np.uint8) << 1) | \
+            (self.cnt.astype(np.uint8) << 2)
+        return self.lo, None, self.s[lj].copy(), self.w[lj].copy(), flags
