@@ -32,7 +32,8 @@ namespace gp {
 #define GP_ABLATE 0
 #endif
 #ifndef GP_MINB
-#define GP_MINB 1  // __launch_bounds__ minimum waves per SIMD (= resident 256-thread blocks per CU)
+#define GP_MINB 5  // __launch_bounds__ minimum waves per SIMD (= resident 256-thread blocks per CU):
+                   // the LDS tile allows 5, so keep VGPRs <= 96 to not lose the fifth
 #endif
 #define ABL_NO_RGATHER 1   // in-list: decide but do not gather the sender's (s, w)
 #define ABL_NO_LGATHER 2   // lattice: decide but do not gather
@@ -41,6 +42,7 @@ namespace gp {
 #define ABL_NO_EPHILOX 16  // in-list: no Philox (sender never random)
 #define ABL_BITMAP_ONLY 32 // in-list: always read the random-edge bitmap, never recompute Philox
 #define ABL_NO_RATIO 64    // skip the ratio test
+#define ABL_CHEAP_DECIDE 128  // in-list: a one-multiply hash instead of the sender's Philox draw
 
 namespace {
 
@@ -116,7 +118,9 @@ __device__ __forceinline__ double2 ld_sw(const double2* p) { return *p; }
 }  // namespace
 
 // ---------------------------------------------------------------- push-sum
-template <int TOPO>
+// REMOTE: some in-edge senders live on other ranks (multi-GPU slabs); the
+// single-GPU build of the kernel has no exchange-tag paths at all.
+template <int TOPO, bool REMOTE>
 __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t r) {
     __shared__ TileLds L;
     Ctl* ctl = a.ctl;
@@ -191,10 +195,12 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                     const uint32_t i = isrc[m];
                     bool sent = false;
                     if (q < cnt) {
-                        if (i - a.lo >= a.nloc) {  // sender on another rank: the exchange tagged its message
+                        if (REMOTE && i - a.lo >= a.nloc) {  // sender on another rank: the exchange tagged its message
                             sent = a.rtag[e_lo + q] == r;
                         } else if (GP_ABLATE & ABL_NO_EPHILOX) {
                             sent = false;
+                        } else if ((GP_ABLATE & ABL_CHEAP_DECIDE) && all_active) {
+                            sent = ((i * 2654435761u + r * 40503u) >> 29) == 0u;
                         } else if (all_active && !(GP_ABLATE & ABL_BITMAP_ONLY)) {
                             const uint32_t di = popc6(present_mask<IMP3D>(i, G)) + 1u;
                             sent = uniform(a.k0, a.k1, S_PUSHSUM, i, r, di) == di - 1u;
@@ -211,7 +217,7 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                     if (snt[m]) {
                         const uint32_t q = threadIdx.x + m * TPB;
                         v[m] = (GP_ABLATE & ABL_NO_RGATHER) ? make_double2((double)isrc[m], 1.0)
-                               : (isrc[m] - a.lo >= a.nloc) ? a.rmsg[e_lo + q] : ld_sw(swc + isrc[m]);
+                               : (REMOTE && isrc[m] - a.lo >= a.nloc) ? a.rmsg[e_lo + q] : ld_sw(swc + isrc[m]);
                     }
                 }
                 const uint32_t wbase = (threadIdx.x >> 6) * WCAP;
@@ -283,11 +289,11 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                             if (p < (uint16_t)MSG_CAP) mi = L.msg[p];
                             else if (p == POS_GLOBAL) {
                                 const uint32_t i = L.src[e - e_lo];
-                                mi = (i - a.lo >= a.nloc) ? a.rmsg[e] : ld_sw(swc + i);
+                                mi = (REMOTE && i - a.lo >= a.nloc) ? a.rmsg[e] : ld_sw(swc + i);
                             }
                         } else {  // rare: tile in-degree above SRC_CAP
                             const uint32_t i = in_src[e];
-                            if (i - a.lo >= a.nloc) {
+                            if (REMOTE && i - a.lo >= a.nloc) {
                                 sent = a.rtag[e] == r;
                                 if (sent) mi = a.rmsg[e];
                             } else {
@@ -379,8 +385,8 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
 // ---------------------------------------------------------------- gossip
 // Deliveries to j = lattice senders pointing here + Imp3D random-edge senders
 // (bitmap) + the injector; all dropped if j was converged at round start.
-template <int TOPO>
-__global__ __launch_bounds__(TPB) void k_gossip_tile(RoundArgs a, uint32_t r) {
+template <int TOPO, bool REMOTE>
+__global__ __launch_bounds__(TPB, GP_MINB) void k_gossip_tile(RoundArgs a, uint32_t r) {
     __shared__ TileLds L;
     Ctl* ctl = a.ctl;
     if (ld_agent(&ctl->done)) return;
@@ -432,7 +438,7 @@ __global__ __launch_bounds__(TPB) void k_gossip_tile(RoundArgs a, uint32_t r) {
                     const uint32_t q = threadIdx.x + m * TPB;
                     const uint32_t li = isrc[m] - a.lo;
                     wv[m] = q >= cnt ? 0ull
-                            : li < a.nloc ? a.rbc[(isrc[m] >> 6) - (a.lo >> 6)]
+                            : (!REMOTE || li < a.nloc) ? a.rbc[(isrc[m] >> 6) - (a.lo >> 6)]
                                           : (a.rtag[e_lo + q] == r ? ~0ull : 0ull);
                 }
 #pragma unroll
@@ -474,7 +480,7 @@ __global__ __launch_bounds__(TPB) void k_gossip_tile(RoundArgs a, uint32_t r) {
                             for (uint32_t e = e_b; e < e_e; ++e) {
                                 const uint32_t i = a.in_src[e];
                                 const uint32_t li = i - a.lo;
-                                inc += li < a.nloc ? (uint32_t)((a.rbc[(i >> 6) - (a.lo >> 6)] >> (i & 63)) & 1ull)
+                                inc += (!REMOTE || li < a.nloc) ? (uint32_t)((a.rbc[(i >> 6) - (a.lo >> 6)] >> (i & 63)) & 1ull)
                                                    : (a.rtag[e] == r ? 1u : 0u);
                             }
                         }
@@ -576,17 +582,24 @@ RoundArgs make_round_args(const DevState& S, uint32_t round) {
 hipError_t launch_round_tile(const DevState& S, uint32_t round, int grid, hipStream_t st) {
     const RoundArgs a = make_round_args(S, round);
     const dim3 g(grid), b(TPB);
+    const bool remote = S.rtag != nullptr;  // Imp3D slabs of a multi-rank run
     if (S.alg == PUSHSUM) {
         switch (S.topo) {
-            case LINE: hipLaunchKernelGGL(k_ps_tile<LINE>, g, b, 0, st, a, round); break;
-            case GRID3D: hipLaunchKernelGGL(k_ps_tile<GRID3D>, g, b, 0, st, a, round); break;
-            default: hipLaunchKernelGGL(k_ps_tile<IMP3D>, g, b, 0, st, a, round); break;
+            case LINE: hipLaunchKernelGGL((k_ps_tile<LINE, false>), g, b, 0, st, a, round); break;
+            case GRID3D: hipLaunchKernelGGL((k_ps_tile<GRID3D, false>), g, b, 0, st, a, round); break;
+            default:
+                if (remote) hipLaunchKernelGGL((k_ps_tile<IMP3D, true>), g, b, 0, st, a, round);
+                else hipLaunchKernelGGL((k_ps_tile<IMP3D, false>), g, b, 0, st, a, round);
+                break;
         }
     } else {
         switch (S.topo) {
-            case LINE: hipLaunchKernelGGL(k_gossip_tile<LINE>, g, b, 0, st, a, round); break;
-            case GRID3D: hipLaunchKernelGGL(k_gossip_tile<GRID3D>, g, b, 0, st, a, round); break;
-            default: hipLaunchKernelGGL(k_gossip_tile<IMP3D>, g, b, 0, st, a, round); break;
+            case LINE: hipLaunchKernelGGL((k_gossip_tile<LINE, false>), g, b, 0, st, a, round); break;
+            case GRID3D: hipLaunchKernelGGL((k_gossip_tile<GRID3D, false>), g, b, 0, st, a, round); break;
+            default:
+                if (remote) hipLaunchKernelGGL((k_gossip_tile<IMP3D, true>), g, b, 0, st, a, round);
+                else hipLaunchKernelGGL((k_gossip_tile<IMP3D, false>), g, b, 0, st, a, round);
+                break;
         }
     }
     return hipGetLastError();

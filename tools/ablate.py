@@ -22,6 +22,7 @@ VARIANTS = {
     "no_ephilox": (4, 16), "no_gathers": (4, 1 | 2), "stream_only": (4, 2 | 4 | 8),
     "bitmap_only": (4, 32), "no_ratio": (4, 64),
     "minb6": (4, 0, 6), "minb8": (4, 0, 8),
+    "cheap_decide": (4, 128), "cheap_no_nextdir": (4, 128 | 8),
 }
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off"]
 
@@ -32,7 +33,7 @@ def build():
     procs = []
     for name, v in VARIANTS.items():
         npt, mask = v[0], v[1]
-        minb = v[2] if len(v) > 2 else 1
+        minb = v[2] if len(v) > 2 else 5
         obj = os.path.join(OUT, f"gp_round_{name}.o")
         cmd = ["/opt/rocm/bin/hipcc", *FLAGS, f"-DGP_NPT={npt}", f"-DGP_ABLATE={mask}", f"-DGP_MINB={minb}",
                "-c", "-o", obj, os.path.join(CSRC, "gp_round.hip")]
@@ -42,9 +43,9 @@ def build():
     objdir = os.path.join(ROOT, "build", "obj")
     for name in VARIANTS:
         so = os.path.join(OUT, f"lib_{name}.so")
-        objs = [os.path.join(objdir, "gp_api.o"), os.path.join(objdir, "gp_kernels.o"),
-                os.path.join(OUT, f"gp_round_{name}.o"), sort_obj]
-        subprocess.check_call(["/opt/rocm/bin/hipcc", *FLAGS, "-shared", "-o", so, *objs])
+        objs = [os.path.join(objdir, f) for f in ("gp_api.o", "gp_kernels.o", "gp_wave.o", "gp_col.o", "gp_xchg.o")]
+        objs += [os.path.join(OUT, f"gp_round_{name}.o"), sort_obj]
+        subprocess.check_call(["/opt/rocm/bin/hipcc", *FLAGS, "-shared", "-o", so, *objs, "-L/opt/rocm/lib", "-lrccl"])
 
 
 def run(n, only=None):
