@@ -632,11 +632,12 @@ void choose_kernel(gp_sim* s, int64_t nloc_max, int& kernel, uint32_t& col_xsegs
     if (lattice && cfg->algorithm == GP_GOSSIP && g >= 200) kernel = KERNEL_COL;
     if (const char* e = std::getenv("GP_KERNEL")) {
         if (!std::strcmp(e, "tile")) kernel = KERNEL_TILE;
+        else if (!std::strcmp(e, "tile2")) kernel = KERNEL_TILE2;
         else if (!std::strcmp(e, "wave")) kernel = KERNEL_WAVE;
         else if (!std::strcmp(e, "col") && lattice) kernel = KERNEL_COL;
     }
     col_xsegs = 1;
-    if (cfg->topology != GP_FULL && kernel != KERNEL_TILE) {
+    if (cfg->topology != GP_FULL && kernel != KERNEL_TILE && kernel != KERNEL_TILE2) {
         // exactly the resident grid (a persistent sweep), a multiple of the 8 XCDs
         const int bpc = kernel == KERNEL_COL ? col_blocks_per_cu(cfg->topology, cfg->algorithm)
                                              : wave_blocks_per_cu(cfg->topology, cfg->algorithm);

@@ -100,7 +100,7 @@ struct RoundArgs {
     uint32_t walk;  // 0: XCD-contiguous eighths, 1: one global sweep (tile t -> block t % grid)
 };
 
-enum KernelVariant : int { KERNEL_WAVE = 0, KERNEL_TILE = 1, KERNEL_COL = 2 };
+enum KernelVariant : int { KERNEL_WAVE = 0, KERNEL_TILE = 1, KERNEL_COL = 2, KERNEL_TILE2 = 3 };
 
 // Arguments of the wave-autonomous round kernels (gp_wave.hip, gp_col.hip).
 struct WaveArgs {

@@ -35,6 +35,9 @@ namespace gp {
 #define GP_MINB 5  // __launch_bounds__ minimum waves per SIMD (= resident 256-thread blocks per CU):
                    // the LDS tile allows 5, so keep VGPRs <= 96 to not lose the fifth
 #endif
+#ifndef GP_MINB2
+#define GP_MINB2 4  // k_ps_tile2: its message burst needs the registers of 4 waves/SIMD
+#endif
 #define ABL_NO_RGATHER 1   // in-list: decide but do not gather the sender's (s, w)
 #define ABL_NO_LGATHER 2   // lattice: decide but do not gather
 #define ABL_NO_INLIST 4    // skip the Imp3D in-list
@@ -43,6 +46,9 @@ namespace gp {
 #define ABL_BITMAP_ONLY 32 // in-list: always read the random-edge bitmap, never recompute Philox
 #define ABL_NO_RATIO 64    // skip the ratio test
 #define ABL_CHEAP_DECIDE 128  // in-list: a one-multiply hash instead of the sender's Philox draw
+#define ABL_NO_XGATHER 256    // lattice: no gather from the x-1 / x+1 planes
+#define ABL_NO_YGATHER 512    // lattice: no gather from the y-1 / y+1 rows
+#define ABL_NO_ZGATHER 1024   // lattice: no gather from z-1 / z+1
 
 namespace {
 
@@ -114,6 +120,54 @@ struct TileWalk {
 };
 
 __device__ __forceinline__ double2 ld_sw(const double2* p) { return *p; }
+
+// ---- compacted-gather tile (k_ps_tile2)
+constexpr int MCAP2 = 1280;                 // lattice + random messages gathered per tile (mean ~1030)
+constexpr int MI2 = MCAP2 / TPB;            // gathers per thread
+constexpr uint32_t REMOTE_TAG = 0xFFFFF000u;  // list entry >= this: remote message of staged edge ~entry
+
+struct Tile2Lds {
+    union {
+        struct {
+            uint32_t rows[W_ROWS];  // direction bytes of [j0 - H, j1 + H)
+            uint32_t xm[W_PLANE];   // direction bytes of [j0 - g^2, j1 - g^2)
+            uint32_t xp[W_PLANE];   // direction bytes of [j0 + g^2, j1 + g^2)
+            uint32_t src[SRC_CAP];  // in_src[in_off[j0] .. in_off[j1])
+        } s;
+        double2 msg[MCAP2];         // after the decisions: the tile's messages (slot m's first
+                                    // dword holds its source id until the gather lands)
+    } u;
+    uint32_t off[TILE + 1];         // in_off[T .. T + TILE]
+    uint16_t pos[SRC_CAP];          // staged in-edge -> message slot (POS_NONE / POS_GLOBAL)
+    uint32_t out[TILE / 4];
+    uint32_t scan[TPB / 64 + 1];
+    uint32_t red[2][TPB / 64];
+};
+
+// Exclusive scan of one value per thread over the block; `total` = block sum.
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* lds, uint32_t& total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+    }
+    if (lane == 63) lds[wid] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (int w = 0; w < TPB / 64; ++w) {
+            const uint32_t t = lds[w];
+            lds[w] = run;
+            run += t;
+        }
+        lds[TPB / 64] = run;
+    }
+    __syncthreads();
+    total = lds[TPB / 64];
+    return incl - v + lds[wid];
+}
 
 }  // namespace
 
@@ -268,8 +322,12 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                 double2 m[ND];
 #pragma unroll
                 for (uint32_t d = 0; d < ND; ++d)
-                    m[d] = (!(GP_ABLATE & ABL_NO_LGATHER) && (from & (1u << d))) ? ld_sw(swc + nbr<TOPO>(j, d, G))
-                                                                               : make_double2(0.0, 0.0);
+                    m[d] = (!(GP_ABLATE & ABL_NO_LGATHER) && (from & (1u << d)) &&
+                            !((GP_ABLATE & ABL_NO_XGATHER) && TOPO != LINE && d < 2) &&
+                            !((GP_ABLATE & ABL_NO_YGATHER) && TOPO != LINE && (d == 2 || d == 3)) &&
+                            !((GP_ABLATE & ABL_NO_ZGATHER) && (TOPO == LINE || d >= 4)))
+                               ? ld_sw(swc + nbr<TOPO>(j, d, G))
+                               : make_double2(0.0, 0.0);
                 bool recv = from != 0;
 #pragma unroll
                 for (uint32_t d = 0; d < ND; ++d) {
@@ -359,6 +417,331 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
         __syncthreads();
     }
     // block reduction of alerts / newly active
+    uint32_t x = alerts, y = newly;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        x += __shfl_xor(x, o, 64);
+        y += __shfl_xor(y, o, 64);
+    }
+    if (lane == 0) {
+        L.red[0][threadIdx.x >> 6] = x;
+        L.red[1][threadIdx.x >> 6] = y;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        x = 0;
+        y = 0;
+        for (int w = 0; w < TPB / 64; ++w) {
+            x += L.red[0][w];
+            y += L.red[1][w];
+        }
+        if (x) atomicAdd(&ctl->round_alerts, (unsigned long long)x);
+        if (y) atomicAdd(&ctl->round_active, (unsigned long long)y);
+    }
+}
+
+// ---------------------------------------------------------------- push-sum, compacted gathers
+// Same round as k_ps_tile, different schedule: after staging, every thread
+// decides its nodes' lattice senders (from the staged bytes) and its share of
+// the tile's in-edges (Philox / bitmap / tag); a block scan assigns every
+// message of the tile -- lattice and random alike -- a slot, the source ids go
+// into those slots (the staging area is dead by then), and the whole tile's
+// messages are gathered as one dense burst (MI2 loads per thread instead of 6
+// mostly-masked loads per node), overlapped with the next-round Philox draws.
+// The fold then reads every message from LDS, in canonical order.
+template <int TOPO, bool REMOTE>
+__global__ __launch_bounds__(TPB, GP_MINB2) void k_ps_tile2(RoundArgs a, uint32_t r) {
+    __shared__ Tile2Lds L;
+    Ctl* ctl = a.ctl;
+    if (ld_agent(&ctl->done)) return;
+    const bool all_active = ld_agent(&ctl->all_active) != 0;
+    const double2* __restrict__ swc = a.swc;
+    double2* __restrict__ swn = a.swn;
+    const uint64_t* __restrict__ rbc = a.rbc;
+    const uint32_t* __restrict__ in_src = a.in_src;
+    const Geom G = a.G;
+    const uint32_t H = TOPO == LINE ? 1u : G.g;
+    constexpr uint32_t ND = TOPO == LINE ? 2 : 6;
+    constexpr int FU = SRC_CAP / TPB;
+    uint32_t alerts = 0, newly = 0;
+    const int lane = threadIdx.x & 63;
+    uint32_t* const list = reinterpret_cast<uint32_t*>(L.u.msg);
+
+    for (TileWalk tw(a.ntiles, a.walk); tw.t < tw.end; tw.t += tw.step) {
+        const uint32_t T = (a.lo / TILE + tw.t) * TILE;
+        const uint32_t j0 = max(a.lo, T);
+        const uint32_t j1 = min(a.lo + a.nloc, T + TILE);
+        uint32_t e_lo = 0, e_hi = 0;
+        if (TOPO == IMP3D) {
+            e_lo = a.in_off[j0];
+            e_hi = a.in_off[j1];
+        }
+        const uint32_t b_rows = stage_bytes(L.u.s.rows, a.nbc, (int64_t)j0 - H, (int64_t)j1 + H, a.ext_lo, a.ext_hi);
+        uint32_t b_xm = 0, b_xp = 0;
+        if (TOPO != LINE) {
+            b_xm = stage_bytes(L.u.s.xm, a.nbc, (int64_t)j0 - G.g2, (int64_t)j1 - G.g2, a.ext_lo, a.ext_hi);
+            b_xp = stage_bytes(L.u.s.xp, a.nbc, (int64_t)j0 + G.g2, (int64_t)j1 + G.g2, a.ext_lo, a.ext_hi);
+        }
+        const uint32_t cnt = e_hi - e_lo;
+        const bool staged = TOPO == IMP3D && cnt <= (uint32_t)SRC_CAP;
+        if (TOPO == IMP3D) {
+            for (uint32_t q = j0 - T + threadIdx.x; q <= j1 - T; q += TPB) L.off[q] = a.in_off[T + q];
+            if (staged)
+                for (uint32_t q = threadIdx.x; q < cnt; q += TPB) L.u.s.src[q] = in_src[e_lo + q];
+        }
+        __syncthreads();
+        // ---- 1a. decisions: lattice senders per node, random-edge senders per staged edge
+        uint32_t frp = 0, bown = 0, msk = 0;  // per node k, byte k: from-bits, own byte, present mask
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            const uint32_t jl = k * TPB + threadIdx.x;
+            const uint32_t j = T + jl;
+            const bool valid = j >= j0 && j < j1;
+            uint32_t from = 0, mask = 0, b = 0;
+            if (valid) {
+                b = lds_byte(L.u.s.rows, j - b_rows);
+                mask = present_mask<TOPO>(j, G);
+                if (TOPO == LINE) {
+                    if ((mask & 1u) && (lds_byte(L.u.s.rows, j - 1 - b_rows) & DIR_MASK) == 1u) from |= 1u;
+                    if ((mask & 2u) && (lds_byte(L.u.s.rows, j + 1 - b_rows) & DIR_MASK) == 0u) from |= 2u;
+                } else {
+                    if ((mask & 1u) && (lds_byte(L.u.s.xm, j - G.g2 - b_xm) & DIR_MASK) == 1u) from |= 1u;
+                    if ((mask & 2u) && (lds_byte(L.u.s.xp, j + G.g2 - b_xp) & DIR_MASK) == 0u) from |= 2u;
+                    if ((mask & 4u) && (lds_byte(L.u.s.rows, j + G.g - b_rows) & DIR_MASK) == 3u) from |= 4u;
+                    if ((mask & 8u) && (lds_byte(L.u.s.rows, j - G.g - b_rows) & DIR_MASK) == 2u) from |= 8u;
+                    if ((mask & 16u) && (lds_byte(L.u.s.rows, j + 1 - b_rows) & DIR_MASK) == 5u) from |= 16u;
+                    if ((mask & 32u) && (lds_byte(L.u.s.rows, j - 1 - b_rows) & DIR_MASK) == 4u) from |= 32u;
+                }
+            }
+            frp |= from << (8 * k);
+            bown |= b << (8 * k);
+            msk |= mask << (8 * k);
+        }
+        uint32_t isrc[FU];
+        uint32_t sbits = 0;  // bit m: staged edge tid + m * TPB was used by its sender
+        if (staged) {
+#pragma unroll
+            for (int m = 0; m < FU; ++m) {
+                const uint32_t q = threadIdx.x + m * TPB;
+                isrc[m] = q < cnt ? L.u.s.src[q] : a.lo;
+            }
+#pragma unroll
+            for (int m = 0; m < FU; ++m) {
+                const uint32_t q = threadIdx.x + m * TPB;
+                const uint32_t i = isrc[m];
+                bool sent = false;
+                if (q < cnt) {
+                    if (REMOTE && i - a.lo >= a.nloc) {
+                        sent = a.rtag[e_lo + q] == r;
+                    } else if (all_active) {
+                        const uint32_t di = popc6(present_mask<IMP3D>(i, G)) + 1u;
+                        sent = uniform(a.k0, a.k1, S_PUSHSUM, i, r, di) == di - 1u;
+                    } else {
+                        sent = (rbc[(i >> 6) - (a.lo >> 6)] >> (i & 63)) & 1ull;
+                    }
+                }
+                sbits |= sent ? (1u << m) : 0u;
+            }
+        }
+        uint32_t mine = (uint32_t)__popc(sbits);
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) mine += popc6((frp >> (8 * k)) & 0xFFu);
+        uint32_t total;
+        const uint32_t tbase = block_excl_scan(mine, L.scan, total);  // barriers: the staging area is dead now
+        // ---- 1b. slots: this thread's messages get [tbase, tbase + mine); sources into the slots
+        uint32_t slot = tbase;
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            const uint32_t j = T + k * TPB + threadIdx.x;
+            const uint32_t f = (frp >> (8 * k)) & 0xFFu;
+#pragma unroll
+            for (uint32_t d = 0; d < ND; ++d) {
+                if ((f >> d) & 1u) {
+                    if (slot < (uint32_t)MCAP2) list[4 * slot] = nbr<TOPO>(j, d, G);
+                    ++slot;
+                }
+            }
+        }
+        if (staged) {
+#pragma unroll
+            for (int m = 0; m < FU; ++m) {
+                const uint32_t q = threadIdx.x + m * TPB;
+                if (q < cnt) {
+                    uint16_t p = POS_NONE;
+                    if ((sbits >> m) & 1u) {
+                        if (slot < (uint32_t)MCAP2) {
+                            list[4 * slot] = (REMOTE && isrc[m] - a.lo >= a.nloc) ? 0xFFFFFFFFu - q : isrc[m];
+                            p = (uint16_t)slot;
+                        } else {
+                            p = POS_GLOBAL;
+                        }
+                        ++slot;
+                    }
+                    L.pos[q] = p;
+                }
+            }
+        }
+        __syncthreads();
+        // ---- 2. one dense gather burst for the tile's messages, overlapped with
+        //         the next-round direction draws of this thread's nodes
+        const uint32_t M = min(total, (uint32_t)MCAP2);
+        double2 own[NPT];  // own (s, w): loaded with the burst, used by the fold
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            const uint32_t j = T + k * TPB + threadIdx.x;
+            own[k] = (j >= j0 && j < j1) ? swc[j] : make_double2(0.0, 1.0);
+        }
+        double2 v[MI2];
+#pragma unroll
+        for (int it = 0; it < MI2; ++it) {
+            const uint32_t m = it * TPB + threadIdx.x;
+            v[it] = make_double2(0.0, 0.0);
+            if (m < M) {
+                const uint32_t src = list[4 * m];
+                v[it] = (REMOTE && src >= REMOTE_TAG) ? a.rmsg[e_lo + (0xFFFFFFFFu - src)] : ld_sw(swc + src);
+            }
+        }
+        uint32_t dirs = 0, rcv = 0;
+        if (!(TOPO == IMP3D && !staged)) {
+#pragma unroll
+            for (int k = 0; k < NPT; ++k) {
+                const uint32_t jl = k * TPB + threadIdx.x;
+                const uint32_t j = T + jl;
+                const bool valid = j >= j0 && j < j1;
+                bool recv = ((frp >> (8 * k)) & 0xFFu) != 0;
+                if (TOPO == IMP3D && valid) {
+                    const uint32_t e_b = L.off[jl], e_e = L.off[jl + 1];
+                    for (uint32_t e = e_b; e < e_e && !recv; ++e) recv = L.pos[e - e_lo] != POS_NONE;
+                }
+                const uint32_t b = (bown >> (8 * k)) & 0xFFu;
+                const uint32_t mask = (msk >> (8 * k)) & 0xFFu;
+                const uint32_t deg = popc6(mask) + (TOPO == IMP3D ? 1u : 0u);
+                const bool active = valid && ((b & B_ACTIVE) || recv);
+                uint32_t dir = DIR_NONE;
+                if (active && deg > 0) dir = slot_to_dir(mask, uniform(a.k0, a.k1, S_PUSHSUM, j, r + 1, deg));
+                dirs |= dir << (8 * k);
+                rcv |= (recv ? 1u : 0u) << k;
+            }
+        }
+#pragma unroll
+        for (int it = 0; it < MI2; ++it) {
+            const uint32_t m = it * TPB + threadIdx.x;
+            if (m < M) L.u.msg[m] = v[it];
+        }
+        __syncthreads();
+        // ---- 3. fold in canonical order from LDS, ratio test, outputs
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            const uint32_t jl = k * TPB + threadIdx.x;
+            const uint32_t j = T + jl;
+            const bool valid = j >= j0 && j < j1;
+            uint32_t dir = DIR_NONE;
+            if (valid) {
+                const uint32_t b = (bown >> (8 * k)) & 0xFFu;
+                const uint32_t mask = (msk >> (8 * k)) & 0xFFu;
+                const uint32_t deg = popc6(mask) + (TOPO == IMP3D ? 1u : 0u);
+                bool active = (b & B_ACTIVE) != 0;
+                const double2 sv = own[k];
+                const bool halve = active && deg > 0;
+                double acc_s = halve ? sv.x * 0.5 : sv.x;
+                double acc_w = halve ? sv.y * 0.5 : sv.y;
+                const uint32_t f = (frp >> (8 * k)) & 0xFFu;
+                uint32_t mm = tbase;  // this node's lattice slots follow those of the thread's earlier nodes
+#pragma unroll
+                for (int k2 = 0; k2 < k; ++k2) mm += popc6((frp >> (8 * k2)) & 0xFFu);
+#pragma unroll
+                for (uint32_t d = 0; d < ND; ++d) {
+                    if ((f >> d) & 1u) {
+                        const double2 mv = mm < (uint32_t)MCAP2 ? L.u.msg[mm] : ld_sw(swc + nbr<TOPO>(j, d, G));
+                        acc_s = acc_s + mv.x * 0.5;
+                        acc_w = acc_w + mv.y * 0.5;
+                        ++mm;
+                    }
+                }
+                bool recv = f != 0;
+                if (TOPO == IMP3D) {
+                    const uint32_t e_b = L.off[jl], e_e = L.off[jl + 1];
+                    for (uint32_t e = e_b; e < e_e; ++e) {
+                        bool sent = false;
+                        double2 mi = make_double2(0.0, 0.0);
+                        if (staged) {
+                            const uint16_t p = L.pos[e - e_lo];
+                            sent = p != POS_NONE;
+                            if (p < (uint16_t)MCAP2) {
+                                mi = L.u.msg[p];
+                            } else if (p == POS_GLOBAL) {
+                                const uint32_t i = in_src[e];
+                                mi = (REMOTE && i - a.lo >= a.nloc) ? a.rmsg[e] : ld_sw(swc + i);
+                            }
+                        } else {  // rare: tile in-degree above SRC_CAP
+                            const uint32_t i = in_src[e];
+                            if (REMOTE && i - a.lo >= a.nloc) {
+                                sent = a.rtag[e] == r;
+                                if (sent) mi = a.rmsg[e];
+                            } else {
+                                if (all_active) {
+                                    const uint32_t di = popc6(present_mask<IMP3D>(i, G)) + 1u;
+                                    sent = uniform(a.k0, a.k1, S_PUSHSUM, i, r, di) == di - 1u;
+                                } else {
+                                    sent = (rbc[(i >> 6) - (a.lo >> 6)] >> (i & 63)) & 1ull;
+                                }
+                                if (sent) mi = ld_sw(swc + i);
+                            }
+                        }
+                        if (sent) {
+                            acc_s = acc_s + mi.x * 0.5;
+                            acc_w = acc_w + mi.y * 0.5;
+                            recv = true;
+                        }
+                    }
+                }
+                uint32_t flags = b & (B_ACTIVE | B_CONV | (3u << CNT_SHIFT));
+                if (recv) {
+                    if (!(b & B_CONV)) {
+                        const double r_old = sv.x / sv.y;
+                        const double r_new = acc_s / acc_w;
+                        uint32_t cn = (b >> CNT_SHIFT) & 3u;
+                        cn = fabs(r_new - r_old) > 1e-10 ? 0u : cn + 1u;
+                        flags = (flags & ~(3u << CNT_SHIFT)) | (cn << CNT_SHIFT);
+                        if (cn == 3) {
+                            flags |= B_CONV;
+                            ++alerts;
+                        }
+                    }
+                    if (!active) {
+                        ++newly;
+                        flags |= B_ACTIVE;
+                        active = true;
+                    }
+                }
+                if (TOPO == IMP3D && !staged) {
+                    if (active && deg > 0) dir = slot_to_dir(mask, uniform(a.k0, a.k1, S_PUSHSUM, j, r + 1, deg));
+                } else {
+                    dir = (dirs >> (8 * k)) & 0xFFu;
+                }
+                reinterpret_cast<uint8_t*>(L.out)[jl] = (uint8_t)(flags | dir);
+                swn[j] = make_double2(acc_s, acc_w);
+            }
+            if (TOPO == IMP3D && !all_active) {
+                const unsigned long long bits = __ballot(valid && dir == DIR_RANDOM);
+                if (lane == 0) {
+                    const int64_t wi = (int64_t)((T + k * TPB + (threadIdx.x & ~63u)) >> 6) - (int64_t)(a.lo >> 6);
+                    if (wi >= 0) a.rbn[wi] = bits;
+                }
+            }
+        }
+        __syncthreads();
+        for (uint32_t w = threadIdx.x; w < (uint32_t)(TILE / 4); w += TPB) {
+            const uint32_t jw = T + w * 4;
+            if (jw >= j0 && jw + 4 <= j1) {
+                reinterpret_cast<uint32_t*>(a.nbn + T)[w] = L.out[w];
+            } else {
+                for (uint32_t b = 0; b < 4; ++b)
+                    if (jw + b >= j0 && jw + b < j1) a.nbn[jw + b] = reinterpret_cast<const uint8_t*>(L.out)[w * 4 + b];
+            }
+        }
+        __syncthreads();
+    }
     uint32_t x = alerts, y = newly;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -583,7 +966,16 @@ hipError_t launch_round_tile(const DevState& S, uint32_t round, int grid, hipStr
     const RoundArgs a = make_round_args(S, round);
     const dim3 g(grid), b(TPB);
     const bool remote = S.rtag != nullptr;  // Imp3D slabs of a multi-rank run
-    if (S.alg == PUSHSUM) {
+    if (S.alg == PUSHSUM && S.kernel == KERNEL_TILE2) {
+        switch (S.topo) {
+            case LINE: hipLaunchKernelGGL((k_ps_tile2<LINE, false>), g, b, 0, st, a, round); break;
+            case GRID3D: hipLaunchKernelGGL((k_ps_tile2<GRID3D, false>), g, b, 0, st, a, round); break;
+            default:
+                if (remote) hipLaunchKernelGGL((k_ps_tile2<IMP3D, true>), g, b, 0, st, a, round);
+                else hipLaunchKernelGGL((k_ps_tile2<IMP3D, false>), g, b, 0, st, a, round);
+                break;
+        }
+    } else if (S.alg == PUSHSUM) {
         switch (S.topo) {
             case LINE: hipLaunchKernelGGL((k_ps_tile<LINE, false>), g, b, 0, st, a, round); break;
             case GRID3D: hipLaunchKernelGGL((k_ps_tile<GRID3D, false>), g, b, 0, st, a, round); break;

@@ -37,7 +37,7 @@ CASES = [  # (num_nodes, topology, algorithm, seed, rounds, checkpoint, ranks)
 ]
 
 
-@pytest.mark.parametrize("kernel", ["tile", "wave", "col"])
+@pytest.mark.parametrize("kernel", ["tile", "tile2", "wave", "col"])
 @pytest.mark.parametrize("n,topo,alg,seed,rounds,chk,ranks", CASES, ids=lambda v: str(v))
 def test_virtual_ranks_parity(kernel, n, topo, alg, seed, rounds, chk, ranks, monkeypatch):
     if kernel == "col" and topo == "line":

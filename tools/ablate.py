@@ -23,6 +23,7 @@ VARIANTS = {
     "bitmap_only": (4, 32), "no_ratio": (4, 64),
     "minb6": (4, 0, 6), "minb8": (4, 0, 8),
     "cheap_decide": (4, 128), "cheap_no_nextdir": (4, 128 | 8),
+    "no_xgather": (4, 256), "no_ygather": (4, 512), "no_zgather": (4, 1024),
 }
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off"]
 
