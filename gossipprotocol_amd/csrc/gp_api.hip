@@ -33,6 +33,7 @@
 
 #include "../../include/gossip_hip.h"
 #include "gp_internal.hpp"
+#include "gp_full.hpp"
 #include "gp_xchg.hpp"
 
 using namespace gp;
@@ -86,6 +87,13 @@ struct Slab {
     std::vector<uint32_t> cap_out, cap_in;
     std::vector<size_t> soff, sbytes, roff, rbytes;
     unsigned int* overflow = nullptr;  // device flag
+    // full topology over several ranks (gp_full.hip)
+    uint32_t *key0 = nullptr, *val0 = nullptr, *key1 = nullptr, *val1 = nullptr, *seg = nullptr;
+    uint32_t *ckey = nullptr, *cidx = nullptr, *ckey2 = nullptr, *cidx2 = nullptr, *head = nullptr;
+    double2* cval = nullptr;
+    uint32_t ccap = 0, bits1 = 32, bits2 = 32;
+    void *tmp1 = nullptr, *tmp2 = nullptr;
+    size_t tmp1_bytes = 0, tmp2_bytes = 0;
 };
 
 size_t xbuf_bytes(uint32_t cap, bool push) {
@@ -197,11 +205,14 @@ int make_bounds(gp_sim* s) {
         set_err("at most %d ranks are supported (got %d)", XMAXW, W);
         return GP_EINVAL;
     }
-    if (topo == GP_FULL) {
-        set_err("the full topology runs on one GPU in this release (num_gpus = 1)");
-        return GP_EINVAL;
-    }
-    if (topo == GP_LINE) {
+    if (topo == GP_FULL) {  // contiguous ids, no halo: every message goes through the exchange
+        if (s->P < W) {
+            set_err("full topology with %lld nodes cannot be split over %d ranks", (long long)s->P, W);
+            return GP_EINVAL;
+        }
+        for (int w = 0; w <= W; ++w) s->bounds[w] = (uint32_t)(s->P * w / W);
+        s->halo = 0;
+    } else if (topo == GP_LINE) {
         if (s->P < W) {
             set_err("line with %lld nodes cannot be split over %d ranks", (long long)s->P, W);
             return GP_EINVAL;
@@ -266,7 +277,7 @@ int alloc_slab(gp_sim* s, Slab& sl, int r) {
                 return rc;
         }
     }
-    if (S.topo == FULL && S.alg == PUSHSUM) {
+    if (S.topo == FULL && S.alg == PUSHSUM && W == 1) {
         const uint32_t P = S.G.P;
         if ((rc = dev_alloc_t(s, &S.key[0], P)) || (rc = dev_alloc_t(s, &S.key[1], P)) ||
             (rc = dev_alloc_t(s, &S.val[0], P)) || (rc = dev_alloc_t(s, &S.val[1], P)) ||
@@ -378,17 +389,36 @@ int build_imp3d(gp_sim* s) {
     return GP_OK;
 }
 
+int finalize(gp_sim* s, uint32_t round_done, uint32_t round_next);
+
 // Fixed-capacity exchange buffers per rank pair: capacity = expected messages
 // per round + 12 sigma + 64 (never more than the pair's random edges).
 int setup_exchange(gp_sim* s) {
     const int W = s->world;
     const bool push = s->cfg.algorithm == GP_PUSHSUM;
+    const bool full = s->cfg.topology == GP_FULL;
     std::vector<uint32_t> caps((size_t)W * W, 0);  // caps[a * W + b]: a -> b
     double* mu = nullptr;
     unsigned long long* n = nullptr;
     HIP_TRY(hipMalloc(&mu, sizeof(double) * XMAXW));
     HIP_TRY(hipMalloc(&n, sizeof(unsigned long long) * XMAXW));
+    if (full) {
+        // every active sender picks a uniform target among P-1: messages a -> b are at
+        // most Binomial(nloc_a, nloc_b / (P-1))
+        for (Slab& sl : s->slab) {
+            const int a = sl.rank;
+            const double na = (double)(s->bounds[a + 1] - s->bounds[a]);
+            for (int b = 0; b < W; ++b) {
+                if (b == a) continue;
+                const double nb = (double)(s->bounds[b + 1] - s->bounds[b]);
+                const double m = na * nb / (double)(s->P - 1);
+                const double c = std::ceil(m + 12.0 * std::sqrt(m) + 64.0);
+                caps[(size_t)a * W + b] = (uint32_t)std::min(c, na);
+            }
+        }
+    }
     for (Slab& sl : s->slab) {
+        if (full) break;
         DevState& S = sl.S;
         HIP_TRY(hipMemsetAsync(mu, 0, sizeof(double) * XMAXW, s->stream));
         HIP_TRY(hipMemsetAsync(n, 0, sizeof(unsigned long long) * XMAXW, s->stream));
@@ -451,15 +481,143 @@ int setup_exchange(gp_sim* s) {
         HIP_TRY(hipMemsetAsync(sl.xsend, 0, so ? so : 16, s->stream));
         HIP_TRY(hipMemsetAsync(sl.xrecv, 0, ro ? ro : 16, s->stream));
         sl.overflow = &sl.S.ctl->overflow;
+        if (full && push) {  // message staging of the two sorts (gp_full.hip)
+            const uint32_t nl = sl.S.nloc;
+            uint64_t cc = nl;
+            for (int b = 0; b < W; ++b)
+                if (b != a) cc += sl.cap_in[b];
+            if (cc > 0xFFFFFF00ull) {
+                set_err("full topology: %llu staged messages per rank exceed the 32-bit range", (unsigned long long)cc);
+                return GP_EINVAL;
+            }
+            sl.ccap = (uint32_t)cc;
+            if ((rc = dev_alloc_t(s, &sl.key0, nl)) || (rc = dev_alloc_t(s, &sl.val0, nl)) ||
+                (rc = dev_alloc_t(s, &sl.key1, nl)) || (rc = dev_alloc_t(s, &sl.val1, nl)) ||
+                (rc = dev_alloc_t(s, &sl.seg, XMAXW + 1)) || (rc = dev_alloc_t(s, &sl.ckey, sl.ccap)) ||
+                (rc = dev_alloc_t(s, &sl.cidx, sl.ccap)) || (rc = dev_alloc_t(s, &sl.ckey2, sl.ccap)) ||
+                (rc = dev_alloc_t(s, &sl.cidx2, sl.ccap)) || (rc = dev_alloc_t(s, &sl.cval, sl.ccap)) ||
+                (rc = dev_alloc_t(s, &sl.head, nl)))
+                return rc;
+            sl.bits1 = bits_for((uint64_t)s->P);  // inactive senders stage key ~0: sorts last
+            sl.bits2 = bits_for((uint64_t)nl);    // padding key ~0 sorts after every receiver
+            HIP_TRY(sort_pairs(nullptr, sl.tmp1_bytes, sl.key0, sl.key1, sl.val0, sl.val1, nl, sl.bits1, s->stream));
+            HIP_TRY(sort_pairs(nullptr, sl.tmp2_bytes, sl.ckey, sl.ckey2, sl.cidx, sl.cidx2, sl.ccap, sl.bits2,
+                               s->stream));
+            if ((rc = dev_alloc(s, &sl.tmp1, sl.tmp1_bytes)) || (rc = dev_alloc(s, &sl.tmp2, sl.tmp2_bytes))) return rc;
+        }
     }
     return GP_OK;
+}
+
+// Move every rank's exchange buffers to their destinations (device copies for
+// in-process ranks, one RCCL group otherwise).
+int transfer_xbufs(gp_sim* s) {
+    const int W = s->world;
+    if (s->mode == MODE_VIRTUAL) {
+        for (Slab& a : s->slab)
+            for (Slab& d : s->slab)
+                if (&a != &d && a.sbytes[d.rank])
+                    HIP_TRY(hipMemcpyAsync(d.xrecv + d.roff[a.rank], a.xsend + a.soff[d.rank], a.sbytes[d.rank],
+                                           hipMemcpyDeviceToDevice, s->stream));
+        return GP_OK;
+    }
+    Slab& sl = s->slab[0];
+    NCCL_TRY(ncclGroupStart());
+    for (int p = 0; p < W; ++p) {
+        if (p == sl.rank) continue;
+        if (sl.sbytes[p]) NCCL_TRY(ncclSend(sl.xsend + sl.soff[p], sl.sbytes[p], ncclUint8, p, s->comm, s->stream));
+        if (sl.rbytes[p]) NCCL_TRY(ncclRecv(sl.xrecv + sl.roff[p], sl.rbytes[p], ncclUint8, p, s->comm, s->stream));
+    }
+    NCCL_TRY(ncclGroupEnd());
+    return GP_OK;
+}
+
+FullArgs make_full_args(gp_sim* s, Slab& sl, uint32_t round) {
+    DevState& S = sl.S;
+    const int cur = round & 1;
+    const bool push = S.alg == PUSHSUM;
+    const uint32_t d = S.lo - S.base;  // node arrays start at `base`; index these by id - lo
+    FullArgs a{};
+    a.nb = push ? S.nb[0] + d : nullptr;
+    a.swc = push ? S.sw[cur] + d : nullptr;
+    a.swn = push ? S.sw[cur ^ 1] + d : nullptr;
+    a.c = S.c;
+    a.inc = S.inc;
+    a.key0 = sl.key0;
+    a.val0 = sl.val0;
+    a.key1 = sl.key1;
+    a.val1 = sl.val1;
+    a.seg = sl.seg;
+    a.ckey = sl.ckey;
+    a.cidx = sl.cidx;
+    a.ckey2 = sl.ckey2;
+    a.cidx2 = sl.cidx2;
+    a.cval = sl.cval;
+    a.head = sl.head;
+    a.ccap = sl.ccap;
+    a.ctl = S.ctl;
+    a.overflow = sl.overflow;
+    a.P = S.G.P;
+    a.lo = S.lo;
+    a.nloc = S.nloc;
+    a.k0 = S.k0;
+    a.k1 = S.k1;
+    a.seed_node = S.seed_node;
+    a.W = s->world;
+    a.me = sl.rank;
+    for (int w = 0; w <= s->world; ++w) a.bounds[w] = s->bounds[w];
+    for (int p = 0; p < s->world; ++p) {
+        a.peer[p] = xpeer(sl.xsend, sl.soff[p], sl.cap_out[p]);
+        a.rpeer[p] = xpeer(sl.xrecv, sl.roff[p], sl.cap_in[p]);
+    }
+    return a;
+}
+
+// Full topology on several ranks: one round (gp_full.hip).
+int launch_round_full_multi(gp_sim* s, uint32_t r, hipEvent_t e0, hipEvent_t e1) {
+    const bool push = s->cfg.algorithm == GP_PUSHSUM;
+    int rc;
+    if (e0) HIP_TRY(hipEventRecord(e0, s->stream));
+    for (Slab& sl : s->slab) {
+        FullArgs a = make_full_args(s, sl, r);
+        if (push) {
+            HIP_TRY(launch_fullm_ps_send(a, r, s->grid, s->stream));
+            HIP_TRY(sort_pairs(sl.tmp1, sl.tmp1_bytes, sl.key0, sl.key1, sl.val0, sl.val1, sl.S.nloc, sl.bits1,
+                               s->stream));
+            HIP_TRY(launch_fullm_split(a, s->stream));
+            HIP_TRY(launch_fullm_ps_pack(a, std::max(1, s->grid / 8), s->stream));
+        } else {
+            ZeroArgs z{};
+            for (int p = 0; p < s->world; ++p) z.cnt[p] = a.peer[p].cnt;
+            z.n = s->world;
+            HIP_TRY(launch_zero_counts(z, s->stream));
+            HIP_TRY(launch_fullm_gossip_send(a, r, s->grid, s->stream));
+        }
+    }
+    if ((rc = transfer_xbufs(s))) return rc;
+    for (Slab& sl : s->slab) {
+        FullArgs a = make_full_args(s, sl, r);
+        if (push) {
+            HIP_TRY(launch_fullm_ps_combine(a, s->grid, s->stream));
+            HIP_TRY(sort_pairs(sl.tmp2, sl.tmp2_bytes, sl.ckey, sl.ckey2, sl.cidx, sl.cidx2, sl.ccap, sl.bits2,
+                               s->stream));
+            HIP_TRY(hipMemsetAsync(sl.head, 0xFF, sizeof(uint32_t) * sl.S.nloc, s->stream));
+            HIP_TRY(launch_fullm_ps_mark(a, s->grid, s->stream));
+            HIP_TRY(launch_fullm_ps_recv(a, s->grid, s->stream));
+        } else {
+            HIP_TRY(launch_fullm_gossip_unpack(a, std::max(1, s->grid / 8), s->stream));
+            HIP_TRY(launch_fullm_gossip_recv(a, s->grid, s->stream));
+        }
+    }
+    if (e1) HIP_TRY(hipEventRecord(e1, s->stream));
+    return finalize(s, r, r + 1);
 }
 
 // Halo refresh + Imp3D random-edge exchange for round `rn`, whose state the
 // previous round kernel has just written to buffers rn & 1.
 int exchange(gp_sim* s, uint32_t rn) {
     const int W = s->world;
-    if (W == 1) return GP_OK;
+    if (W == 1 || s->cfg.topology == GP_FULL) return GP_OK;  // full: the exchange is inside the round
     const int b = rn & 1;
     const bool push = s->cfg.algorithm == GP_PUSHSUM;
     const bool imp = s->cfg.topology == GP_IMP3D;
@@ -507,12 +665,10 @@ int exchange(gp_sim* s, uint32_t rn) {
                                        hipMemcpyDeviceToDevice, s->stream));
             }
         }
-        if (imp)
-            for (Slab& a : s->slab)
-                for (Slab& d : s->slab)
-                    if (&a != &d && a.sbytes[d.rank])
-                        HIP_TRY(hipMemcpyAsync(d.xrecv + d.roff[a.rank], a.xsend + a.soff[d.rank], a.sbytes[d.rank],
-                                               hipMemcpyDeviceToDevice, s->stream));
+        if (imp) {
+            int rc = transfer_xbufs(s);
+            if (rc) return rc;
+        }
     } else {
         Slab& sl = s->slab[0];
         DevState& S = sl.S;
@@ -580,6 +736,7 @@ int finalize(gp_sim* s, uint32_t round_done, uint32_t round_next) {
 
 // One synchronous round r: round kernel(s), exchange, finalize.
 int launch_round(gp_sim* s, uint32_t r, hipEvent_t e0, hipEvent_t e1) {
+    if (s->cfg.topology == GP_FULL && s->world > 1) return launch_round_full_multi(s, r, e0, e1);
     for (size_t q = 0; q < s->slab.size(); ++q) {
         DevState& S = s->slab[q].S;
         if (q == 0 && e0) HIP_TRY(hipEventRecord(e0, s->stream));
@@ -681,10 +838,9 @@ int build_sim(gp_sim* s) {
         sl.S.tile_walk = walk;
         if ((rc = alloc_slab(s, sl, sl.rank))) return rc;
     }
-    if (s->cfg.topology == GP_IMP3D) {
-        if ((rc = build_imp3d(s))) return rc;
-        if (s->world > 1 && (rc = setup_exchange(s))) return rc;
-    }
+    if (s->cfg.topology == GP_IMP3D && (rc = build_imp3d(s))) return rc;
+    if ((s->cfg.topology == GP_IMP3D || s->cfg.topology == GP_FULL) && s->world > 1 && (rc = setup_exchange(s)))
+        return rc;
     if (hipHostMalloc((void**)&s->host_ctl, sizeof(Ctl), hipHostMallocDefault) != hipSuccess) {
         set_err("hipHostMalloc failed");
         return GP_ENOMEM;

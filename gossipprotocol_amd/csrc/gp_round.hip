@@ -601,7 +601,7 @@ __global__ __launch_bounds__(TPB, GP_MINB2) void k_ps_tile2(RoundArgs a, uint32_
                 v[it] = (REMOTE && src >= REMOTE_TAG) ? a.rmsg[e_lo + (0xFFFFFFFFu - src)] : ld_sw(swc + src);
             }
         }
-        uint32_t dirs = 0, rcv = 0;
+        uint32_t dirs = 0;
         if (!(TOPO == IMP3D && !staged)) {
 #pragma unroll
             for (int k = 0; k < NPT; ++k) {
@@ -620,7 +620,7 @@ __global__ __launch_bounds__(TPB, GP_MINB2) void k_ps_tile2(RoundArgs a, uint32_
                 uint32_t dir = DIR_NONE;
                 if (active && deg > 0) dir = slot_to_dir(mask, uniform(a.k0, a.k1, S_PUSHSUM, j, r + 1, deg));
                 dirs |= dir << (8 * k);
-                rcv |= (recv ? 1u : 0u) << k;
+
             }
         }
 #pragma unroll

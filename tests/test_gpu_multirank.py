@@ -34,6 +34,10 @@ CASES = [  # (num_nodes, topology, algorithm, seed, rounds, checkpoint, ranks)
     (27000, "3D", "gossip", 4, 2000, 500, 3),
     (5000, "line", "gossip", 6, 8000, 2000, 2),
     (777, "line", "push-sum", 2, 1500, 500, 4),
+    (30000, "full", "push-sum", 8, 300, 50, 2),
+    (20000, "full", "push-sum", 5, 120, 40, 3),
+    (50000, "full", "gossip", 3, 400, 100, 3),
+    (3000, "full", "gossip", 9, 2000, 400, 2),
 ]
 
 
@@ -42,6 +46,8 @@ CASES = [  # (num_nodes, topology, algorithm, seed, rounds, checkpoint, ranks)
 def test_virtual_ranks_parity(kernel, n, topo, alg, seed, rounds, chk, ranks, monkeypatch):
     if kernel == "col" and topo == "line":
         pytest.skip("column march is a lattice kernel")
+    if topo == "full" and kernel != "tile":
+        pytest.skip("the full topology has one kernel set")
     monkeypatch.setenv("GP_KERNEL", kernel)
     sim, orc = Sim(n, topo, alg, seed=seed, virtual_ranks=ranks), Oracle(n, topo, alg, seed)
     assert sim.info().num_gpus == ranks
@@ -58,11 +64,12 @@ def test_virtual_ranks_parity(kernel, n, topo, alg, seed, rounds, chk, ranks, mo
     sim.close()
 
 
-def test_virtual_ranks_converge_like_single():
+@pytest.mark.parametrize("topo", ["Imp3D", "full"])
+def test_virtual_ranks_converge_like_single(topo):
     """Whole runs to convergence: same round count and alert sequence for 1, 2, 4, 8 ranks."""
     ref = None
     for ranks in (1, 2, 4, 8):
-        sim = Sim(8000, "Imp3D", "push-sum", seed=3, virtual_ranks=ranks)
+        sim = Sim(8000, topo, "push-sum", seed=3, virtual_ranks=ranks)
         alerts = sim.step(100000)
         st = sim.state()
         key = (sim.rounds, tuple(alerts), st["s"].tobytes(), st["w"].tobytes())
