@@ -790,11 +790,12 @@ void choose_kernel(gp_sim* s, int64_t nloc_max, int& kernel, uint32_t& col_xsegs
     if (const char* e = std::getenv("GP_KERNEL")) {
         if (!std::strcmp(e, "tile")) kernel = KERNEL_TILE;
         else if (!std::strcmp(e, "tile2")) kernel = KERNEL_TILE2;
+        else if (!std::strcmp(e, "xtile") && lattice) kernel = KERNEL_XTILE;
         else if (!std::strcmp(e, "wave")) kernel = KERNEL_WAVE;
         else if (!std::strcmp(e, "col") && lattice) kernel = KERNEL_COL;
     }
     col_xsegs = 1;
-    if (cfg->topology != GP_FULL && kernel != KERNEL_TILE && kernel != KERNEL_TILE2) {
+    if (cfg->topology != GP_FULL && kernel != KERNEL_TILE && kernel != KERNEL_TILE2 && kernel != KERNEL_XTILE) {
         // exactly the resident grid (a persistent sweep), a multiple of the 8 XCDs
         const int bpc = kernel == KERNEL_COL ? col_blocks_per_cu(cfg->topology, cfg->algorithm)
                                              : wave_blocks_per_cu(cfg->topology, cfg->algorithm);
@@ -808,6 +809,14 @@ void choose_kernel(gp_sim* s, int64_t nloc_max, int& kernel, uint32_t& col_xsegs
             xs = std::min<int64_t>(xs, std::max<int64_t>(1, planes / 16));
             col_xsegs = (uint32_t)xs;
         }
+    }
+    if (kernel == KERNEL_XTILE) {
+        // x-segments: about 16 (window, segment) items per CU slot, >= 8 planes per segment
+        const int64_t nwin = xtile_windows((uint32_t)(g * g));
+        const int64_t planes = std::max<int64_t>(1, g / s->world);
+        int64_t xs = std::max<int64_t>(1, (cap + nwin - 1) / nwin);
+        xs = std::min<int64_t>(xs, std::max<int64_t>(1, planes / 8));
+        col_xsegs = (uint32_t)xs;
     }
     if (const char* e = std::getenv("GP_GRID")) cap = std::max<int64_t>(1, std::atoll(e));
     if (const char* e = std::getenv("GP_XSEGS")) col_xsegs = (uint32_t)std::max(1, std::atoi(e));

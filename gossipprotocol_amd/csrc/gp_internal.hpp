@@ -98,9 +98,10 @@ struct RoundArgs {
     uint32_t k0, k1, seed_node, ntiles;
     uint32_t lo, nloc, ext_lo, ext_hi;  // owned ids [lo, lo + nloc); arrays hold [ext_lo, ext_hi)
     uint32_t walk;  // 0: XCD-contiguous eighths, 1: one global sweep (tile t -> block t % grid)
+    uint32_t xs_len;  // k_ps_xtile: planes per x-segment
 };
 
-enum KernelVariant : int { KERNEL_WAVE = 0, KERNEL_TILE = 1, KERNEL_COL = 2, KERNEL_TILE2 = 3 };
+enum KernelVariant : int { KERNEL_WAVE = 0, KERNEL_TILE = 1, KERNEL_COL = 2, KERNEL_TILE2 = 3, KERNEL_XTILE = 4 };
 
 // Arguments of the wave-autonomous round kernels (gp_wave.hip, gp_col.hip).
 struct WaveArgs {
@@ -142,6 +143,10 @@ uint32_t round_tiles(uint32_t P);
 uint32_t rbits_words_for(uint32_t lo, uint32_t nloc);
 hipError_t launch_round_tile(const DevState& S, uint32_t round, int grid, hipStream_t st);
 hipError_t launch_rbits_init(const DevState& S, int grid, hipStream_t st);
+
+// ---- x-marching tiled push-sum kernel (gp_xtile.hip): 3D / Imp3D
+hipError_t launch_round_xtile(const RoundArgs& a, int topo, bool remote, uint32_t round, int grid, hipStream_t st);
+uint32_t xtile_windows(uint32_t g2);
 
 // ---- kernels (gp_kernels.hip)
 hipError_t launch_init(const DevState& S, int grid, hipStream_t st);

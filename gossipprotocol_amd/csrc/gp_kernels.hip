@@ -461,7 +461,8 @@ hipError_t launch_histogram(const uint32_t* keys, uint32_t n, uint32_t* counts, 
 hipError_t launch_bulk(const DevState& S, uint32_t round, int grid, hipStream_t st) {
     const dim3 g(grid), b(BULK_THREADS);
     if (S.topo != FULL) {
-        if (S.kernel == KERNEL_TILE || S.kernel == KERNEL_TILE2) return launch_round_tile(S, round, grid, st);
+        if (S.kernel == KERNEL_TILE || S.kernel == KERNEL_TILE2 || S.kernel == KERNEL_XTILE)
+            return launch_round_tile(S, round, grid, st);
         if (S.kernel == KERNEL_COL) return launch_round_col(make_wave_args(S, round), S.topo, S.alg, round, grid, st);
         return launch_round_wave(make_wave_args(S, round), S.topo, S.alg, round, grid, st);
     }
@@ -475,20 +476,24 @@ hipError_t launch_bulk(const DevState& S, uint32_t round, int grid, hipStream_t 
 }
 
 const char* bulk_kernel_name(const DevState& S) {
-    static const char* ps[4][4] = {{"k_ps_wave<LINE>", "k_full_ps_send+sort+mark+recv", "k_ps_wave<GRID3D>",
+    static const char* ps[5][4] = {{"k_ps_wave<LINE>", "k_full_ps_send+sort+mark+recv", "k_ps_wave<GRID3D>",
                                     "k_ps_wave<IMP3D>"},
                                    {"k_ps_tile<LINE>", "k_full_ps_send+sort+mark+recv", "k_ps_tile<GRID3D>",
                                     "k_ps_tile<IMP3D>"},
                                    {"k_ps_wave<LINE>", "k_full_ps_send+sort+mark+recv", "k_ps_col<GRID3D>",
                                     "k_ps_col<IMP3D>"},
                                    {"k_ps_tile2<LINE>", "k_full_ps_send+sort+mark+recv", "k_ps_tile2<GRID3D>",
-                                    "k_ps_tile2<IMP3D>"}};
-    static const char* go[4][4] = {{"k_gossip_wave<LINE>", "k_full_gossip_send+recv", "k_gossip_wave<GRID3D>",
+                                    "k_ps_tile2<IMP3D>"},
+                                   {"k_ps_tile<LINE>", "k_full_ps_send+sort+mark+recv", "k_ps_xtile<GRID3D>",
+                                    "k_ps_xtile<IMP3D>"}};
+    static const char* go[5][4] = {{"k_gossip_wave<LINE>", "k_full_gossip_send+recv", "k_gossip_wave<GRID3D>",
                                     "k_gossip_wave<IMP3D>"},
                                    {"k_gossip_tile<LINE>", "k_full_gossip_send+recv", "k_gossip_tile<GRID3D>",
                                     "k_gossip_tile<IMP3D>"},
                                    {"k_gossip_wave<LINE>", "k_full_gossip_send+recv", "k_gossip_col<GRID3D>",
                                     "k_gossip_col<IMP3D>"},
+                                   {"k_gossip_tile<LINE>", "k_full_gossip_send+recv", "k_gossip_tile<GRID3D>",
+                                    "k_gossip_tile<IMP3D>"},
                                    {"k_gossip_tile<LINE>", "k_full_gossip_send+recv", "k_gossip_tile<GRID3D>",
                                     "k_gossip_tile<IMP3D>"}};
     const int v = S.kernel;

@@ -959,6 +959,11 @@ RoundArgs make_round_args(const DevState& S, uint32_t round) {
     a.seed_node = S.seed_node;
     a.ntiles = (S.lo + S.nloc + TILE - 1) / TILE - S.lo / TILE;
     a.walk = S.tile_walk;
+    a.xs_len = 0;
+    if (S.G.g2) {
+        const uint32_t planes = S.nloc / S.G.g2, xs = S.col_xsegs ? S.col_xsegs : 1u;
+        a.xs_len = (planes + xs - 1) / xs;
+    }
     return a;
 }
 
@@ -966,6 +971,8 @@ hipError_t launch_round_tile(const DevState& S, uint32_t round, int grid, hipStr
     const RoundArgs a = make_round_args(S, round);
     const dim3 g(grid), b(TPB);
     const bool remote = S.rtag != nullptr;  // Imp3D slabs of a multi-rank run
+    if (S.alg == PUSHSUM && S.kernel == KERNEL_XTILE && S.topo != LINE)
+        return launch_round_xtile(a, S.topo, remote, round, grid, st);
     if (S.alg == PUSHSUM && S.kernel == KERNEL_TILE2) {
         switch (S.topo) {
             case LINE: hipLaunchKernelGGL((k_ps_tile2<LINE, false>), g, b, 0, st, a, round); break;

@@ -41,11 +41,11 @@ CASES = [  # (num_nodes, topology, algorithm, seed, rounds, checkpoint, ranks)
 ]
 
 
-@pytest.mark.parametrize("kernel", ["tile", "tile2", "wave", "col"])
+@pytest.mark.parametrize("kernel", ["tile", "tile2", "xtile", "wave", "col"])
 @pytest.mark.parametrize("n,topo,alg,seed,rounds,chk,ranks", CASES, ids=lambda v: str(v))
 def test_virtual_ranks_parity(kernel, n, topo, alg, seed, rounds, chk, ranks, monkeypatch):
-    if kernel == "col" and topo == "line":
-        pytest.skip("column march is a lattice kernel")
+    if kernel in ("col", "xtile") and topo == "line":
+        pytest.skip("lattice kernel")
     if topo == "full" and kernel != "tile":
         pytest.skip("the full topology has one kernel set")
     monkeypatch.setenv("GP_KERNEL", kernel)

@@ -172,7 +172,7 @@ KERNEL_CASES = [  # (num_nodes, topology, algorithm, seed, rounds, checkpoint, x
 ]
 
 
-@pytest.mark.parametrize("kernel", ["wave", "col", "tile", "tile2"])
+@pytest.mark.parametrize("kernel", ["wave", "col", "tile", "tile2", "xtile"])
 @pytest.mark.parametrize("n,topo,alg,seed,rounds,chk,xsegs", KERNEL_CASES, ids=lambda v: str(v))
 def test_kernel_variant_parity(kernel, n, topo, alg, seed, rounds, chk, xsegs, monkeypatch):
     """Every round-kernel variant (chunk / column march / tiled) bit-exact vs the oracle,
