@@ -348,8 +348,9 @@ int build_imp3d(gp_sim* s) {
         const int r = sl.rank;
         const uint32_t ne = edge0[r + 1] - edge0[r];
         sl.nedges = ne;
-        if ((rc = dev_alloc_t(s, &S.rnd, S.nloc)) || (rc = dev_alloc_t(s, &S.in_off, (size_t)S.nloc + 1)) ||
-            (rc = dev_alloc_t(s, &S.in_src, ne)))
+        // in-lists padded by 4 words: the tile kernels stage them with 16-byte LDS-DMA
+        if ((rc = dev_alloc_t(s, &S.rnd, S.nloc)) || (rc = dev_alloc_t(s, &S.in_off, (size_t)S.nloc + 1 + 4)) ||
+            (rc = dev_alloc_t(s, &S.in_src, (size_t)ne + 4)))
             return rc;
         HIP_TRY(hipMemcpyAsync(S.rnd, rnd_all + S.lo, sizeof(uint32_t) * S.nloc, hipMemcpyDeviceToDevice, s->stream));
         HIP_TRY(hipMemcpyAsync(S.in_off, off_all + S.lo, sizeof(uint32_t) * ((size_t)S.nloc + 1),
@@ -774,7 +775,7 @@ double alg_bytes(const gp_sim* s) {
 
 // Kernel variant and grid for this run (measured defaults, GP_KERNEL / GP_GRID /
 // GP_XSEGS / GP_WALK override for experiments).
-void choose_kernel(gp_sim* s, int64_t nloc_max, int& kernel, uint32_t& col_xsegs, uint32_t& walk) {
+void choose_kernel(gp_sim* s, int64_t nloc_max, int& kernel, uint32_t& col_xsegs, uint32_t& walk, uint32_t& wx) {
     hipDeviceProp_t prop;
     (void)hipGetDeviceProperties(&prop, s->device);
     const gp_config* cfg = &s->cfg;
@@ -823,6 +824,8 @@ void choose_kernel(gp_sim* s, int64_t nloc_max, int& kernel, uint32_t& col_xsegs
     s->grid = (int)std::max<int64_t>(1, std::min(kernel == KERNEL_COL ? cap : blocks, cap));
     walk = 0;
     if (const char* e = std::getenv("GP_WALK")) walk = (uint32_t)std::atoi(e);
+    wx = 40;
+    if (const char* e = std::getenv("GP_WX")) wx = (uint32_t)std::max(1, std::atoi(e));
 }
 
 // Everything after the handle exists: slabs, topology, initial state, round 0.
@@ -832,8 +835,8 @@ int build_sim(gp_sim* s) {
     int64_t nloc_max = 0;
     for (int w = 0; w < s->world; ++w) nloc_max = std::max<int64_t>(nloc_max, s->bounds[w + 1] - s->bounds[w]);
     int kernel;
-    uint32_t col_xsegs, walk;
-    choose_kernel(s, nloc_max, kernel, col_xsegs, walk);
+    uint32_t col_xsegs, walk, wx;
+    choose_kernel(s, nloc_max, kernel, col_xsegs, walk, wx);
     if (s->mode == MODE_VIRTUAL) {
         s->slab.resize(s->world);
         for (int w = 0; w < s->world; ++w) s->slab[w].rank = w;
@@ -845,6 +848,7 @@ int build_sim(gp_sim* s) {
         sl.S.kernel = kernel;
         sl.S.col_xsegs = col_xsegs;
         sl.S.tile_walk = walk;
+        sl.S.tile_wx = wx;
         if ((rc = alloc_slab(s, sl, sl.rank))) return rc;
     }
     if (s->cfg.topology == GP_IMP3D && (rc = build_imp3d(s))) return rc;

@@ -78,6 +78,7 @@ struct DevState {
     // column kernels: x segments per patch (set at create from the resident grid)
     uint32_t col_xsegs;
     uint32_t tile_walk;  // RoundArgs::walk
+    uint32_t tile_wx;    // RoundArgs::wx
 };
 
 // Arguments of the tiled round kernels (gp_round.hip): only what they read.
@@ -97,7 +98,8 @@ struct RoundArgs {
     Geom G;
     uint32_t k0, k1, seed_node, ntiles;
     uint32_t lo, nloc, ext_lo, ext_hi;  // owned ids [lo, lo + nloc); arrays hold [ext_lo, ext_hi)
-    uint32_t walk;  // 0: XCD-contiguous eighths, 1: one global sweep (tile t -> block t % grid)
+    uint32_t walk;  // 0: XCD-contiguous eighths, 1: one global sweep (tile t -> block t % grid), 2: x-windows
+    uint32_t wx;    // walk 2: planes per x-window
     uint32_t xs_len;  // k_ps_xtile: planes per x-segment
 };
 

@@ -62,12 +62,16 @@ constexpr int SRC_CAP = 1536;              // staged in-list entries per tile (m
 constexpr int MSG_CAP = 384;               // random-edge messages parked per tile (mean ~146)
 constexpr uint16_t POS_NONE = 0xFFFF, POS_GLOBAL = 0xFFFE;
 
+// Staged ranges are moved by 16-byte LDS-DMA (global_load_lds_dwordx4) from a
+// 16-byte aligned start: every array has 8 words of slack for the alignment.
+constexpr int DMA_SLACK = 8;
+
 struct TileLds {
-    uint32_t rows[W_ROWS];     // direction bytes of [j0 - H, j1 + H)
-    uint32_t xm[W_PLANE];      // direction bytes of [j0 - g^2, j1 - g^2)
-    uint32_t xp[W_PLANE];      // direction bytes of [j0 + g^2, j1 + g^2)
-    uint32_t off[TILE + 1];    // in_off[j0 .. j1]
-    uint32_t src[SRC_CAP];     // in_src[in_off[j0] .. in_off[j1])
+    uint32_t rows[W_ROWS + DMA_SLACK];   // direction bytes of [j0 - H, j1 + H)
+    uint32_t xm[W_PLANE + DMA_SLACK];    // direction bytes of [j0 - g^2, j1 - g^2)
+    uint32_t xp[W_PLANE + DMA_SLACK];    // direction bytes of [j0 + g^2, j1 + g^2)
+    uint32_t off[TILE + 1 + DMA_SLACK];  // in_off[j0 .. j1]
+    uint32_t src[SRC_CAP + DMA_SLACK];   // in_src[in_off[j0] .. in_off[j1])
     uint32_t sent[SRC_CAP / 4];  // gossip: byte per staged in-edge, sender used its random edge
     uint16_t pos[SRC_CAP];     // push-sum: slot of the edge's parked message (POS_NONE: not sent)
     double2 msg[MSG_CAP];      // push-sum: random-edge messages gathered by the flattened pass
@@ -94,28 +98,130 @@ __device__ __forceinline__ uint32_t stage_bytes(uint32_t* lds, const uint8_t* nb
     return ws;
 }
 
+
+typedef __attribute__((address_space(1))) void gvoid_t;
+typedef __attribute__((address_space(3))) void lvoid_t;
+
+// Copy nbytes (rounded up to 16) from a 16-byte aligned global address into LDS
+// with LDS-DMA: no VGPR round trip and no wait inside the loop, so every
+// staging copy of a tile is in flight at once (retired by the next
+// __syncthreads, which waits vmcnt(0)).  One wave-instruction moves 1 KiB.
+__device__ __forceinline__ void dma_copy(void* lds, const char* g16, uint32_t nbytes) {
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint32_t c = (threadIdx.x >> 6) * 1024u; c < nbytes; c += TPB * 16u) {
+        const uint32_t o = c + lane * 16u;
+        if (o < nbytes)
+            __builtin_amdgcn_global_load_lds((gvoid_t*)(g16 + o), (lvoid_t*)(reinterpret_cast<char*>(lds) + c), 16, 0,
+                                             0);
+    }
+}
+
+// LDS-DMA version of stage_bytes: node bytes nb[lo, hi) clamped to [ext_lo,
+// ext_hi); returns the node id of LDS byte 0 (up to 15 bytes below lo).  Reads
+// at most 15 bytes past hi (node arrays are padded).
+__device__ __forceinline__ uint32_t dma_stage_bytes(uint32_t* lds, const uint8_t* nb, int64_t lo, int64_t hi,
+                                                    uint32_t ext_lo, uint32_t ext_hi) {
+    if (lo < (int64_t)ext_lo) lo = ext_lo;
+    if (hi > (int64_t)ext_hi) hi = ext_hi;
+    const char* p = reinterpret_cast<const char*>(nb + lo);
+    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 15u);
+    if (hi > lo) dma_copy(lds, p - mis, (uint32_t)(hi - lo) + mis);
+    return (uint32_t)lo - mis;
+}
+
+// LDS-DMA of the words w[lo, hi); returns how many words below lo were staged
+// (w[lo + i] lands in lds[i + returned]).  Reads at most 3 words past hi
+// (the in-list arrays are padded).
+__device__ __forceinline__ uint32_t dma_stage_words(uint32_t* lds, const uint32_t* w, uint32_t lo, uint32_t hi) {
+    const char* p = reinterpret_cast<const char*>(w + lo);
+    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 15u);
+    if (hi > lo) dma_copy(lds, p - mis, (hi - lo) * 4u + mis);
+    return mis >> 2;
+}
+
 template <typename T>
 __device__ __forceinline__ T ld_agent(const T* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// XCD-contiguous tile walk: blocks with equal blockIdx % 8 own one contiguous
-// eighth of the tiles (speed only -- any placement is correct).
+// Tile walks (speed only -- any placement is correct; every tile of the slab
+// is visited exactly once).  Blocks with equal blockIdx % 8 share an XCD.
+//   walk 0: XCD-contiguous eighths of the tile range;
+//   walk 1: one global sweep (tile t -> block t % grid);
+//   walk 2 (3D / Imp3D): x-window walk.  Each XCD owns an eighth of the slab's
+//     x-planes, cut into windows of ~wx planes; inside a window the walk is
+//     x-fastest: item u -> plane x = x_w + u % nx_w, k-th tile starting in that
+//     plane.  The blocks resident on an XCD at one time then work on the same
+//     in-plane position of ~wx consecutive planes (x+-1 neighbours) and of a few
+//     consecutive k (y+-1 rows), so lattice gathers and the x+-1 byte planes hit
+//     the XCD's L2 instead of HBM.
 struct TileWalk {
     uint32_t t, end, step;
-    __device__ TileWalk(uint32_t ntiles, uint32_t walk) {
+    // walk 2 only
+    uint32_t mode, tb, tend, g2, x0, xa, nxa, kp, nwin;
+    __device__ TileWalk(const RoundArgs& a) {
         const uint32_t G = gridDim.x;
-        if (walk == 0 && G >= 8 && (G & 7) == 0) {
+        mode = a.walk;
+        if (mode == 2 && a.G.g2 && G >= 8 && (G & 7) == 0) {
+            const uint32_t c = blockIdx.x & 7;
+            g2 = a.G.g2;
+            tb = a.lo / TILE;
+            tend = (uint32_t)(((uint64_t)a.lo + a.nloc + TILE - 1) / TILE);
+            x0 = a.lo / g2;
+            const uint32_t X0 = x0, nx = a.nloc / g2;
+            xa = X0 + (uint32_t)((uint64_t)nx * c / 8);
+            nxa = X0 + (uint32_t)((uint64_t)nx * (c + 1) / 8) - xa;
+            kp = (g2 + TILE - 1) / TILE + 1;
+            nwin = a.wx ? (nxa + a.wx - 1) / a.wx : 1u;
+            if (nwin == 0) nwin = 1;
+            t = blockIdx.x >> 3;
+            end = nxa * kp;
+            step = G >> 3;
+        } else if (mode == 0 && G >= 8 && (G & 7) == 0) {
+            mode = 0;
             const uint32_t x = blockIdx.x & 7, k = blockIdx.x >> 3;
-            const uint32_t lo = (uint32_t)((uint64_t)ntiles * x / 8);
-            end = (uint32_t)((uint64_t)ntiles * (x + 1) / 8);
+            const uint32_t lo = (uint32_t)((uint64_t)a.ntiles * x / 8);
+            end = (uint32_t)((uint64_t)a.ntiles * (x + 1) / 8);
             t = lo + k;
             step = G >> 3;
         } else {
+            mode = 1;
             t = blockIdx.x;
-            end = ntiles;
+            end = a.ntiles;
             step = G;
         }
+    }
+    // first global tile index of plane x (the slab's first tile may start below lo)
+    __device__ __forceinline__ uint32_t first(uint32_t x) const {
+        return x <= x0 ? tb : min((uint32_t)(((uint64_t)x * g2 + TILE - 1) / TILE), tend);
+    }
+    // tile (relative to lo / TILE) of walk item t; false: empty item (block-uniform)
+    __device__ __forceinline__ bool tile(uint32_t& rel) const {
+        if (mode != 2) {
+            rel = t;
+            return true;
+        }
+        const uint32_t pl = t / kp;  // planes of this XCD before the item's window start (approx.)
+        uint32_t v = (uint32_t)((uint64_t)pl * nwin / nxa);
+        if (v >= nwin) v = nwin - 1;
+        uint32_t xs = (uint32_t)((uint64_t)nxa * v / nwin);
+        while (v > 0 && xs * kp > t) {
+            --v;
+            xs = (uint32_t)((uint64_t)nxa * v / nwin);
+        }
+        for (;;) {
+            const uint32_t xe = (uint32_t)((uint64_t)nxa * (v + 1) / nwin);
+            if (v + 1 >= nwin || xe * kp > t) break;
+            ++v;
+            xs = xe;
+        }
+        const uint32_t xe = (uint32_t)((uint64_t)nxa * (v + 1) / nwin);
+        const uint32_t u = t - xs * kp, nxv = xe - xs;
+        const uint32_t x = xa + xs + u % nxv, k = u / nxv;
+        const uint32_t ti = first(x) + k;
+        if (ti >= first(x + 1)) return false;
+        rel = ti - tb;
+        return true;
     }
 };
 
@@ -189,18 +295,26 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
     uint32_t alerts = 0, newly = 0;
     const int lane = threadIdx.x & 63;
 
-    for (TileWalk tw(a.ntiles, a.walk); tw.t < tw.end; tw.t += tw.step) {
+    // the next tile's in-edge range is loaded one tile ahead (two uniform loads),
+    // so the senders can be staged in the same phase as everything else
+    uint32_t pf_tile = 0xFFFFFFFFu, pf_lo = 0, pf_hi = 0;
+    for (TileWalk tw(a); tw.t < tw.end; tw.t += tw.step) {
+        uint32_t ti;
+        if (!tw.tile(ti)) continue;
         // tiles sit on global multiples of TILE (4-aligned word I/O, 64-aligned
         // ballot words); the slab's first and last tile may be partial
-        const uint32_t T = (a.lo / TILE + tw.t) * TILE;
+        const uint32_t T = (a.lo / TILE + ti) * TILE;
         const uint32_t j0 = max(a.lo, T);
         const uint32_t j1 = min(a.lo + a.nloc, T + TILE);
-        // the tile's in-edge range first (two uniform loads), so the senders can be
-        // staged in the same phase as everything else
         uint32_t e_lo = 0, e_hi = 0;
         if (TOPO == IMP3D) {
-            e_lo = a.in_off[j0];
-            e_hi = a.in_off[j1];
+            if (pf_tile == ti) {
+                e_lo = pf_lo;
+                e_hi = pf_hi;
+            } else {
+                e_lo = a.in_off[j0];
+                e_hi = a.in_off[j1];
+            }
         }
         // own (s, w): issue first, consumed after staging
         double2 own[NPT];
@@ -209,18 +323,29 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
             const uint32_t j = T + k * TPB + threadIdx.x;
             own[k] = (j >= j0 && j < j1) ? swc[j] : make_double2(0.0, 1.0);
         }
-        const uint32_t b_rows = stage_bytes(L.rows, a.nbc, (int64_t)j0 - H, (int64_t)j1 + H, a.ext_lo, a.ext_hi);
+        // every staging copy of the tile in flight at once (LDS-DMA)
+        const uint32_t b_rows = dma_stage_bytes(L.rows, a.nbc, (int64_t)j0 - H, (int64_t)j1 + H, a.ext_lo, a.ext_hi);
         uint32_t b_xm = 0, b_xp = 0;
         if (TOPO != LINE) {
-            b_xm = stage_bytes(L.xm, a.nbc, (int64_t)j0 - G.g2, (int64_t)j1 - G.g2, a.ext_lo, a.ext_hi);
-            b_xp = stage_bytes(L.xp, a.nbc, (int64_t)j0 + G.g2, (int64_t)j1 + G.g2, a.ext_lo, a.ext_hi);
+            b_xm = dma_stage_bytes(L.xm, a.nbc, (int64_t)j0 - G.g2, (int64_t)j1 - G.g2, a.ext_lo, a.ext_hi);
+            b_xp = dma_stage_bytes(L.xp, a.nbc, (int64_t)j0 + G.g2, (int64_t)j1 + G.g2, a.ext_lo, a.ext_hi);
         }
         const uint32_t cnt = e_hi - e_lo;
         const bool staged = cnt <= (uint32_t)SRC_CAP;
+        int o_off = 0, o_src = 0;  // L.off[jl + o_off] = in_off[T + jl]; L.src[q + o_src] = in_src[e_lo + q]
         if (TOPO == IMP3D) {
-            for (uint32_t q = j0 - T + threadIdx.x; q <= j1 - T; q += TPB) L.off[q] = a.in_off[T + q];
-            if (staged)
-                for (uint32_t q = threadIdx.x; q < cnt; q += TPB) L.src[q] = in_src[e_lo + q];
+            o_off = (int)dma_stage_words(L.off, a.in_off, j0, j1 + 1) - (int)(j0 - T);
+            if (staged) o_src = (int)dma_stage_words(L.src, in_src, e_lo, e_hi);
+            // prefetch the next tile's in-edge range
+            TileWalk nw = tw;
+            nw.t += nw.step;
+            uint32_t nti;
+            if (nw.t < nw.end && nw.tile(nti)) {
+                const uint32_t nT = (a.lo / TILE + nti) * TILE;
+                pf_lo = a.in_off[max(a.lo, nT)];
+                pf_hi = a.in_off[min(a.lo + a.nloc, nT + TILE)];
+                pf_tile = nti;
+            }
         }
         __syncthreads();
         if (TOPO == IMP3D) {
@@ -241,7 +366,7 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
 #pragma unroll
                 for (int m = 0; m < FU; ++m) {
                     const uint32_t q = threadIdx.x + m * TPB;
-                    isrc[m] = q < cnt ? L.src[q] : 0u;
+                    isrc[m] = q < cnt ? L.src[q + o_src] : 0u;
                 }
 #pragma unroll
                 for (int m = 0; m < FU; ++m) {
@@ -337,7 +462,7 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                     }
                 }
                 if (TOPO == IMP3D && !(GP_ABLATE & ABL_NO_INLIST)) {
-                    const uint32_t e_b = L.off[jl], e_e = L.off[jl + 1];
+                    const uint32_t e_b = L.off[jl + o_off], e_e = L.off[jl + 1 + o_off];
                     for (uint32_t e = e_b; e < e_e; ++e) {
                         bool sent = false;
                         double2 mi = make_double2(0.0, 0.0);
@@ -346,7 +471,7 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                             sent = p != POS_NONE;
                             if (p < (uint16_t)MSG_CAP) mi = L.msg[p];
                             else if (p == POS_GLOBAL) {
-                                const uint32_t i = L.src[e - e_lo];
+                                const uint32_t i = L.src[e - e_lo + o_src];
                                 mi = (REMOTE && i - a.lo >= a.nloc) ? a.rmsg[e] : ld_sw(swc + i);
                             }
                         } else {  // rare: tile in-degree above SRC_CAP
@@ -467,8 +592,10 @@ __global__ __launch_bounds__(TPB, GP_MINB2) void k_ps_tile2(RoundArgs a, uint32_
     const int lane = threadIdx.x & 63;
     uint32_t* const list = reinterpret_cast<uint32_t*>(L.u.msg);
 
-    for (TileWalk tw(a.ntiles, a.walk); tw.t < tw.end; tw.t += tw.step) {
-        const uint32_t T = (a.lo / TILE + tw.t) * TILE;
+    for (TileWalk tw(a); tw.t < tw.end; tw.t += tw.step) {
+        uint32_t ti;
+        if (!tw.tile(ti)) continue;
+        const uint32_t T = (a.lo / TILE + ti) * TILE;
         const uint32_t j0 = max(a.lo, T);
         const uint32_t j1 = min(a.lo + a.nloc, T + TILE);
         uint32_t e_lo = 0, e_hi = 0;
@@ -779,10 +906,12 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_gossip_tile(RoundArgs a, uint3
     uint32_t alerts = 0;
     const int lane = threadIdx.x & 63;
 
-    for (TileWalk tw(a.ntiles, a.walk); tw.t < tw.end; tw.t += tw.step) {
+    for (TileWalk tw(a); tw.t < tw.end; tw.t += tw.step) {
+        uint32_t ti;
+        if (!tw.tile(ti)) continue;
         // tiles sit on global multiples of TILE (4-aligned word I/O, 64-aligned
         // ballot words); the slab's first and last tile may be partial
-        const uint32_t T = (a.lo / TILE + tw.t) * TILE;
+        const uint32_t T = (a.lo / TILE + ti) * TILE;
         const uint32_t j0 = max(a.lo, T);
         const uint32_t j1 = min(a.lo + a.nloc, T + TILE);
         uint32_t e_lo = 0, e_hi = 0;
@@ -796,16 +925,17 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_gossip_tile(RoundArgs a, uint3
             const uint32_t j = T + k * TPB + threadIdx.x;
             c0[k] = (j >= j0 && j < j1) ? a.c[j] : (int32_t)GOSSIP_DONE;
         }
-        const uint32_t b_rows = stage_bytes(L.rows, a.nbc, (int64_t)j0 - H, (int64_t)j1 + H, a.ext_lo, a.ext_hi);
+        const uint32_t b_rows = dma_stage_bytes(L.rows, a.nbc, (int64_t)j0 - H, (int64_t)j1 + H, a.ext_lo, a.ext_hi);
         uint32_t b_xm = 0, b_xp = 0;
         if (TOPO != LINE) {
-            b_xm = stage_bytes(L.xm, a.nbc, (int64_t)j0 - G.g2, (int64_t)j1 - G.g2, a.ext_lo, a.ext_hi);
-            b_xp = stage_bytes(L.xp, a.nbc, (int64_t)j0 + G.g2, (int64_t)j1 + G.g2, a.ext_lo, a.ext_hi);
+            b_xm = dma_stage_bytes(L.xm, a.nbc, (int64_t)j0 - G.g2, (int64_t)j1 - G.g2, a.ext_lo, a.ext_hi);
+            b_xp = dma_stage_bytes(L.xp, a.nbc, (int64_t)j0 + G.g2, (int64_t)j1 + G.g2, a.ext_lo, a.ext_hi);
         }
         const uint32_t cnt = e_hi - e_lo;
         const bool staged = cnt <= (uint32_t)SRC_CAP;
+        int o_off = 0;  // L.off[jl + o_off] = in_off[T + jl]
         if (TOPO == IMP3D) {
-            for (uint32_t q = j0 - T + threadIdx.x; q <= j1 - T; q += TPB) L.off[q] = a.in_off[T + q];
+            o_off = (int)dma_stage_words(L.off, a.in_off, j0, j1 + 1) - (int)(j0 - T);
             if (staged) {
                 // all sender loads, then all bitmap loads, in flight together
                 constexpr int FU = SRC_CAP / TPB;
@@ -856,7 +986,7 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_gossip_tile(RoundArgs a, uint3
                         inc += (mask & 32u) && (lds_byte(L.rows, j - 1 - b_rows) & DIR_MASK) == 4u;
                     }
                     if (TOPO == IMP3D) {
-                        const uint32_t e_b = L.off[jl], e_e = L.off[jl + 1];
+                        const uint32_t e_b = L.off[jl + o_off], e_e = L.off[jl + 1 + o_off];
                         if (staged) {
                             for (uint32_t e = e_b; e < e_e; ++e) inc += lds_byte(L.sent, e - e_lo);
                         } else {
@@ -959,6 +1089,7 @@ RoundArgs make_round_args(const DevState& S, uint32_t round) {
     a.seed_node = S.seed_node;
     a.ntiles = (S.lo + S.nloc + TILE - 1) / TILE - S.lo / TILE;
     a.walk = S.tile_walk;
+    a.wx = S.tile_wx;
     a.xs_len = 0;
     if (S.G.g2) {
         const uint32_t planes = S.nloc / S.G.g2, xs = S.col_xsegs ? S.col_xsegs : 1u;

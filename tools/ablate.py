@@ -17,13 +17,12 @@ CSRC = os.path.join(ROOT, "gossipprotocol_amd", "csrc")
 OUT = os.path.join(ROOT, "build", "ablate")
 # name -> (GP_NPT, GP_ABLATE mask) for gp_round.hip (mask bits at the top of gp_round.hip)
 VARIANTS = {
-    "base_npt4": (4, 0), "npt2": (2, 0), "npt8": (8, 0),
+    "base_npt4": (4, 0),
     "no_rgather": (4, 1), "no_lgather": (4, 2), "no_inlist": (4, 4), "no_nextdir": (4, 8),
-    "no_ephilox": (4, 16), "no_gathers": (4, 1 | 2), "stream_only": (4, 2 | 4 | 8),
-    "bitmap_only": (4, 32), "no_ratio": (4, 64),
-    "minb6": (4, 0, 6), "minb8": (4, 0, 8),
+    "no_ephilox": (4, 16), "no_gathers": (4, 1 | 2), "no_ratio": (4, 64),
     "cheap_decide": (4, 128), "cheap_no_nextdir": (4, 128 | 8),
     "no_xgather": (4, 256), "no_ygather": (4, 512), "no_zgather": (4, 1024),
+    "no_ephilox_nextdir": (4, 16 | 8), "all_off": (4, 16 | 2 | 8 | 64),
 }
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off"]
 
@@ -44,7 +43,8 @@ def build():
     objdir = os.path.join(ROOT, "build", "obj")
     for name in VARIANTS:
         so = os.path.join(OUT, f"lib_{name}.so")
-        objs = [os.path.join(objdir, f) for f in ("gp_api.o", "gp_kernels.o", "gp_wave.o", "gp_col.o", "gp_xchg.o")]
+        objs = [os.path.join(objdir, f) for f in ("gp_api.o", "gp_kernels.o", "gp_wave.o", "gp_col.o", "gp_xchg.o",
+                                                  "gp_full.o", "gp_xtile.o")]
         objs += [os.path.join(OUT, f"gp_round_{name}.o"), sort_obj]
         subprocess.check_call(["/opt/rocm/bin/hipcc", *FLAGS, "-shared", "-o", so, *objs, "-L/opt/rocm/lib", "-lrccl"])
 
@@ -61,7 +61,7 @@ def run(n, only=None):
                 "pre=0\nwhile s.info().active < P and pre < 300: pre += len(s.step(8))\n"
                 "s.sync(); s.kernel_stats(reset=True); s.step(10); s.sync()\n"
                 "ms,k,_=s.kernel_stats(); print(json.dumps(ms/k))\n") % (ROOT, n)
-        env = dict(os.environ, GOSSIP_HIP_LIB_EXPERIMENT=so, GP_GRID=os.environ.get("GP_GRID", "8192"))
+        env = dict(os.environ, GOSSIP_HIP_LIB_EXPERIMENT=so)
         if "@" in name:
             name, grid = name.split("@")
             so = os.path.join(OUT, f"lib_{name}.so")
@@ -72,7 +72,7 @@ def run(n, only=None):
             sys.exit(1)
         res[name] = float(out.stdout.strip().splitlines()[-1])
         print(f"{name:14s} {res[name]:8.2f} ms/round", flush=True)
-    for grid in ((1536, 3072, 8192, 16384, 65536) if not only else ()):
+    for grid in ((8192, 16384, 32768) if not only and os.environ.get("ABLATE_GRIDS") else ()):
         so = os.path.join(OUT, "lib_base_npt4.so")
         code = ("import sys,json; sys.path.insert(0,%r)\n"
                 "from gossipprotocol_amd import Simulation\n"
