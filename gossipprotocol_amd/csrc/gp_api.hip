@@ -265,6 +265,10 @@ int alloc_slab(gp_sim* s, Slab& sl, int r) {
             (rc = dev_alloc_t(s, &S.nb[0], next)))
             return rc;
         if (S.topo != FULL && (rc = dev_alloc_t(s, &S.nb[1], next))) return rc;
+        // zero sentinel just past the ids the slab holds: the tile kernels gather it for
+        // lattice directions without a sender (never written by any round)
+        for (int bb = 0; bb < 2; ++bb)
+            HIP_TRY(hipMemsetAsync(S.sw[bb] + (S.ext_hi - S.base), 0, sizeof(double2), s->stream));
     } else {
         if ((rc = dev_alloc_t(s, &S.c, nl))) return rc;
         if (S.topo == FULL) {
@@ -289,6 +293,17 @@ int alloc_slab(gp_sim* s, Slab& sl, int r) {
         HIP_TRY(sort_pairs(nullptr, tb, S.key[0], S.key[1], S.val[0], S.val[1], P, S.key_bits, s->stream));
         S.sort_tmp_bytes = tb;
         if ((rc = dev_alloc(s, &S.sort_tmp, tb))) return rc;
+    }
+    S.ebits = nullptr;
+    S.etot = nullptr;
+    S.emsg = nullptr;
+    const char* ge = std::getenv("GP_EDGES");
+    if (S.topo == IMP3D && S.alg == PUSHSUM && S.kernel == KERNEL_TILE && !(ge && ge[0] == '0')) {
+        // in-edge pass output (k_ps_edges): per tile EDGE_WORDS bitmap words, a count, EDGE_MSGS slots
+        const size_t nt = (size_t)((S.lo + (uint64_t)S.nloc + 1023) / 1024 - S.lo / 1024);
+        if ((rc = dev_alloc_t(s, &S.ebits, nt * EDGE_WORDS)) || (rc = dev_alloc_t(s, &S.etot, nt)) ||
+            (rc = dev_alloc_t(s, &S.emsg, nt * EDGE_MSGS)))
+            return rc;
     }
     if (S.topo == IMP3D) {
         S.rbits_words = S.kernel == KERNEL_COL ? col_rbits_words(S.nloc / S.G.g2, S.G.g)
@@ -822,9 +837,11 @@ void choose_kernel(gp_sim* s, int64_t nloc_max, int& kernel, uint32_t& col_xsegs
     if (const char* e = std::getenv("GP_GRID")) cap = std::max<int64_t>(1, std::atoll(e));
     if (const char* e = std::getenv("GP_XSEGS")) col_xsegs = (uint32_t)std::max(1, std::atoi(e));
     s->grid = (int)std::max<int64_t>(1, std::min(kernel == KERNEL_COL ? cap : blocks, cap));
-    walk = 0;
+    // tile walk: x-windows of 8 planes once every XCD gets a few windows (measured,
+    // profiles/r01: 18.2 -> 17.2 ms/round at P = 1e9), else XCD-contiguous eighths
+    walk = (lattice && g / s->world >= 64) ? 2u : 0u;
     if (const char* e = std::getenv("GP_WALK")) walk = (uint32_t)std::atoi(e);
-    wx = 40;
+    wx = 8;
     if (const char* e = std::getenv("GP_WX")) wx = (uint32_t)std::max(1, std::atoi(e));
 }
 

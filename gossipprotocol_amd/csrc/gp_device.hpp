@@ -36,6 +36,12 @@ constexpr uint32_t GOSSIP_DONE = 11;  // rumours >= 11 stops sending (Program.fs
 GP_HD void philox2(uint32_t node, uint32_t round, uint32_t stream, uint32_t k0, uint32_t k1,
                    uint32_t& x, uint32_t& y) {
     uint32_t c0 = node, c1 = round, c2 = stream, c3 = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+    // The key is wave-uniform: recompute its schedule per call on the scalar
+    // unit instead of letting the compiler keep 20 round keys live across a
+    // kernel (they end up spilled to VGPR lanes and cost a v_readlane each).
+    asm volatile("" : "+s"(k0), "+s"(k1));
+#endif
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
         if (r) {
@@ -173,6 +179,18 @@ GP_HD uint32_t slot_to_dir(uint32_t mask, uint32_t k) {
         }
     }
     return DIR_RANDOM;
+}
+
+// slot_to_dir with the interior-node case (all six lattice slots present) first.
+GP_HD uint32_t slot_to_dir_fast(uint32_t mask, uint32_t k) {
+    if (mask == 63u) return k < 6u ? k : (uint32_t)DIR_RANDOM;
+    return slot_to_dir(mask, k);
+}
+
+// Present-direction mask from lattice coordinates (same bits as present_mask).
+GP_HD uint32_t mask_xyz(uint32_t x, uint32_t y, uint32_t z, uint32_t gm) {
+    return (x > 0 ? 1u : 0u) | (x < gm ? 2u : 0u) | (y < gm ? 4u : 0u) | (y > 0 ? 8u : 0u) | (z < gm ? 16u : 0u) |
+           (z > 0 ? 32u : 0u);
 }
 
 // Full topology slot k of node i (Program.fs:211-216: all j != i, ascending).

@@ -79,6 +79,11 @@ struct DevState {
     uint32_t col_xsegs;
     uint32_t tile_walk;  // RoundArgs::walk
     uint32_t tile_wx;    // RoundArgs::wx
+    // Imp3D push-sum, tile kernel: output of the in-edge pass (k_ps_edges) per
+    // tile -- bitmap of used in-edges, message count, compact messages
+    unsigned long long* ebits;
+    uint32_t* etot;
+    double2* emsg;
 };
 
 // Arguments of the tiled round kernels (gp_round.hip): only what they read.
@@ -100,6 +105,9 @@ struct RoundArgs {
     uint32_t lo, nloc, ext_lo, ext_hi;  // owned ids [lo, lo + nloc); arrays hold [ext_lo, ext_hi)
     uint32_t walk;  // 0: XCD-contiguous eighths, 1: one global sweep (tile t -> block t % grid), 2: x-windows
     uint32_t wx;    // walk 2: planes per x-window
+    unsigned long long* ebits;  // in-edge pass output (k_ps_edges -> k_ps_tile<IMP3D, *, true>)
+    uint32_t* etot;
+    double2* emsg;
     uint32_t xs_len;  // k_ps_xtile: planes per x-segment
 };
 
@@ -142,6 +150,8 @@ hipError_t launch_col_rbits_init(const DevState& S, hipStream_t st);
 
 // ---- tiled round kernels (gp_round.hip)
 uint32_t round_tiles(uint32_t P);
+// in-edge pass buffers per tile: bitmap words, message slots
+constexpr uint32_t EDGE_WORDS = 24, EDGE_MSGS = 384;
 uint32_t rbits_words_for(uint32_t lo, uint32_t nloc);
 hipError_t launch_round_tile(const DevState& S, uint32_t round, int grid, hipStream_t st);
 hipError_t launch_rbits_init(const DevState& S, int grid, hipStream_t st);

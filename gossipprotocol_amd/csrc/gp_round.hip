@@ -20,6 +20,8 @@
 // Tiles are walked XCD-contiguously (blocks b and b+8 share an XCD on
 // MI355X), so the +-g rows a tile gathers from were just read by its XCD.
 // Built with -ffp-contract=off: the fold must round exactly like the oracle.
+#include <type_traits>
+
 #include "gp_internal.hpp"
 
 namespace gp {
@@ -27,6 +29,9 @@ namespace gp {
 // Experiment knobs (tools/ablate.py); the product build uses the defaults.
 #ifndef GP_NPT
 #define GP_NPT 4
+#endif
+#ifndef GP_NT_STORES
+#define GP_NT_STORES 1
 #endif
 #ifndef GP_ABLATE
 #define GP_ABLATE 0
@@ -48,7 +53,8 @@ namespace gp {
 #define ABL_CHEAP_DECIDE 128  // in-list: a one-multiply hash instead of the sender's Philox draw
 #define ABL_NO_XGATHER 256    // lattice: no gather from the x-1 / x+1 planes
 #define ABL_NO_YGATHER 512    // lattice: no gather from the y-1 / y+1 rows
-#define ABL_NO_ZGATHER 1024   // lattice: no gather from z-1 / z+1
+#define ABL_NO_ZGATHER 1024   // lattice: no gather from z-1 / z+1 (k_ps_tile2 only)
+#define ABL_NO_FAST 2048      // k_ps_tile: always the per-term halving fold
 
 namespace {
 
@@ -78,6 +84,28 @@ struct TileLds {
     uint32_t out[TILE / 4];    // next-round node bytes, stored as words
     uint32_t red[2][TPB / 64];
 };
+
+// k_ps_tile<IMP3D, *, EDGES = true>: the in-edge decisions and random-edge
+// gathers were done by k_ps_edges; the tile stages its in-edge bitmap and its
+// compact messages instead of the senders.
+constexpr int EW = SRC_CAP / 64;  // in-edge bitmap words per tile (k_ps_edges)
+
+struct TileLdsE {
+    uint32_t rows[W_ROWS + DMA_SLACK];
+    uint32_t xm[W_PLANE + DMA_SLACK];
+    uint32_t xp[W_PLANE + DMA_SLACK];
+    uint32_t off[TILE + 1 + DMA_SLACK];
+    unsigned long long bits[EW];   // bit q: staged in-edge q (tile order) was used by its sender
+    uint32_t bpre[EW];             // sent edges before word w
+    double2 msg[MSG_CAP];          // the tile's messages, in edge order
+    uint32_t out[TILE / 4];
+    uint32_t red[2][TPB / 64];
+};
+
+static_assert(EW == (int)EDGE_WORDS && MSG_CAP == (int)EDGE_MSGS && TILE == 1024, "gp_internal.hpp sizes");
+
+template <bool EDGES> struct TileLdsSel { using type = TileLds; };
+template <> struct TileLdsSel<true> { using type = TileLdsE; };
 
 __device__ __forceinline__ uint32_t lds_byte(const uint32_t* w, uint32_t idx) {
     return reinterpret_cast<const uint8_t*>(w)[idx];
@@ -227,6 +255,25 @@ struct TileWalk {
 
 __device__ __forceinline__ double2 ld_sw(const double2* p) { return *p; }
 
+// Next-round state is written once and not read again this round: non-temporal
+// stores keep it from displacing the current round's (s, w) in the XCD's L2,
+// where the neighbouring tiles' lattice gathers look for it.
+__device__ __forceinline__ void st_stream(double2* p, double2 v) {
+#if GP_NT_STORES
+    __builtin_nontemporal_store(v.x, &p->x);
+    __builtin_nontemporal_store(v.y, &p->y);
+#else
+    *p = v;
+#endif
+}
+__device__ __forceinline__ void st_stream(uint32_t* p, uint32_t v) {
+#if GP_NT_STORES
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+
 // ---- compacted-gather tile (k_ps_tile2)
 constexpr int MCAP2 = 1280;                 // lattice + random messages gathered per tile (mean ~1030)
 constexpr int MI2 = MCAP2 / TPB;            // gathers per thread
@@ -280,9 +327,10 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* lds, u
 // ---------------------------------------------------------------- push-sum
 // REMOTE: some in-edge senders live on other ranks (multi-GPU slabs); the
 // single-GPU build of the kernel has no exchange-tag paths at all.
-template <int TOPO, bool REMOTE>
+template <int TOPO, bool REMOTE, bool EDGES>
 __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t r) {
-    __shared__ TileLds L;
+    static_assert(!EDGES || TOPO == IMP3D, "edge pass is Imp3D only");
+    __shared__ typename TileLdsSel<EDGES>::type L;
     Ctl* ctl = a.ctl;
     if (ld_agent(&ctl->done)) return;
     const bool all_active = ld_agent(&ctl->all_active) != 0;
@@ -297,7 +345,7 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
 
     // the next tile's in-edge range is loaded one tile ahead (two uniform loads),
     // so the senders can be staged in the same phase as everything else
-    uint32_t pf_tile = 0xFFFFFFFFu, pf_lo = 0, pf_hi = 0;
+    uint32_t pf_tile = 0xFFFFFFFFu, pf_lo = 0, pf_hi = 0, pf_tot = 0;
     for (TileWalk tw(a); tw.t < tw.end; tw.t += tw.step) {
         uint32_t ti;
         if (!tw.tile(ti)) continue;
@@ -306,14 +354,16 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
         const uint32_t T = (a.lo / TILE + ti) * TILE;
         const uint32_t j0 = max(a.lo, T);
         const uint32_t j1 = min(a.lo + a.nloc, T + TILE);
-        uint32_t e_lo = 0, e_hi = 0;
+        uint32_t e_lo = 0, e_hi = 0, e_tot = 0;
         if (TOPO == IMP3D) {
             if (pf_tile == ti) {
                 e_lo = pf_lo;
                 e_hi = pf_hi;
+                e_tot = pf_tot;
             } else {
                 e_lo = a.in_off[j0];
                 e_hi = a.in_off[j1];
+                if (EDGES) e_tot = a.etot[ti];
             }
         }
         // own (s, w): issue first, consumed after staging
@@ -335,7 +385,15 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
         int o_off = 0, o_src = 0;  // L.off[jl + o_off] = in_off[T + jl]; L.src[q + o_src] = in_src[e_lo + q]
         if (TOPO == IMP3D) {
             o_off = (int)dma_stage_words(L.off, a.in_off, j0, j1 + 1) - (int)(j0 - T);
-            if (staged) o_src = (int)dma_stage_words(L.src, in_src, e_lo, e_hi);
+            if constexpr (EDGES) {
+                if (staged) {
+                    dma_copy(L.bits, reinterpret_cast<const char*>(a.ebits + (size_t)ti * EW), EW * 8u);
+                    dma_copy(L.msg, reinterpret_cast<const char*>(a.emsg + (size_t)ti * MSG_CAP),
+                             min(e_tot, (uint32_t)MSG_CAP) * 16u);
+                }
+            } else {
+                if (staged) o_src = (int)dma_stage_words(L.src, in_src, e_lo, e_hi);
+            }
             // prefetch the next tile's in-edge range
             TileWalk nw = tw;
             nw.t += nw.step;
@@ -344,11 +402,24 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                 const uint32_t nT = (a.lo / TILE + nti) * TILE;
                 pf_lo = a.in_off[max(a.lo, nT)];
                 pf_hi = a.in_off[min(a.lo + a.nloc, nT + TILE)];
+                if (EDGES) pf_tot = a.etot[nti];
                 pf_tile = nti;
             }
         }
         __syncthreads();
-        if (TOPO == IMP3D) {
+        if constexpr (EDGES) {
+            if (staged && threadIdx.x < 64) {  // sent edges before each bitmap word
+                const uint32_t c = threadIdx.x < (uint32_t)EW ? (uint32_t)__popcll(L.bits[threadIdx.x]) : 0u;
+                uint32_t incl = c;
+#pragma unroll
+                for (int o = 1; o < 32; o <<= 1) {
+                    const uint32_t t = __shfl_up(incl, o, 64);
+                    if (lane >= o) incl += t;
+                }
+                if (threadIdx.x < (uint32_t)EW) L.bpre[threadIdx.x] = incl - c;
+            }
+            __syncthreads();
+        } else if (TOPO == IMP3D) {
             if (staged) {
                 // Flattened, lane-balanced pass over the tile's in-edges: decide
                 // whether each sender used its random edge and gather its (s, w)
@@ -415,125 +486,225 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
             __syncthreads();
         }
 
+        // FAST (uniform): every node is active and no value can be subnormal, so the
+        // fold adds the senders' whole (s, w) and halves once at the end.  That is
+        // bit-identical to halving every term: x * 0.5 is exact and commutes with
+        // round-to-nearest for normal numbers, all values are >= 0, and a nonzero
+        // value is >= 2^-r after r rounds (>= 2^-1000 here, far from 2^-1022).
+        const bool fast = all_active && r < 1000u && G.P > 1u && !(GP_ABLATE & ABL_NO_FAST);
+        auto node_loop = [&](auto fast_tag) {
+            constexpr bool FAST = decltype(fast_tag)::value;
+            // lattice coordinates of this thread's first node, advanced by TPB per node
+            uint32_t cx = 0, cy = 0, cz = 0;
+            if (TOPO != LINE) {
+                const uint32_t j = T + threadIdx.x;
+                cx = fastdiv(j, G.div_g2);
+                const uint32_t rem = j - cx * G.g2;
+                cy = fastdiv(rem, G.div_g);
+                cz = rem - cy * G.g;
+            }
 #pragma unroll
-        for (int k = 0; k < NPT; ++k) {
-            const uint32_t jl = k * TPB + threadIdx.x;
-            const uint32_t j = T + jl;
-            const bool valid = j >= j0 && j < j1;
-            uint32_t dir = DIR_NONE;
-            if (valid) {
-                const uint32_t b = lds_byte(L.rows, j - b_rows);
-                const uint32_t mask = present_mask<TOPO>(j, G);
-                const uint32_t deg = popc6(mask) + (TOPO == IMP3D ? 1u : 0u);
-                bool active = (b & B_ACTIVE) != 0;
-                const double2 sv = own[k];
-                const bool halve = active && deg > 0;
-                double acc_s = halve ? sv.x * 0.5 : sv.x;
-                double acc_w = halve ? sv.y * 0.5 : sv.y;
-                // lattice senders: direction bytes from LDS, (s, w) gathered only for real senders
-                uint32_t from = 0;
-                if (TOPO == LINE) {
-                    if ((mask & 1u) && (lds_byte(L.rows, j - 1 - b_rows) & DIR_MASK) == 1u) from |= 1u;
-                    if ((mask & 2u) && (lds_byte(L.rows, j + 1 - b_rows) & DIR_MASK) == 0u) from |= 2u;
-                } else {
-                    if ((mask & 1u) && (lds_byte(L.xm, j - G.g2 - b_xm) & DIR_MASK) == 1u) from |= 1u;
-                    if ((mask & 2u) && (lds_byte(L.xp, j + G.g2 - b_xp) & DIR_MASK) == 0u) from |= 2u;
-                    if ((mask & 4u) && (lds_byte(L.rows, j + G.g - b_rows) & DIR_MASK) == 3u) from |= 4u;
-                    if ((mask & 8u) && (lds_byte(L.rows, j - G.g - b_rows) & DIR_MASK) == 2u) from |= 8u;
-                    if ((mask & 16u) && (lds_byte(L.rows, j + 1 - b_rows) & DIR_MASK) == 5u) from |= 16u;
-                    if ((mask & 32u) && (lds_byte(L.rows, j - 1 - b_rows) & DIR_MASK) == 4u) from |= 32u;
-                }
-                constexpr uint32_t ND = TOPO == LINE ? 2 : 6;
-                double2 m[ND];
-#pragma unroll
-                for (uint32_t d = 0; d < ND; ++d)
-                    m[d] = (!(GP_ABLATE & ABL_NO_LGATHER) && (from & (1u << d)) &&
-                            !((GP_ABLATE & ABL_NO_XGATHER) && TOPO != LINE && d < 2) &&
-                            !((GP_ABLATE & ABL_NO_YGATHER) && TOPO != LINE && (d == 2 || d == 3)) &&
-                            !((GP_ABLATE & ABL_NO_ZGATHER) && (TOPO == LINE || d >= 4)))
-                               ? ld_sw(swc + nbr<TOPO>(j, d, G))
-                               : make_double2(0.0, 0.0);
-                bool recv = from != 0;
-#pragma unroll
-                for (uint32_t d = 0; d < ND; ++d) {
-                    if (from & (1u << d)) {
-                        acc_s = acc_s + m[d].x * 0.5;
-                        acc_w = acc_w + m[d].y * 0.5;
+            for (int k = 0; k < NPT; ++k) {
+                const uint32_t jl = k * TPB + threadIdx.x;
+                const uint32_t j = T + jl;
+                const bool valid = j >= j0 && j < j1;
+                uint32_t dir = DIR_NONE;
+                if (TOPO != LINE && k > 0) {
+                    cz += TPB;
+                    if (cz >= G.g) {
+                        const uint32_t q = fastdiv(cz, G.div_g);
+                        cz -= q * G.g;
+                        cy += q;
+                        if (cy >= G.g) {
+                            const uint32_t q2 = fastdiv(cy, G.div_g);
+                            cy -= q2 * G.g;
+                            cx += q2;
+                        }
                     }
                 }
-                if (TOPO == IMP3D && !(GP_ABLATE & ABL_NO_INLIST)) {
-                    const uint32_t e_b = L.off[jl + o_off], e_e = L.off[jl + 1 + o_off];
-                    for (uint32_t e = e_b; e < e_e; ++e) {
-                        bool sent = false;
-                        double2 mi = make_double2(0.0, 0.0);
-                        if (staged) {
-                            const uint16_t p = L.pos[e - e_lo];
-                            sent = p != POS_NONE;
-                            if (p < (uint16_t)MSG_CAP) mi = L.msg[p];
-                            else if (p == POS_GLOBAL) {
-                                const uint32_t i = L.src[e - e_lo + o_src];
-                                mi = (REMOTE && i - a.lo >= a.nloc) ? a.rmsg[e] : ld_sw(swc + i);
-                            }
-                        } else {  // rare: tile in-degree above SRC_CAP
-                            const uint32_t i = in_src[e];
-                            if (REMOTE && i - a.lo >= a.nloc) {
-                                sent = a.rtag[e] == r;
-                                if (sent) mi = a.rmsg[e];
-                            } else {
-                                if (all_active) {
-                                    const uint32_t di = popc6(present_mask<IMP3D>(i, G)) + 1u;
-                                    sent = uniform(a.k0, a.k1, S_PUSHSUM, i, r, di) == di - 1u;
-                                } else {
-                                    sent = (rbc[(i >> 6) - (a.lo >> 6)] >> (i & 63)) & 1ull;
-                                }
-                                if (sent) mi = ld_sw(swc + i);
-                            }
-                        }
-                        if (sent) {
+                if (valid) {
+                    const uint32_t jr = j - b_rows;
+                    const uint32_t b = lds_byte(L.rows, jr);
+                    const uint32_t mask = TOPO == LINE ? present_mask<TOPO>(j, G) : mask_xyz(cx, cy, cz, G.g - 1u);
+                    const uint32_t deg = popc6(mask) + (TOPO == IMP3D ? 1u : 0u);
+                    bool active = (b & B_ACTIVE) != 0;
+                    const double2 sv = own[k];
+                    const bool halve = active && deg > 0;
+                    double acc_s, acc_w;
+                    if (FAST) {
+                        acc_s = sv.x;
+                        acc_w = sv.y;
+                    } else {
+                        acc_s = halve ? sv.x * 0.5 : sv.x;
+                        acc_w = halve ? sv.y * 0.5 : sv.y;
+                    }
+                    auto fold = [&](const double2 mi) {
+                        if (FAST) {
+                            acc_s = acc_s + mi.x;
+                            acc_w = acc_w + mi.y;
+                        } else {
                             acc_s = acc_s + mi.x * 0.5;
                             acc_w = acc_w + mi.y * 0.5;
-                            recv = true;
+                        }
+                    };
+                    // lattice senders from the staged direction bytes (absent neighbours read
+                    // a harmless in-range byte and are masked out)
+                    uint32_t from = 0;
+                    if (TOPO == LINE) {
+                        from |= ((mask & 1u) && (lds_byte(L.rows, (mask & 1u) ? jr - 1 : jr) & DIR_MASK) == 1u) ? 1u : 0u;
+                        from |= ((mask & 2u) && (lds_byte(L.rows, (mask & 2u) ? jr + 1 : jr) & DIR_MASK) == 0u) ? 2u : 0u;
+                    } else {
+                        const uint32_t bxm = lds_byte(L.xm, (mask & 1u) ? j - G.g2 - b_xm : 0u);
+                        const uint32_t bxp = lds_byte(L.xp, (mask & 2u) ? j + G.g2 - b_xp : 0u);
+                        const uint32_t byp = lds_byte(L.rows, (mask & 4u) ? jr + G.g : jr);
+                        const uint32_t bym = lds_byte(L.rows, (mask & 8u) ? jr - G.g : jr);
+                        const uint32_t bzp = lds_byte(L.rows, (mask & 16u) ? jr + 1 : jr);
+                        const uint32_t bzm = lds_byte(L.rows, (mask & 32u) ? jr - 1 : jr);
+                        from = ((bxm & DIR_MASK) == 1u ? 1u : 0u) | ((bxp & DIR_MASK) == 0u ? 2u : 0u) |
+                               ((byp & DIR_MASK) == 3u ? 4u : 0u) | ((bym & DIR_MASK) == 2u ? 8u : 0u) |
+                               ((bzp & DIR_MASK) == 5u ? 16u : 0u) | ((bzm & DIR_MASK) == 4u ? 32u : 0u);
+                        from &= mask;
+                    }
+                    // one gather per direction, all in flight together; a direction without a
+                    // sender reads the zero sentinel swc[ext_hi] (adding +0.0 is exact)
+                    constexpr uint32_t ND = TOPO == LINE ? 2 : 6;
+                    double2 m[ND];
+#pragma unroll
+                    for (uint32_t d = 0; d < ND; ++d) m[d] = ld_sw(swc + ((from >> d) & 1u ? nbr<TOPO>(j, d, G) : a.ext_hi));
+                    bool recv = from != 0;
+#pragma unroll
+                    for (uint32_t d = 0; d < ND; ++d) fold(m[d]);
+                    if constexpr (EDGES) {
+                        const uint32_t e_b = L.off[jl + o_off], e_e = L.off[jl + 1 + o_off];
+                        if (staged) {
+                            // the node's used in-edges: its window of the tile bitmap, walked
+                            // set bit by set bit (ascending sender = canonical order)
+                            for (uint32_t q0 = e_b - e_lo; q0 < e_e - e_lo; q0 += 64u) {
+                                const uint32_t n = min(64u, e_e - e_lo - q0);
+                                const uint32_t w = q0 >> 6, sh = q0 & 63u;
+                                unsigned long long win = L.bits[w] >> sh;
+                                if (sh && w + 1 < (uint32_t)EW) win |= L.bits[w + 1] << (64u - sh);
+                                if (n < 64u) win &= (1ull << n) - 1ull;
+                                while (win) {
+                                    const uint32_t q = q0 + (uint32_t)__builtin_ctzll(win);
+                                    win &= win - 1ull;
+                                    const uint32_t slot = L.bpre[q >> 6] +
+                                                          (uint32_t)__popcll(L.bits[q >> 6] & ((1ull << (q & 63u)) - 1ull));
+                                    double2 mi;
+                                    if (slot < (uint32_t)MSG_CAP) {
+                                        mi = L.msg[slot];
+                                    } else {  // rare: more messages than the tile's slots
+                                        const uint32_t i = in_src[e_lo + q];
+                                        mi = (REMOTE && i - a.lo >= a.nloc) ? a.rmsg[e_lo + q] : ld_sw(swc + i);
+                                    }
+                                    fold(mi);
+                                    recv = true;
+                                }
+                            }
+                        } else {  // rare: tile in-degree above SRC_CAP (k_ps_edges skipped it)
+                            for (uint32_t e = e_b; e < e_e; ++e) {
+                                const uint32_t i = in_src[e];
+                                bool sent;
+                                double2 mi = make_double2(0.0, 0.0);
+                                if (REMOTE && i - a.lo >= a.nloc) {
+                                    sent = a.rtag[e] == r;
+                                    if (sent) mi = a.rmsg[e];
+                                } else {
+                                    if (all_active) {
+                                        const uint32_t di = popc6(present_mask<IMP3D>(i, G)) + 1u;
+                                        sent = uniform(a.k0, a.k1, S_PUSHSUM, i, r, di) == di - 1u;
+                                    } else {
+                                        sent = (rbc[(i >> 6) - (a.lo >> 6)] >> (i & 63)) & 1ull;
+                                    }
+                                    if (sent) mi = ld_sw(swc + i);
+                                }
+                                if (sent) {
+                                    fold(mi);
+                                    recv = true;
+                                }
+                            }
+                        }
+                    } else if (TOPO == IMP3D && !(GP_ABLATE & ABL_NO_INLIST)) {
+                        const uint32_t e_b = L.off[jl + o_off], e_e = L.off[jl + 1 + o_off];
+                        for (uint32_t e = e_b; e < e_e; ++e) {
+                            bool sent = false;
+                            double2 mi = make_double2(0.0, 0.0);
+                            if (staged) {
+                                const uint16_t p = L.pos[e - e_lo];
+                                sent = p != POS_NONE;
+                                if (p < (uint16_t)MSG_CAP) mi = L.msg[p];
+                                else if (p == POS_GLOBAL) {
+                                    const uint32_t i = L.src[e - e_lo + o_src];
+                                    mi = (REMOTE && i - a.lo >= a.nloc) ? a.rmsg[e] : ld_sw(swc + i);
+                                }
+                            } else {  // rare: tile in-degree above SRC_CAP
+                                const uint32_t i = in_src[e];
+                                if (REMOTE && i - a.lo >= a.nloc) {
+                                    sent = a.rtag[e] == r;
+                                    if (sent) mi = a.rmsg[e];
+                                } else {
+                                    if (all_active) {
+                                        const uint32_t di = popc6(present_mask<IMP3D>(i, G)) + 1u;
+                                        sent = uniform(a.k0, a.k1, S_PUSHSUM, i, r, di) == di - 1u;
+                                    } else {
+                                        sent = (rbc[(i >> 6) - (a.lo >> 6)] >> (i & 63)) & 1ull;
+                                    }
+                                    if (sent) mi = ld_sw(swc + i);
+                                }
+                            }
+                            if (sent) {
+                                fold(mi);
+                                recv = true;
+                            }
                         }
                     }
-                }
-                uint32_t flags = b & (B_ACTIVE | B_CONV | (3u << CNT_SHIFT));
-                if (recv) {
-                    if (!(GP_ABLATE & ABL_NO_RATIO) && !(b & B_CONV)) {
-                        const double r_old = sv.x / sv.y;
-                        const double r_new = acc_s / acc_w;
-                        uint32_t cnt = (b >> CNT_SHIFT) & 3u;
-                        cnt = fabs(r_new - r_old) > 1e-10 ? 0u : cnt + 1u;
-                        flags = (flags & ~(3u << CNT_SHIFT)) | (cnt << CNT_SHIFT);
-                        if (cnt == 3) {
-                            flags |= B_CONV;
-                            ++alerts;
+                    if (FAST) {  // every node is active (deg > 0): halve once
+                        acc_s = acc_s * 0.5;
+                        acc_w = acc_w * 0.5;
+                    }
+                    uint32_t flags = b & (B_ACTIVE | B_CONV | (3u << CNT_SHIFT));
+                    if (recv) {
+                        if (!(GP_ABLATE & ABL_NO_RATIO) && !(b & B_CONV)) {
+                            const double r_old = sv.x / sv.y;
+                            const double r_new = acc_s / acc_w;
+                            uint32_t cnt = (b >> CNT_SHIFT) & 3u;
+                            cnt = fabs(r_new - r_old) > 1e-10 ? 0u : cnt + 1u;
+                            flags = (flags & ~(3u << CNT_SHIFT)) | (cnt << CNT_SHIFT);
+                            if (cnt == 3) {
+                                flags |= B_CONV;
+                                ++alerts;
+                            }
+                        }
+                        if (!active) {
+                            ++newly;
+                            flags |= B_ACTIVE;
+                            active = true;
                         }
                     }
-                    if (!active) {
-                        ++newly;
-                        flags |= B_ACTIVE;
-                        active = true;
+                    if (active && deg > 0)
+                        dir = (GP_ABLATE & ABL_NO_NEXTDIR)
+                                  ? (j % 7u) % (deg)
+                                  : slot_to_dir_fast(mask, uniform(a.k0, a.k1, S_PUSHSUM, j, r + 1, deg));
+                    reinterpret_cast<uint8_t*>(L.out)[jl] = (uint8_t)(flags | dir);
+                    st_stream(swn + j, make_double2(acc_s, acc_w));
+                }
+                if (TOPO == IMP3D) {
+                    const unsigned long long bits = __ballot(valid && dir == DIR_RANDOM);
+                    if (lane == 0) {  // the slab's first tile may start below lo: no word there
+                        const int64_t wi = (int64_t)((T + k * TPB + (threadIdx.x & ~63u)) >> 6) - (int64_t)(a.lo >> 6);
+                        if (wi >= 0) a.rbn[wi] = bits;
                     }
                 }
-                if (active && deg > 0)
-                    dir = (GP_ABLATE & ABL_NO_NEXTDIR) ? (j % 7u) % (deg) : slot_to_dir(mask, uniform(a.k0, a.k1, S_PUSHSUM, j, r + 1, deg));
-                reinterpret_cast<uint8_t*>(L.out)[jl] = (uint8_t)(flags | dir);
-                swn[j] = make_double2(acc_s, acc_w);
             }
-            if (TOPO == IMP3D) {
-                const unsigned long long bits = __ballot(valid && dir == DIR_RANDOM);
-                if (lane == 0) {  // the slab's first tile may start below lo: no word there
-                    const int64_t wi = (int64_t)((T + k * TPB + (threadIdx.x & ~63u)) >> 6) - (int64_t)(a.lo >> 6);
-                    if (wi >= 0) a.rbn[wi] = bits;
-                }
-            }
-        }
+        };
+        if (fast) node_loop(std::true_type{});
+        else node_loop(std::false_type{});
         __syncthreads();
         // node bytes out as words (allocations are padded past P)
         for (uint32_t w = threadIdx.x; w < (uint32_t)(TILE / 4); w += TPB) {
             const uint32_t jw = T + w * 4;
             if (jw >= j0 && jw + 4 <= j1) {
-                reinterpret_cast<uint32_t*>(a.nbn + T)[w] = L.out[w];
+                st_stream(reinterpret_cast<uint32_t*>(a.nbn + T) + w, L.out[w]);
             } else {
                 for (uint32_t b = 0; b < 4; ++b)
                     if (jw + b >= j0 && jw + b < j1) a.nbn[jw + b] = reinterpret_cast<const uint8_t*>(L.out)[w * 4 + b];
@@ -562,6 +733,98 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
         }
         if (x) atomicAdd(&ctl->round_alerts, (unsigned long long)x);
         if (y) atomicAdd(&ctl->round_active, (unsigned long long)y);
+    }
+}
+
+// ---------------------------------------------------------------- push-sum, in-edge pass (Imp3D)
+// Runs before k_ps_tile<IMP3D, *, true> in the same round.  For every tile
+// (same tiles as the round kernel) and every in-edge of it, in receiver order:
+// did the sender use its random edge this round (its Philox draw; the ballot
+// bitmap during activation; the exchange tag for senders on other ranks)?  The
+// answers go to ebits (one bit per edge, EW words per tile), the senders' (s, w)
+// are gathered and stored compactly in edge order (emsg, MSG_CAP slots per
+// tile, count in etot).  No block-wide phase waits on another tile's data, so
+// the Philox chains and the random gathers of many tiles overlap freely.
+template <bool REMOTE>
+__global__ __launch_bounds__(TPB) void k_ps_edges(RoundArgs a, uint32_t r) {
+    __shared__ uint32_t wcnt[EW];
+    Ctl* ctl = a.ctl;
+    if (ld_agent(&ctl->done)) return;
+    const bool all_active = ld_agent(&ctl->all_active) != 0;
+    const double2* __restrict__ swc = a.swc;
+    const uint64_t* __restrict__ rbc = a.rbc;
+    const Geom G = a.G;
+    constexpr int FU = SRC_CAP / TPB;
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    for (uint32_t ti = blockIdx.x; ti < a.ntiles; ti += gridDim.x) {
+        const uint32_t T = (a.lo / TILE + ti) * TILE;
+        const uint32_t j0 = max(a.lo, T);
+        const uint32_t j1 = min(a.lo + a.nloc, T + TILE);
+        const uint32_t e_lo = a.in_off[j0], e_hi = a.in_off[j1];
+        const uint32_t cnt = e_hi - e_lo;
+        if (cnt > (uint32_t)SRC_CAP) continue;  // the round kernel handles such a tile by itself
+        uint32_t isrc[FU];
+#pragma unroll
+        for (int m = 0; m < FU; ++m) {
+            const uint32_t q = threadIdx.x + m * TPB;
+            isrc[m] = q < cnt ? a.in_src[e_lo + q] : 0u;
+        }
+        bool snt[FU];
+#pragma unroll
+        for (int m = 0; m < FU; ++m) {
+            const uint32_t q = threadIdx.x + m * TPB;
+            const uint32_t i = isrc[m];
+            bool sent = false;
+            if (q < cnt) {
+                if (REMOTE && i - a.lo >= a.nloc) {
+                    sent = a.rtag[e_lo + q] == r;
+                } else if (all_active) {
+                    const uint32_t di = popc6(present_mask<IMP3D>(i, G)) + 1u;
+                    sent = uniform(a.k0, a.k1, S_PUSHSUM, i, r, di) == di - 1u;
+                } else {
+                    sent = (rbc[(i >> 6) - (a.lo >> 6)] >> (i & 63)) & 1ull;
+                }
+            }
+            snt[m] = sent;
+        }
+        double2 v[FU];
+#pragma unroll
+        for (int m = 0; m < FU; ++m) {
+            v[m] = make_double2(0.0, 0.0);
+            if (snt[m]) {
+                const uint32_t q = threadIdx.x + m * TPB;
+                v[m] = (REMOTE && isrc[m] - a.lo >= a.nloc) ? a.rmsg[e_lo + q] : ld_sw(swc + isrc[m]);
+            }
+        }
+        // edge q = m * TPB + wv * 64 + lane sits in bitmap word m * 4 + wv
+        unsigned long long bal[FU];
+#pragma unroll
+        for (int m = 0; m < FU; ++m) {
+            bal[m] = __ballot(snt[m]);
+            if (lane == 0) {
+                a.ebits[(size_t)ti * EW + m * (TPB / 64) + wv] = bal[m];
+                wcnt[m * (TPB / 64) + wv] = (uint32_t)__popcll(bal[m]);
+            }
+        }
+        __syncthreads();
+        const uint32_t c = lane < (uint32_t)EW ? wcnt[lane] : 0u;
+        uint32_t incl = c;
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) {
+            const uint32_t t = __shfl_up(incl, o, 64);
+            if (lane >= (uint32_t)o) incl += t;
+        }
+        const uint32_t excl = incl - c;
+        const uint32_t total = __shfl(incl, EW - 1, 64);
+#pragma unroll
+        for (int m = 0; m < FU; ++m) {
+            const uint32_t slot = __shfl(excl, m * (TPB / 64) + wv, 64) +
+                                  __builtin_amdgcn_mbcnt_hi((uint32_t)(bal[m] >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)bal[m], 0u));
+            if (snt[m] && slot < (uint32_t)MSG_CAP) a.emsg[(size_t)ti * MSG_CAP + slot] = v[m];
+        }
+        if (threadIdx.x == 0) a.etot[ti] = total;
+        __syncthreads();
     }
 }
 
@@ -1089,6 +1352,9 @@ RoundArgs make_round_args(const DevState& S, uint32_t round) {
     a.seed_node = S.seed_node;
     a.ntiles = (S.lo + S.nloc + TILE - 1) / TILE - S.lo / TILE;
     a.walk = S.tile_walk;
+    a.ebits = S.ebits;
+    a.etot = S.etot;
+    a.emsg = S.emsg;
     a.wx = S.tile_wx;
     a.xs_len = 0;
     if (S.G.g2) {
@@ -1115,11 +1381,22 @@ hipError_t launch_round_tile(const DevState& S, uint32_t round, int grid, hipStr
         }
     } else if (S.alg == PUSHSUM) {
         switch (S.topo) {
-            case LINE: hipLaunchKernelGGL((k_ps_tile<LINE, false>), g, b, 0, st, a, round); break;
-            case GRID3D: hipLaunchKernelGGL((k_ps_tile<GRID3D, false>), g, b, 0, st, a, round); break;
+            case LINE: hipLaunchKernelGGL((k_ps_tile<LINE, false, false>), g, b, 0, st, a, round); break;
+            case GRID3D: hipLaunchKernelGGL((k_ps_tile<GRID3D, false, false>), g, b, 0, st, a, round); break;
             default:
-                if (remote) hipLaunchKernelGGL((k_ps_tile<IMP3D, true>), g, b, 0, st, a, round);
-                else hipLaunchKernelGGL((k_ps_tile<IMP3D, false>), g, b, 0, st, a, round);
+                if (S.emsg) {  // in-edge pass first (same stream)
+                    if (remote) {
+                        hipLaunchKernelGGL((k_ps_edges<true>), g, b, 0, st, a, round);
+                        hipLaunchKernelGGL((k_ps_tile<IMP3D, true, true>), g, b, 0, st, a, round);
+                    } else {
+                        hipLaunchKernelGGL((k_ps_edges<false>), g, b, 0, st, a, round);
+                        hipLaunchKernelGGL((k_ps_tile<IMP3D, false, true>), g, b, 0, st, a, round);
+                    }
+                } else if (remote) {
+                    hipLaunchKernelGGL((k_ps_tile<IMP3D, true, false>), g, b, 0, st, a, round);
+                } else {
+                    hipLaunchKernelGGL((k_ps_tile<IMP3D, false, false>), g, b, 0, st, a, round);
+                }
                 break;
         }
     } else {

@@ -62,6 +62,7 @@ def run(n, only=None):
                 "s.sync(); s.kernel_stats(reset=True); s.step(10); s.sync()\n"
                 "ms,k,_=s.kernel_stats(); print(json.dumps(ms/k))\n") % (ROOT, n)
         env = dict(os.environ, GOSSIP_HIP_LIB_EXPERIMENT=so)
+        env.setdefault("GP_EDGES", "0")  # the ablation switches act on the single-kernel round
         if "@" in name:
             name, grid = name.split("@")
             so = os.path.join(OUT, f"lib_{name}.so")
