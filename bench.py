@@ -134,7 +134,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    sim = Simulation(args.nodes, args.topology, args.algorithm, seed=args.seed, device=local_rank,
+    # GP_BENCH_DEVICE pins every rank to one device (multi-process rehearsal on a one-GPU box)
+    device = int(os.environ.get("GP_BENCH_DEVICE", local_rank))
+    sim = Simulation(args.nodes, args.topology, args.algorithm, seed=args.seed, device=device,
                      kernel_timing=True, rank=rank, world=world, dist=dist)
     P = sim.population
     t_pre = time.perf_counter()
@@ -197,7 +199,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args)
     if rank == 0 and world == 1 and args.converge:
-        with Simulation(args.nodes, args.topology, args.algorithm, seed=args.seed, device=local_rank) as s2:
+        with Simulation(args.nodes, args.topology, args.algorithm, seed=args.seed, device=device) as s2:
             res = s2.run()
             out["config"]["convergence"] = {"rounds": res.rounds, "converged": res.status == L.GP_STATUS_CONVERGED,
                                             "elapsed_ms": res.elapsed_ms}

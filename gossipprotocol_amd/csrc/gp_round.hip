@@ -95,8 +95,8 @@ struct TileLdsE {
     uint32_t xm[W_PLANE + DMA_SLACK];
     uint32_t xp[W_PLANE + DMA_SLACK];
     uint32_t off[TILE + 1 + DMA_SLACK];
-    unsigned long long bits[EW];   // bit q: staged in-edge q (tile order) was used by its sender
-    uint32_t bpre[EW];             // sent edges before word w
+    unsigned long long bits[EW + 1];  // bit q: staged in-edge q (tile order) was used by its sender; bits[EW] = 0
+    uint32_t bpre[EW + 1];            // sent edges before word w; bpre[EW] = all of them
     double2 msg[MSG_CAP];          // the tile's messages, in edge order
     uint32_t out[TILE / 4];
     uint32_t red[2][TPB / 64];
@@ -104,7 +104,24 @@ struct TileLdsE {
 
 static_assert(EW == (int)EDGE_WORDS && MSG_CAP == (int)EDGE_MSGS && TILE == 1024, "gp_internal.hpp sizes");
 
-template <bool EDGES> struct TileLdsSel { using type = TileLds; };
+// k_ps_tile<*, *, EDGES = false>: the tile decides its in-edges itself and
+// parks the used ones' messages compactly in edge order (same layout as
+// k_ps_edges' output).
+struct TileLdsP {
+    uint32_t rows[W_ROWS + DMA_SLACK];
+    uint32_t xm[W_PLANE + DMA_SLACK];
+    uint32_t xp[W_PLANE + DMA_SLACK];
+    uint32_t off[TILE + 1 + DMA_SLACK];
+    uint32_t src[SRC_CAP + DMA_SLACK];  // in_src[in_off[j0] .. in_off[j1])
+    unsigned long long bits[EW + 1];
+    uint32_t bpre[EW + 1];
+    uint32_t wcnt[EW];
+    double2 msg[MSG_CAP];
+    uint32_t out[TILE / 4];
+    uint32_t red[2][TPB / 64];
+};
+
+template <bool EDGES> struct TileLdsSel { using type = TileLdsP; };
 template <> struct TileLdsSel<true> { using type = TileLdsE; };
 
 __device__ __forceinline__ uint32_t lds_byte(const uint32_t* w, uint32_t idx) {
@@ -416,22 +433,21 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                     const uint32_t t = __shfl_up(incl, o, 64);
                     if (lane >= o) incl += t;
                 }
-                if (threadIdx.x < (uint32_t)EW) L.bpre[threadIdx.x] = incl - c;
+                if (threadIdx.x <= (uint32_t)EW) L.bpre[threadIdx.x] = incl - c;
+                if (threadIdx.x == (uint32_t)EW) L.bits[EW] = 0ull;
             }
             __syncthreads();
         } else if (TOPO == IMP3D) {
             if (staged) {
                 // Flattened, lane-balanced pass over the tile's in-edges: decide
-                // whether each sender used its random edge and gather its (s, w)
-                // into a compact LDS buffer, so the per-receiver loop below
-                // neither runs a wave's max in-degree of Philox draws nor waits
-                // on a random HBM read.  All FU decisions of a thread are
-                // independent (ILP across the Philox chains), then all gathers
-                // are issued together; slots come from a per-wave ballot prefix
-                // into the wave's own quarter of the buffer.  The slot order is
-                // irrelevant: the fold walks edges in canonical order.
+                // whether each sender used its random edge (all FU Philox chains of a
+                // thread independent), issue all gathers of the used edges' (s, w),
+                // and park them compactly in edge order: bit q of the tile bitmap
+                // marks edge q used, its message sits at slot prefix(q).  A node's
+                // messages are then one contiguous, canonically ordered slot range.
+                // Edge q = m * TPB + wave * 64 + lane lives in bitmap word m * 4 + wave.
                 constexpr int FU = SRC_CAP / TPB;
-                constexpr uint32_t WCAP = MSG_CAP / (TPB / 64);
+                const uint32_t wv = threadIdx.x >> 6;
                 uint32_t isrc[FU];
                 bool snt[FU];
 #pragma unroll
@@ -470,17 +486,32 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                                : (REMOTE && isrc[m] - a.lo >= a.nloc) ? a.rmsg[e_lo + q] : ld_sw(swc + isrc[m]);
                     }
                 }
-                const uint32_t wbase = (threadIdx.x >> 6) * WCAP;
-                uint32_t wn = 0;
+                unsigned long long bal[FU];
 #pragma unroll
                 for (int m = 0; m < FU; ++m) {
-                    const uint32_t q = threadIdx.x + m * TPB;
-                    const unsigned long long bal = __ballot(snt[m]);
-                    const uint32_t slot = wn + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                    wn += (uint32_t)__popcll(bal);
-                    if (q < cnt) L.pos[q] = !snt[m] ? POS_NONE : (slot < WCAP ? (uint16_t)(wbase + slot) : POS_GLOBAL);
-                    if (snt[m] && slot < WCAP) L.msg[wbase + slot] = v[m];
+                    bal[m] = __ballot(snt[m]);
+                    if (lane == 0) {
+                        L.bits[m * (TPB / 64) + wv] = bal[m];
+                        L.wcnt[m * (TPB / 64) + wv] = (uint32_t)__popcll(bal[m]);
+                    }
+                }
+                __syncthreads();
+                const uint32_t c = lane < EW ? L.wcnt[lane] : 0u;
+                uint32_t incl = c;
+#pragma unroll
+                for (int o = 1; o < 32; o <<= 1) {
+                    const uint32_t t = __shfl_up(incl, o, 64);
+                    if (lane >= o) incl += t;
+                }
+                const uint32_t excl = incl - c;
+                if (threadIdx.x <= (uint32_t)EW) L.bpre[threadIdx.x] = excl;
+                if (threadIdx.x == (uint32_t)EW) L.bits[EW] = 0ull;
+#pragma unroll
+                for (int m = 0; m < FU; ++m) {
+                    const uint32_t slot = __shfl(excl, m * (TPB / 64) + wv, 64) +
+                                          __builtin_amdgcn_mbcnt_hi((uint32_t)(bal[m] >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)bal[m], 0u));
+                    if (snt[m] && slot < (uint32_t)MSG_CAP) L.msg[slot] = v[m];
                 }
             }
             __syncthreads();
@@ -574,33 +605,35 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                     bool recv = from != 0;
 #pragma unroll
                     for (uint32_t d = 0; d < ND; ++d) fold(m[d]);
-                    if constexpr (EDGES) {
+                    if (TOPO == IMP3D && !(GP_ABLATE & ABL_NO_INLIST)) {
                         const uint32_t e_b = L.off[jl + o_off], e_e = L.off[jl + 1 + o_off];
                         if (staged) {
-                            // the node's used in-edges: its window of the tile bitmap, walked
-                            // set bit by set bit (ascending sender = canonical order)
-                            for (uint32_t q0 = e_b - e_lo; q0 < e_e - e_lo; q0 += 64u) {
-                                const uint32_t n = min(64u, e_e - e_lo - q0);
-                                const uint32_t w = q0 >> 6, sh = q0 & 63u;
-                                unsigned long long win = L.bits[w] >> sh;
-                                if (sh && w + 1 < (uint32_t)EW) win |= L.bits[w + 1] << (64u - sh);
-                                if (n < 64u) win &= (1ull << n) - 1ull;
-                                while (win) {
-                                    const uint32_t q = q0 + (uint32_t)__builtin_ctzll(win);
-                                    win &= win - 1ull;
-                                    const uint32_t slot = L.bpre[q >> 6] +
-                                                          (uint32_t)__popcll(L.bits[q >> 6] & ((1ull << (q & 63u)) - 1ull));
-                                    double2 mi;
-                                    if (slot < (uint32_t)MSG_CAP) {
-                                        mi = L.msg[slot];
-                                    } else {  // rare: more messages than the tile's slots
-                                        const uint32_t i = in_src[e_lo + q];
-                                        mi = (REMOTE && i - a.lo >= a.nloc) ? a.rmsg[e_lo + q] : ld_sw(swc + i);
+                            // k_ps_edges (or the pass above) stored the used in-edges' messages compactly in edge
+                            // order, so this node's messages are the slots [prefix(e_b),
+                            // prefix(e_e)), already in canonical (ascending sender) order
+                            auto prefix = [&](uint32_t q) {
+                                const uint32_t w = q >> 6;
+                                return L.bpre[w] + (uint32_t)__popcll(L.bits[w] & ((1ull << (q & 63u)) - 1ull));
+                            };
+                            const uint32_t s0 = prefix(e_b - e_lo), s1 = prefix(e_e - e_lo);
+                            for (uint32_t sl = s0; sl < s1; ++sl) {
+                                double2 mi;
+                                if (sl < (uint32_t)MSG_CAP) {
+                                    mi = L.msg[sl];
+                                } else {  // rare: more messages than the tile's slots -- find the edge
+                                    uint32_t q = e_b - e_lo, k2 = sl - s0;
+                                    for (;; ++q) {
+                                        if ((L.bits[q >> 6] >> (q & 63u)) & 1ull) {
+                                            if (k2 == 0) break;
+                                            --k2;
+                                        }
                                     }
-                                    fold(mi);
-                                    recv = true;
+                                    const uint32_t i = in_src[e_lo + q];
+                                    mi = (REMOTE && i - a.lo >= a.nloc) ? a.rmsg[e_lo + q] : ld_sw(swc + i);
                                 }
+                                fold(mi);
                             }
+                            recv = recv || s1 > s0;
                         } else {  // rare: tile in-degree above SRC_CAP (k_ps_edges skipped it)
                             for (uint32_t e = e_b; e < e_e; ++e) {
                                 const uint32_t i = in_src[e];
@@ -622,39 +655,6 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                                     fold(mi);
                                     recv = true;
                                 }
-                            }
-                        }
-                    } else if (TOPO == IMP3D && !(GP_ABLATE & ABL_NO_INLIST)) {
-                        const uint32_t e_b = L.off[jl + o_off], e_e = L.off[jl + 1 + o_off];
-                        for (uint32_t e = e_b; e < e_e; ++e) {
-                            bool sent = false;
-                            double2 mi = make_double2(0.0, 0.0);
-                            if (staged) {
-                                const uint16_t p = L.pos[e - e_lo];
-                                sent = p != POS_NONE;
-                                if (p < (uint16_t)MSG_CAP) mi = L.msg[p];
-                                else if (p == POS_GLOBAL) {
-                                    const uint32_t i = L.src[e - e_lo + o_src];
-                                    mi = (REMOTE && i - a.lo >= a.nloc) ? a.rmsg[e] : ld_sw(swc + i);
-                                }
-                            } else {  // rare: tile in-degree above SRC_CAP
-                                const uint32_t i = in_src[e];
-                                if (REMOTE && i - a.lo >= a.nloc) {
-                                    sent = a.rtag[e] == r;
-                                    if (sent) mi = a.rmsg[e];
-                                } else {
-                                    if (all_active) {
-                                        const uint32_t di = popc6(present_mask<IMP3D>(i, G)) + 1u;
-                                        sent = uniform(a.k0, a.k1, S_PUSHSUM, i, r, di) == di - 1u;
-                                    } else {
-                                        sent = (rbc[(i >> 6) - (a.lo >> 6)] >> (i & 63)) & 1ull;
-                                    }
-                                    if (sent) mi = ld_sw(swc + i);
-                                }
-                            }
-                            if (sent) {
-                                fold(mi);
-                                recv = true;
                             }
                         }
                     }

@@ -8,5 +8,5 @@ timeout -k 10 200 python -u tools/perf_round.py 1000000000 Imp3D push-sum 10 > g
 GP_KERNEL=tile timeout -k 10 200 python -u tools/perf_round.py 100000000 Imp3D gossip 20 >> gpurun_out/perf_iter.log 2>&1 || exit 1
 timeout -k 10 200 python -u tools/perf_round.py 1000000 3D push-sum 200 >> gpurun_out/perf_iter.log 2>&1 || exit 1
 cat gpurun_out/perf_iter.log
-GP_EDGES=0 timeout -k 10 200 python -u tools/perf_round.py 1000000000 Imp3D push-sum 10 >> gpurun_out/perf_iter.log 2>&1 || exit 1
+GP_EDGES=1 timeout -k 10 200 python -u tools/perf_round.py 1000000000 Imp3D push-sum 10 >> gpurun_out/perf_iter.log 2>&1 || exit 1
 tail -1 gpurun_out/perf_iter.log
