@@ -30,6 +30,19 @@ constexpr uint8_t B_ACTIVE = 8, B_CONV = 16;
 constexpr int CNT_SHIFT = 5;
 constexpr uint32_t GOSSIP_DONE = 11;  // rumours >= 11 stops sending (Program.fs:85)
 
+// a ^ b ^ k (k wave-uniform).  gfx950 has a three-input bitwise op with a
+// lookup table, v_bitop3_b32 (0x96 = a ^ b ^ c); the compiler does not form it
+// and emits two v_xor_b32 instead.
+GP_HD uint32_t xor3(uint32_t a, uint32_t b, uint32_t k) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+    return r;
+#else
+    return a ^ b ^ k;
+#endif
+}
+
 // ---------------------------------------------------------------- Philox4x32-10
 // Random123 Philox4x32 with 10 rounds; ctr = (node_lo, round, stream, node_hi),
 // key = (seed_lo, seed_hi).  Only output words 0 and 1 are consumed.
@@ -50,8 +63,8 @@ GP_HD void philox2(uint32_t node, uint32_t round, uint32_t stream, uint32_t k0, 
         }
         const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
         const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
-        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
-        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        const uint32_t n0 = xor3((uint32_t)(p1 >> 32), c1, k0);
+        const uint32_t n2 = xor3((uint32_t)(p0 >> 32), c3, k1);
         c1 = (uint32_t)p1;
         c3 = (uint32_t)p0;
         c0 = n0;

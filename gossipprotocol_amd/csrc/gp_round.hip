@@ -30,6 +30,9 @@ namespace gp {
 #ifndef GP_NPT
 #define GP_NPT 4
 #endif
+#ifndef GP_NT_LOADS
+#define GP_NT_LOADS 1
+#endif
 #ifndef GP_NT_STORES
 #define GP_NT_STORES 1
 #endif
@@ -151,15 +154,18 @@ typedef __attribute__((address_space(3))) void lvoid_t;
 // with LDS-DMA: no VGPR round trip and no wait inside the loop, so every
 // staging copy of a tile is in flight at once (retired by the next
 // __syncthreads, which waits vmcnt(0)).  One wave-instruction moves 1 KiB.
+template <int AUX = 0>
 __device__ __forceinline__ void dma_copy(void* lds, const char* g16, uint32_t nbytes) {
     const uint32_t lane = threadIdx.x & 63u;
     for (uint32_t c = (threadIdx.x >> 6) * 1024u; c < nbytes; c += TPB * 16u) {
         const uint32_t o = c + lane * 16u;
         if (o < nbytes)
             __builtin_amdgcn_global_load_lds((gvoid_t*)(g16 + o), (lvoid_t*)(reinterpret_cast<char*>(lds) + c), 16, 0,
-                                             0);
+                                             AUX);
     }
 }
+// cache-policy bits of a single-use (streamed once per round) staging copy: nt
+constexpr int DMA_ONCE = GP_NT_LOADS ? 2 : 0;
 
 // LDS-DMA version of stage_bytes: node bytes nb[lo, hi) clamped to [ext_lo,
 // ext_hi); returns the node id of LDS byte 0 (up to 15 bytes below lo).  Reads
@@ -180,7 +186,7 @@ __device__ __forceinline__ uint32_t dma_stage_bytes(uint32_t* lds, const uint8_t
 __device__ __forceinline__ uint32_t dma_stage_words(uint32_t* lds, const uint32_t* w, uint32_t lo, uint32_t hi) {
     const char* p = reinterpret_cast<const char*>(w + lo);
     const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 15u);
-    if (hi > lo) dma_copy(lds, p - mis, (hi - lo) * 4u + mis);
+    if (hi > lo) dma_copy<DMA_ONCE>(lds, p - mis, (hi - lo) * 4u + mis);
     return mis >> 2;
 }
 
@@ -271,6 +277,19 @@ struct TileWalk {
 };
 
 __device__ __forceinline__ double2 ld_sw(const double2* p) { return *p; }
+
+// Random-edge gathers touch one line per message and are never re-read this
+// round: load them non-temporally so they do not evict the lattice
+// neighbourhood the tiles share through the XCD's L2.
+typedef double gp_d2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ double2 ld_sw_once(const double2* p) {
+#if GP_NT_LOADS
+    const gp_d2v v = __builtin_nontemporal_load(reinterpret_cast<const gp_d2v*>(p));
+    return make_double2(v.x, v.y);
+#else
+    return *p;
+#endif
+}
 
 // Next-round state is written once and not read again this round: non-temporal
 // stores keep it from displacing the current round's (s, w) in the XCD's L2,
@@ -483,7 +502,7 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                     if (snt[m]) {
                         const uint32_t q = threadIdx.x + m * TPB;
                         v[m] = (GP_ABLATE & ABL_NO_RGATHER) ? make_double2((double)isrc[m], 1.0)
-                               : (REMOTE && isrc[m] - a.lo >= a.nloc) ? a.rmsg[e_lo + q] : ld_sw(swc + isrc[m]);
+                               : (REMOTE && isrc[m] - a.lo >= a.nloc) ? a.rmsg[e_lo + q] : ld_sw_once(swc + isrc[m]);
                     }
                 }
                 unsigned long long bal[FU];
