@@ -376,6 +376,11 @@ int build_imp3d(gp_sim* s) {
         if (ne)
             HIP_TRY(hipMemcpyAsync(S.in_src, src_sorted + edge0[r], sizeof(uint32_t) * ne, hipMemcpyDeviceToDevice,
                                    s->stream));
+        S.in_srcd = nullptr;
+        if (S.alg == PUSHSUM && S.kernel == KERNEL_TILE && s->P <= (1ll << 30) && s->g >= 2) {
+            if ((rc = dev_alloc_t(s, &S.in_srcd, (size_t)ne + 4))) return rc;
+            if (ne) HIP_TRY(launch_pack_src_deg(S.in_src, S.in_srcd, ne, S.G, s->grid, s->stream));
+        }
         if (W > 1) {
             if ((rc = dev_alloc_t(s, &sl.pos, S.nloc)) || (rc = dev_alloc_t(s, &S.rtag, ne)) ||
                 (S.alg == PUSHSUM && (rc = dev_alloc_t(s, &S.rmsg, ne))))

@@ -53,6 +53,7 @@ struct DevState {
     uint32_t* rnd;
     uint32_t* in_off;  // P+1
     uint32_t* in_src;  // P
+    uint32_t* in_srcd; // push-sum tile kernel: in_src with deg - 4 in bits 30-31 (P <= 2^30), else null
     // gossip injector
     uint32_t* live_bits;   // ceil(T / INJ_CHUNK) * 2048 words, bit = id still listed
     uint32_t* chunk_live;  // live ids per chunk
@@ -96,6 +97,7 @@ struct RoundArgs {
     uint64_t* rbn;
     const uint32_t* in_off;  // indexed by global id
     const uint32_t* in_src;
+    const uint32_t* in_srcd; // in_src with the sender's deg - 4 in bits 30-31, or null
     const uint32_t* rtag;    // per local in-edge: round of the delivered remote message
     const double2* rmsg;
     int32_t* c;              // indexed by global id
@@ -155,6 +157,8 @@ constexpr uint32_t EDGE_WORDS = 24, EDGE_MSGS = 384;
 uint32_t rbits_words_for(uint32_t lo, uint32_t nloc);
 hipError_t launch_round_tile(const DevState& S, uint32_t round, int grid, hipStream_t st);
 hipError_t launch_rbits_init(const DevState& S, int grid, hipStream_t st);
+hipError_t launch_pack_src_deg(const uint32_t* src, uint32_t* out, uint32_t n, const Geom& G, int grid,
+                               hipStream_t st);
 
 // ---- x-marching tiled push-sum kernel (gp_xtile.hip): 3D / Imp3D
 hipError_t launch_round_xtile(const RoundArgs& a, int topo, bool remote, uint32_t round, int grid, hipStream_t st);

@@ -374,6 +374,7 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
     double2* __restrict__ swn = a.swn;
     const uint64_t* __restrict__ rbc = a.rbc;
     const uint32_t* __restrict__ in_src = a.in_src;
+    const bool packed = a.in_srcd != nullptr;  // staged senders carry deg - 4 in bits 30-31
     const Geom G = a.G;
     const uint32_t H = TOPO == LINE ? 1u : G.g;
     uint32_t alerts = 0, newly = 0;
@@ -428,7 +429,7 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                              min(e_tot, (uint32_t)MSG_CAP) * 16u);
                 }
             } else {
-                if (staged) o_src = (int)dma_stage_words(L.src, in_src, e_lo, e_hi);
+                if (staged) o_src = (int)dma_stage_words(L.src, packed ? a.in_srcd : in_src, e_lo, e_hi);
             }
             // prefetch the next tile's in-edge range
             TileWalk nw = tw;
@@ -469,10 +470,13 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                 const uint32_t wv = threadIdx.x >> 6;
                 uint32_t isrc[FU];
                 bool snt[FU];
+                uint32_t ideg[FU];
 #pragma unroll
                 for (int m = 0; m < FU; ++m) {
                     const uint32_t q = threadIdx.x + m * TPB;
-                    isrc[m] = q < cnt ? L.src[q + o_src] : 0u;
+                    const uint32_t raw = q < cnt ? L.src[q + o_src] : 0u;
+                    isrc[m] = packed ? raw & 0x3FFFFFFFu : raw;
+                    ideg[m] = (raw >> 30) + 4u;
                 }
 #pragma unroll
                 for (int m = 0; m < FU; ++m) {
@@ -487,7 +491,7 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                         } else if ((GP_ABLATE & ABL_CHEAP_DECIDE) && all_active) {
                             sent = ((i * 2654435761u + r * 40503u) >> 29) == 0u;
                         } else if (all_active && !(GP_ABLATE & ABL_BITMAP_ONLY)) {
-                            const uint32_t di = popc6(present_mask<IMP3D>(i, G)) + 1u;
+                            const uint32_t di = packed ? ideg[m] : popc6(present_mask<IMP3D>(i, G)) + 1u;
                             sent = uniform(a.k0, a.k1, S_PUSHSUM, i, r, di) == di - 1u;
                         } else {
                             sent = (rbc[(i >> 6) - (a.lo >> 6)] >> (i & 63)) & 1ull;
@@ -1357,6 +1361,7 @@ RoundArgs make_round_args(const DevState& S, uint32_t round) {
     a.rbn = S.rbits[cur ^ 1];
     a.in_off = S.in_off ? S.in_off - S.lo : nullptr;
     a.in_src = S.in_src;
+    a.in_srcd = S.in_srcd;
     a.rtag = S.rtag;
     a.rmsg = S.rmsg;
     a.c = S.c ? S.c - S.lo : nullptr;
@@ -1428,6 +1433,24 @@ hipError_t launch_round_tile(const DevState& S, uint32_t round, int grid, hipStr
                 break;
         }
     }
+    return hipGetLastError();
+}
+
+// Imp3D push-sum senders with their degree packed in the top two bits
+// (deg - 4 in [0, 3]; every node has 3..6 lattice slots + the random one when
+// g >= 2), so the tile kernel's in-edge pass needs no division to find it.
+// Valid when every id fits 30 bits (P <= 2^30).
+__global__ __launch_bounds__(TPB) void k_pack_src_deg(const uint32_t* src, uint32_t* out, uint32_t n, Geom G) {
+    for (uint32_t e = blockIdx.x * TPB + threadIdx.x; e < n; e += gridDim.x * TPB) {
+        const uint32_t i = src[e];
+        const uint32_t deg = popc6(present_mask<IMP3D>(i, G)) + 1u;
+        out[e] = i | ((deg - 4u) << 30);
+    }
+}
+
+hipError_t launch_pack_src_deg(const uint32_t* src, uint32_t* out, uint32_t n, const Geom& G, int grid,
+                               hipStream_t st) {
+    hipLaunchKernelGGL(k_pack_src_deg, dim3(grid), dim3(TPB), 0, st, src, out, n, G);
     return hipGetLastError();
 }
 
