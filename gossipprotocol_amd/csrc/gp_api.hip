@@ -300,7 +300,8 @@ int alloc_slab(gp_sim* s, Slab& sl, int r) {
     // separate in-edge pass (k_ps_edges): opt-in, GP_EDGES=1 (measured slower than the
     // in-tile pass: 17.9 vs 16.2 ms/round at P = 1e9, profiles/r01)
     const char* ge = std::getenv("GP_EDGES");
-    if (S.topo == IMP3D && S.alg == PUSHSUM && S.kernel == KERNEL_TILE && ge && ge[0] == '1') {
+    if (S.topo == IMP3D && S.alg == PUSHSUM && S.kernel == KERNEL_TILE && ge && ge[0] == '1' &&
+        round_tiles(1024) == 1) {  // edge buffers are sized for 1024-node tiles
         // in-edge pass output (k_ps_edges): per tile EDGE_WORDS bitmap words, a count, EDGE_MSGS slots
         const size_t nt = (size_t)((S.lo + (uint64_t)S.nloc + 1023) / 1024 - S.lo / 1024);
         if ((rc = dev_alloc_t(s, &S.ebits, nt * EDGE_WORDS)) || (rc = dev_alloc_t(s, &S.etot, nt)) ||

@@ -27,6 +27,12 @@
 namespace gp {
 
 // Experiment knobs (tools/ablate.py); the product build uses the defaults.
+#ifndef GP_PREFETCH
+#define GP_PREFETCH 0
+#endif
+#ifndef GP_TPB
+#define GP_TPB 256
+#endif
 #ifndef GP_NPT
 #define GP_NPT 4
 #endif
@@ -57,18 +63,17 @@ namespace gp {
 #define ABL_NO_XGATHER 256    // lattice: no gather from the x-1 / x+1 planes
 #define ABL_NO_YGATHER 512    // lattice: no gather from the y-1 / y+1 rows
 #define ABL_NO_ZGATHER 1024   // lattice: no gather from z-1 / z+1 (k_ps_tile2 only)
-#define ABL_NO_FAST 2048      // k_ps_tile: always the per-term halving fold
 
 namespace {
 
-constexpr int TPB = BULK_THREADS;          // 256
+constexpr int TPB = GP_TPB;                // 256 (experiments: 128)
 constexpr int NPT = GP_NPT;                // nodes per thread per tile
 constexpr int TILE = TPB * NPT;            // 1024
 constexpr int HMAX = 1625;                 // largest lattice edge with g^3 < 2^32
 constexpr int W_ROWS = (TILE + 2 * HMAX) / 4 + 4;
 constexpr int W_PLANE = TILE / 4 + 4;
-constexpr int SRC_CAP = 1536;              // staged in-list entries per tile (mean 1024)
-constexpr int MSG_CAP = 384;               // random-edge messages parked per tile (mean ~146)
+constexpr int SRC_CAP = TILE * 3 / 2;       // staged in-list entries per tile (mean TILE)
+constexpr int MSG_CAP = TILE * 3 / 8;       // random-edge messages parked per tile (mean ~TILE / 7)
 constexpr uint16_t POS_NONE = 0xFFFF, POS_GLOBAL = 0xFFFE;
 
 // Staged ranges are moved by 16-byte LDS-DMA (global_load_lds_dwordx4) from a
@@ -105,7 +110,7 @@ struct TileLdsE {
     uint32_t red[2][TPB / 64];
 };
 
-static_assert(EW == (int)EDGE_WORDS && MSG_CAP == (int)EDGE_MSGS && TILE == 1024, "gp_internal.hpp sizes");
+static_assert(TILE != 1024 || (EW == (int)EDGE_WORDS && MSG_CAP == (int)EDGE_MSGS), "gp_internal.hpp sizes");
 
 // k_ps_tile<*, *, EDGES = false>: the tile decides its in-edges itself and
 // parks the used ones' messages compactly in edge order (same layout as
@@ -382,7 +387,7 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
 
     // the next tile's in-edge range is loaded one tile ahead (two uniform loads),
     // so the senders can be staged in the same phase as everything else
-    uint32_t pf_tile = 0xFFFFFFFFu, pf_lo = 0, pf_hi = 0, pf_tot = 0;
+    uint32_t pf_tile = 0xFFFFFFFFu, pf_lo = 0, pf_hi = 0, pf_tot = 0, pf_j0 = 0, pf_j1 = 0;
     for (TileWalk tw(a); tw.t < tw.end; tw.t += tw.step) {
         uint32_t ti;
         if (!tw.tile(ti)) continue;
@@ -441,6 +446,8 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                 pf_hi = a.in_off[min(a.lo + a.nloc, nT + TILE)];
                 if (EDGES) pf_tot = a.etot[nti];
                 pf_tile = nti;
+                pf_j0 = max(a.lo, nT);
+                pf_j1 = min(a.lo + a.nloc, nT + TILE);
             }
         }
         __syncthreads();
@@ -540,14 +547,20 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
             __syncthreads();
         }
 
-        // FAST (uniform): every node is active and no value can be subnormal, so the
-        // fold adds the senders' whole (s, w) and halves once at the end.  That is
-        // bit-identical to halving every term: x * 0.5 is exact and commutes with
-        // round-to-nearest for normal numbers, all values are >= 0, and a nonzero
-        // value is >= 2^-r after r rounds (>= 2^-1000 here, far from 2^-1022).
-        const bool fast = all_active && r < 1000u && G.P > 1u && !(GP_ABLATE & ABL_NO_FAST);
-        auto node_loop = [&](auto fast_tag) {
-            constexpr bool FAST = decltype(fast_tag)::value;
+        if constexpr (!EDGES) {
+            // warm the XCD's L2 with the next tile's (s, w) while this tile folds: LDS-DMA
+            // into a dead staging area (the senders are not read again this tile)
+            if (GP_PREFETCH && TOPO == IMP3D && pf_tile != 0xFFFFFFFFu && pf_j1 > pf_j0) {
+                const char* g = reinterpret_cast<const char*>(swc + pf_j0);
+                const uint32_t nbytes = (pf_j1 - pf_j0) * 16u;
+                char* sink = reinterpret_cast<char*>(L.src) + (threadIdx.x >> 6) * 1024u;
+                for (uint32_t c = (threadIdx.x >> 6) * 1024u; c < nbytes; c += TPB * 16u) {
+                    const uint32_t o = c + lane * 16u;
+                    if (o < nbytes) __builtin_amdgcn_global_load_lds((gvoid_t*)(g + o), (lvoid_t*)sink, 16, 0, 0);
+                }
+            }
+        }
+        {
             // lattice coordinates of this thread's first node, advanced by TPB per node
             uint32_t cx = 0, cy = 0, cz = 0;
             if (TOPO != LINE) {
@@ -584,22 +597,13 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                     bool active = (b & B_ACTIVE) != 0;
                     const double2 sv = own[k];
                     const bool halve = active && deg > 0;
-                    double acc_s, acc_w;
-                    if (FAST) {
-                        acc_s = sv.x;
-                        acc_w = sv.y;
-                    } else {
-                        acc_s = halve ? sv.x * 0.5 : sv.x;
-                        acc_w = halve ? sv.y * 0.5 : sv.y;
-                    }
+                    // canonical fold: own half, lattice slots in slot order, random edges by
+                    // ascending sender; every message contributes the sender's half
+                    double acc_s = halve ? sv.x * 0.5 : sv.x;
+                    double acc_w = halve ? sv.y * 0.5 : sv.y;
                     auto fold = [&](const double2 mi) {
-                        if (FAST) {
-                            acc_s = acc_s + mi.x;
-                            acc_w = acc_w + mi.y;
-                        } else {
-                            acc_s = acc_s + mi.x * 0.5;
-                            acc_w = acc_w + mi.y * 0.5;
-                        }
+                        acc_s = acc_s + mi.x * 0.5;
+                        acc_w = acc_w + mi.y * 0.5;
                     };
                     // lattice senders from the staged direction bytes (absent neighbours read
                     // a harmless in-range byte and are masked out)
@@ -681,10 +685,6 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                             }
                         }
                     }
-                    if (FAST) {  // every node is active (deg > 0): halve once
-                        acc_s = acc_s * 0.5;
-                        acc_w = acc_w * 0.5;
-                    }
                     uint32_t flags = b & (B_ACTIVE | B_CONV | (3u << CNT_SHIFT));
                     if (recv) {
                         if (!(GP_ABLATE & ABL_NO_RATIO) && !(b & B_CONV)) {
@@ -719,9 +719,7 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                     }
                 }
             }
-        };
-        if (fast) node_loop(std::true_type{});
-        else node_loop(std::false_type{});
+        }
         __syncthreads();
         // node bytes out as words (allocations are padded past P)
         for (uint32_t w = threadIdx.x; w < (uint32_t)(TILE / 4); w += TPB) {

@@ -18,11 +18,10 @@ OUT = os.path.join(ROOT, "build", "ablate")
 # name -> (GP_NPT, GP_ABLATE mask) for gp_round.hip (mask bits at the top of gp_round.hip)
 VARIANTS = {
     "base_npt4": (4, 0),
-    "no_rgather": (4, 1), "no_lgather": (4, 2), "no_inlist": (4, 4), "no_nextdir": (4, 8),
-    "no_ephilox": (4, 16), "no_gathers": (4, 1 | 2), "no_ratio": (4, 64),
+    "no_rgather": (4, 1), "no_inlist": (4, 4), "no_nextdir": (4, 8),
+    "no_ephilox": (4, 16), "no_ratio": (4, 64),
     "cheap_decide": (4, 128), "cheap_no_nextdir": (4, 128 | 8),
-    "no_xgather": (4, 256), "no_ygather": (4, 512), "no_zgather": (4, 1024),
-    "no_ephilox_nextdir": (4, 16 | 8), "all_off": (4, 16 | 2 | 8 | 64),
+    "prefetch": (4, 0, 5, 256, ["-DGP_PREFETCH=1"]), "minb6": (4, 0, 6), "tpb128": (4, 0, 10, 128), "tpb128_m8": (4, 0, 8, 128), "tpb128_n8": (8, 0, 10, 128),
 }
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off"]
 
@@ -34,8 +33,10 @@ def build():
     for name, v in VARIANTS.items():
         npt, mask = v[0], v[1]
         minb = v[2] if len(v) > 2 else 5
+        tpb = v[3] if len(v) > 3 else 256
+        extra = v[4] if len(v) > 4 else []
         obj = os.path.join(OUT, f"gp_round_{name}.o")
-        cmd = ["/opt/rocm/bin/hipcc", *FLAGS, f"-DGP_NPT={npt}", f"-DGP_ABLATE={mask}", f"-DGP_MINB={minb}",
+        cmd = ["/opt/rocm/bin/hipcc", *FLAGS, f"-DGP_NPT={npt}", f"-DGP_ABLATE={mask}", f"-DGP_MINB={minb}", f"-DGP_TPB={tpb}", *extra,
                "-c", "-o", obj, os.path.join(CSRC, "gp_round.hip")]
         procs.append(subprocess.Popen(cmd))
     for p in procs:
@@ -62,7 +63,6 @@ def run(n, only=None):
                 "s.sync(); s.kernel_stats(reset=True); s.step(10); s.sync()\n"
                 "ms,k,_=s.kernel_stats(); print(json.dumps(ms/k))\n") % (ROOT, n)
         env = dict(os.environ, GOSSIP_HIP_LIB_EXPERIMENT=so)
-        env.setdefault("GP_EDGES", "0")  # the ablation switches act on the single-kernel round
         if "@" in name:
             name, grid = name.split("@")
             so = os.path.join(OUT, f"lib_{name}.so")
