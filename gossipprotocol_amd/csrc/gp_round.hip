@@ -623,6 +623,7 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                                ((bzp & DIR_MASK) == 5u ? 16u : 0u) | ((bzm & DIR_MASK) == 4u ? 32u : 0u);
                         from &= mask;
                     }
+                    if (GP_ABLATE & ABL_NO_LGATHER) from = 0;
                     // one gather per direction, all in flight together; a direction without a
                     // sender reads the zero sentinel swc[ext_hi] (adding +0.0 is exact)
                     constexpr uint32_t ND = TOPO == LINE ? 2 : 6;

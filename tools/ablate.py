@@ -16,12 +16,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "gossipprotocol_amd", "csrc")
 OUT = os.path.join(ROOT, "build", "ablate")
 # name -> (GP_NPT, GP_ABLATE mask) for gp_round.hip (mask bits at the top of gp_round.hip)
-VARIANTS = {
+VARIANTS = {  # name -> (NPT, GP_ABLATE mask[, GP_MINB[, GP_TPB[, extra -D flags]]])
     "base_npt4": (4, 0),
-    "no_rgather": (4, 1), "no_inlist": (4, 4), "no_nextdir": (4, 8),
+    "no_rgather": (4, 1), "no_lgather": (4, 2), "no_inlist": (4, 4), "no_nextdir": (4, 8),
     "no_ephilox": (4, 16), "no_ratio": (4, 64),
     "cheap_decide": (4, 128), "cheap_no_nextdir": (4, 128 | 8),
-    "prefetch": (4, 0, 5, 256, ["-DGP_PREFETCH=1"]), "minb6": (4, 0, 6), "tpb128": (4, 0, 10, 128), "tpb128_m8": (4, 0, 8, 128), "tpb128_n8": (8, 0, 10, 128),
+    "minb6": (4, 0, 6), "tpb128": (4, 0, 10, 128),
+    "prefetch": (4, 0, 5, 256, ["-DGP_PREFETCH=1"]), "sc1st": (4, 0, 5, 256, ["-DGP_NT_STORES=2"]),
+    "plainst": (4, 0, 5, 256, ["-DGP_NT_STORES=0"]), "plainld": (4, 0, 5, 256, ["-DGP_NT_LOADS=0"]),
 }
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off"]
 
@@ -57,11 +59,11 @@ def run(n, only=None):
         so = os.path.join(OUT, f"lib_{name.split('@')[0]}.so")
         code = ("import sys,json; sys.path.insert(0,%r)\n"
                 "from gossipprotocol_amd import Simulation\n"
-                "s=Simulation(%d,'Imp3D','push-sum',kernel_timing=True)\n"
+                "s=Simulation(%d,%r,'push-sum',kernel_timing=True)\n"
                 "P=s.population\n"
                 "pre=0\nwhile s.info().active < P and pre < 300: pre += len(s.step(8))\n"
                 "s.sync(); s.kernel_stats(reset=True); s.step(10); s.sync()\n"
-                "ms,k,_=s.kernel_stats(); print(json.dumps(ms/k))\n") % (ROOT, n)
+                "ms,k,_=s.kernel_stats(); print(json.dumps(ms/k))\n") % (ROOT, n, os.environ.get("ABLATE_TOPO", "Imp3D"))
         env = dict(os.environ, GOSSIP_HIP_LIB_EXPERIMENT=so)
         if "@" in name:
             name, grid = name.split("@")
