@@ -378,7 +378,8 @@ int build_imp3d(gp_sim* s) {
             HIP_TRY(hipMemcpyAsync(S.in_src, src_sorted + edge0[r], sizeof(uint32_t) * ne, hipMemcpyDeviceToDevice,
                                    s->stream));
         S.in_srcd = nullptr;
-        if (S.alg == PUSHSUM && S.kernel == KERNEL_TILE && s->P <= (1ll << 30) && s->g >= 2) {
+        const char* np = std::getenv("GP_NO_PACK");  // tests: force the unpacked (P > 2^30) path
+        if (S.alg == PUSHSUM && S.kernel == KERNEL_TILE && s->P <= (1ll << 30) && s->g >= 2 && !(np && np[0] == '1')) {
             if ((rc = dev_alloc_t(s, &S.in_srcd, (size_t)ne + 4))) return rc;
             if (ne) HIP_TRY(launch_pack_src_deg(S.in_src, S.in_srcd, ne, S.G, s->grid, s->stream));
         }

@@ -190,3 +190,35 @@ def test_kernel_variant_parity(kernel, n, topo, alg, seed, rounds, chk, xsegs, m
         if len(ga) < k:
             break
     sim.close()
+
+
+WALK_CASES = [  # (num_nodes, topology, seed, rounds, checkpoint)
+    (512000, "Imp3D", 3, 90, 45),
+    (125000, "3D", 5, 120, 60),
+]
+
+
+@pytest.mark.parametrize("edges", ["0", "1"])
+@pytest.mark.parametrize("pack", ["0", "1"])
+@pytest.mark.parametrize("walk", ["0", "1", "2"])
+@pytest.mark.parametrize("n,topo,seed,rounds,chk", WALK_CASES, ids=lambda v: str(v))
+def test_tile_walk_and_sender_packing_parity(n, topo, seed, rounds, chk, walk, pack, edges, monkeypatch):
+    """Push-sum tile kernel bit-exact vs the oracle for every tile walk (XCD eighths,
+    global sweep, x-windows of 3 planes), with the senders' degree packed into the
+    staged ids or computed (the P > 2^30 path), and with the separate in-edge pass."""
+    if topo != "Imp3D" and (pack == "1" or edges == "1"):
+        pytest.skip("sender packing / edge pass are Imp3D only")
+    monkeypatch.setenv("GP_KERNEL", "tile")
+    monkeypatch.setenv("GP_WALK", walk)
+    monkeypatch.setenv("GP_WX", "3")
+    monkeypatch.setenv("GP_NO_PACK", "0" if pack == "1" else "1")
+    monkeypatch.setenv("GP_EDGES", edges)
+    sim, orc = Sim(n, topo, "push-sum", seed=seed), Oracle(n, topo, "push-sum", seed)
+    done = 0
+    while done < rounds:
+        k = min(chk, rounds - done)
+        ga, oa = sim.step(k), orc.step(k)
+        assert ga == oa, f"alerts differ in rounds {done}..{done + k}"
+        assert_same_state("push-sum", sim.state(), orc.state())
+        done += k
+    sim.close()
