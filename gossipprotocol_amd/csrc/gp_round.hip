@@ -115,16 +115,21 @@ static_assert(TILE != 1024 || (EW == (int)EDGE_WORDS && MSG_CAP == (int)EDGE_MSG
 // k_ps_tile<*, *, EDGES = false>: the tile decides its in-edges itself and
 // parks the used ones' messages compactly in edge order (same layout as
 // k_ps_edges' output).
+// The used in-edges' (s, w) are gathered by LDS-DMA straight into per-edge
+// slots (edge q's message at slot q -- lane-linear, so one global_load_lds per
+// edge batch, no registers, no compaction); edges past SLOTS (rare: a tile with
+// more than TILE + 64 in-edges) are gathered by the fold itself.
+constexpr int SLOTS = TILE + 64;
+
 struct TileLdsP {
     uint32_t rows[W_ROWS + DMA_SLACK];
     uint32_t xm[W_PLANE + DMA_SLACK];
     uint32_t xp[W_PLANE + DMA_SLACK];
     uint32_t off[TILE + 1 + DMA_SLACK];
-    uint32_t src[SRC_CAP + DMA_SLACK];  // in_src[in_off[j0] .. in_off[j1])
-    unsigned long long bits[EW + 1];
-    uint32_t bpre[EW + 1];
-    uint32_t wcnt[EW];
-    double2 msg[MSG_CAP];
+    uint32_t src[1];                  // unused: the senders go straight to registers
+    unsigned long long bits[EW + 1];  // bit q: in-edge q (tile order) was used by its sender; bits[EW] = 0
+    uint32_t bpre[1];                 // unused (EDGES layout)
+    double2 msg[SLOTS];               // edge q's message at slot q
     uint32_t out[TILE / 4];
     uint32_t red[2][TPB / 64];
 };
@@ -424,7 +429,9 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
         }
         const uint32_t cnt = e_hi - e_lo;
         const bool staged = cnt <= (uint32_t)SRC_CAP;
-        int o_off = 0, o_src = 0;  // L.off[jl + o_off] = in_off[T + jl]; L.src[q + o_src] = in_src[e_lo + q]
+        int o_off = 0;  // L.off[jl + o_off] = in_off[T + jl]
+        constexpr int FU = SRC_CAP / TPB;
+        uint32_t rawsrc[FU];  // staged senders (Imp3D, !EDGES)
         if (TOPO == IMP3D) {
             o_off = (int)dma_stage_words(L.off, a.in_off, j0, j1 + 1) - (int)(j0 - T);
             if constexpr (EDGES) {
@@ -433,8 +440,13 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                     dma_copy(L.msg, reinterpret_cast<const char*>(a.emsg + (size_t)ti * MSG_CAP),
                              min(e_tot, (uint32_t)MSG_CAP) * 16u);
                 }
-            } else {
-                if (staged) o_src = (int)dma_stage_words(L.src, packed ? a.in_srcd : in_src, e_lo, e_hi);
+            } else if (staged) {  // the senders straight to registers, consumed after the barrier
+                const uint32_t* srcp = packed ? a.in_srcd : in_src;
+#pragma unroll
+                for (int m = 0; m < FU; ++m) {
+                    const uint32_t q = threadIdx.x + m * TPB;
+                    rawsrc[m] = q < cnt ? srcp[e_lo + q] : 0u;
+                }
             }
             // prefetch the next tile's in-edge range
             TileWalk nw = tw;
@@ -468,22 +480,16 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
             if (staged) {
                 // Flattened, lane-balanced pass over the tile's in-edges: decide
                 // whether each sender used its random edge (all FU Philox chains of a
-                // thread independent), issue all gathers of the used edges' (s, w),
-                // and park them compactly in edge order: bit q of the tile bitmap
-                // marks edge q used, its message sits at slot prefix(q).  A node's
-                // messages are then one contiguous, canonically ordered slot range.
-                // Edge q = m * TPB + wave * 64 + lane lives in bitmap word m * 4 + wave.
-                constexpr int FU = SRC_CAP / TPB;
+                // thread independent), record the answers as a bitmap (edge
+                // q = m * TPB + wave * 64 + lane is bit lane of word m * 4 + wave), and
+                // gather the used edges' (s, w) by LDS-DMA into slot q (non-temporal:
+                // one line per message, never re-read).  The next barrier retires them.
                 const uint32_t wv = threadIdx.x >> 6;
-                uint32_t isrc[FU];
-                bool snt[FU];
-                uint32_t ideg[FU];
+                uint32_t isrc[FU], ideg[FU];
 #pragma unroll
                 for (int m = 0; m < FU; ++m) {
-                    const uint32_t q = threadIdx.x + m * TPB;
-                    const uint32_t raw = q < cnt ? L.src[q + o_src] : 0u;
-                    isrc[m] = packed ? raw & 0x3FFFFFFFu : raw;
-                    ideg[m] = (raw >> 30) + 4u;
+                    isrc[m] = packed ? rawsrc[m] & 0x3FFFFFFFu : rawsrc[m];
+                    ideg[m] = (rawsrc[m] >> 30) + 4u;
                 }
 #pragma unroll
                 for (int m = 0; m < FU; ++m) {
@@ -504,45 +510,15 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                             sent = (rbc[(i >> 6) - (a.lo >> 6)] >> (i & 63)) & 1ull;
                         }
                     }
-                    snt[m] = sent;
-                }
-                double2 v[FU];
-#pragma unroll
-                for (int m = 0; m < FU; ++m) {
-                    v[m] = make_double2(0.0, 0.0);
-                    if (snt[m]) {
-                        const uint32_t q = threadIdx.x + m * TPB;
-                        v[m] = (GP_ABLATE & ABL_NO_RGATHER) ? make_double2((double)isrc[m], 1.0)
-                               : (REMOTE && isrc[m] - a.lo >= a.nloc) ? a.rmsg[e_lo + q] : ld_sw_once(swc + isrc[m]);
+                    const unsigned long long bal = __ballot(sent);
+                    if (lane == 0) L.bits[m * (TPB / 64) + wv] = bal;
+                    if (sent && q < (uint32_t)SLOTS && !(GP_ABLATE & ABL_NO_RGATHER)) {
+                        const double2* src = (REMOTE && i - a.lo >= a.nloc) ? a.rmsg + e_lo + q : swc + i;
+                        __builtin_amdgcn_global_load_lds((gvoid_t*)src,
+                                                         (lvoid_t*)(L.msg + (m * TPB + wv * 64)), 16, 0, DMA_ONCE);
                     }
                 }
-                unsigned long long bal[FU];
-#pragma unroll
-                for (int m = 0; m < FU; ++m) {
-                    bal[m] = __ballot(snt[m]);
-                    if (lane == 0) {
-                        L.bits[m * (TPB / 64) + wv] = bal[m];
-                        L.wcnt[m * (TPB / 64) + wv] = (uint32_t)__popcll(bal[m]);
-                    }
-                }
-                __syncthreads();
-                const uint32_t c = lane < EW ? L.wcnt[lane] : 0u;
-                uint32_t incl = c;
-#pragma unroll
-                for (int o = 1; o < 32; o <<= 1) {
-                    const uint32_t t = __shfl_up(incl, o, 64);
-                    if (lane >= o) incl += t;
-                }
-                const uint32_t excl = incl - c;
-                if (threadIdx.x <= (uint32_t)EW) L.bpre[threadIdx.x] = excl;
-                if (threadIdx.x == (uint32_t)EW) L.bits[EW] = 0ull;
-#pragma unroll
-                for (int m = 0; m < FU; ++m) {
-                    const uint32_t slot = __shfl(excl, m * (TPB / 64) + wv, 64) +
-                                          __builtin_amdgcn_mbcnt_hi((uint32_t)(bal[m] >> 32),
-                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)bal[m], 0u));
-                    if (snt[m] && slot < (uint32_t)MSG_CAP) L.msg[slot] = v[m];
-                }
+                if (threadIdx.x == 0) L.bits[EW] = 0ull;
             }
             __syncthreads();
         }
@@ -635,8 +611,33 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                     for (uint32_t d = 0; d < ND; ++d) fold(m[d]);
                     if (TOPO == IMP3D && !(GP_ABLATE & ABL_NO_INLIST)) {
                         const uint32_t e_b = L.off[jl + o_off], e_e = L.off[jl + 1 + o_off];
-                        if (staged) {
-                            // k_ps_edges (or the pass above) stored the used in-edges' messages compactly in edge
+                        if (staged && !EDGES) {
+                            // the node's used in-edges: its window of the tile bitmap, walked set
+                            // bit by set bit (ascending sender = canonical order); message at slot q
+                            for (uint32_t q0 = e_b - e_lo; q0 < e_e - e_lo; q0 += 64u) {
+                                const uint32_t n = min(64u, e_e - e_lo - q0);
+                                const uint32_t w = q0 >> 6, sh = q0 & 63u;
+                                unsigned long long win = L.bits[w] >> sh;
+                                if (sh) win |= L.bits[w + 1] << (64u - sh);
+                                if (n < 64u) win &= (1ull << n) - 1ull;
+                                while (win) {
+                                    const uint32_t q = q0 + (uint32_t)__builtin_ctzll(win);
+                                    win &= win - 1ull;
+                                    double2 mi;
+                                    if (GP_ABLATE & ABL_NO_RGATHER) {
+                                        mi = make_double2(1.0, 1.0);
+                                    } else if (q < (uint32_t)SLOTS) {
+                                        mi = L.msg[q];
+                                    } else {  // rare: edge past the tile's slots
+                                        const uint32_t i = in_src[e_lo + q];
+                                        mi = (REMOTE && i - a.lo >= a.nloc) ? a.rmsg[e_lo + q] : ld_sw(swc + i);
+                                    }
+                                    fold(mi);
+                                    recv = true;
+                                }
+                            }
+                        } else if (staged) {
+                            // k_ps_edges stored the used in-edges' messages compactly in edge
                             // order, so this node's messages are the slots [prefix(e_b),
                             // prefix(e_e)), already in canonical (ascending sender) order
                             auto prefix = [&](uint32_t q) {
