@@ -475,20 +475,23 @@ __global__ __launch_bounds__(BULK_THREADS) void k_gossip_col(WaveArgs a, uint32_
 }
 
 // Random-edge bits of round 0 in the column layout (only the seed can be sending).
+// Every word is written exactly once (the seed's word with its bit), so no
+// store can race the seed's bit away.
 __global__ __launch_bounds__(BULK_THREADS) void k_col_rbits_init(WaveArgs a, const uint8_t* nb0, uint32_t words) {
-    for (uint32_t w = blockIdx.x * BULK_THREADS + threadIdx.x; w < words; w += gridDim.x * BULK_THREADS)
-        a.rbn[w] = 0ull;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        const uint32_t i = a.seed_node;
-        if (i - a.lo < a.nloc && (nb0[i - a.base] & DIR_MASK) == DIR_RANDOM) {
-            const Geom& G = a.G;
-            const uint32_t x = fastdiv(i, G.div_g2);
-            const uint32_t rem = i - x * G.g2;
-            const uint32_t y = fastdiv(rem, G.div_g);
-            const uint32_t z = rem - y * G.g;
-            a.rbn[col_rb_word(a, x, y, z)] = 1ull << (z & 63);
-        }
+    const uint32_t i = a.seed_node;
+    uint32_t sw = 0xFFFFFFFFu;
+    unsigned long long sbit = 0ull;
+    if (i - a.lo < a.nloc && (nb0[i - a.base] & DIR_MASK) == DIR_RANDOM) {
+        const Geom& G = a.G;
+        const uint32_t x = fastdiv(i, G.div_g2);
+        const uint32_t rem = i - x * G.g2;
+        const uint32_t y = fastdiv(rem, G.div_g);
+        const uint32_t z = rem - y * G.g;
+        sw = col_rb_word(a, x, y, z);
+        sbit = 1ull << (z & 63);
     }
+    for (uint32_t w = blockIdx.x * BULK_THREADS + threadIdx.x; w < words; w += gridDim.x * BULK_THREADS)
+        a.rbn[w] = w == sw ? sbit : 0ull;
 }
 
 uint32_t col_rbits_words(uint32_t planes, uint32_t g) { return planes * g * ((g + 63) / 64) + 16u; }

@@ -222,3 +222,18 @@ def test_tile_walk_and_sender_packing_parity(n, topo, seed, rounds, chk, walk, p
         assert_same_state("push-sum", sim.state(), orc.state())
         done += k
     sim.close()
+
+
+@pytest.mark.parametrize("kernel", ["col", "tile", "wave"])
+def test_seed_random_edge_round0(kernel, monkeypatch):
+    """Many seeds, so that several seed nodes send their round-0 rumour on the random
+    edge: the round-0 random-edge bitmap (k_col_rbits_init / k_rbits_init) must carry
+    that send.  Regression: k_col_rbits_init once raced its own zeroing loop against
+    the seed's bit (lost about one time in four)."""
+    monkeypatch.setenv("GP_KERNEL", kernel)
+    for seed in range(1, 25):
+        sim, orc = Sim(27000, "Imp3D", "gossip", seed=seed), Oracle(27000, "Imp3D", "gossip", seed)
+        assert sim.step(12) == orc.step(12), f"seed {seed}: alerts differ"
+        assert np.array_equal(sim.state()["c"], orc.state()["c"]), f"seed {seed}: counters differ"
+        sim.close()
+        orc.close()
