@@ -63,6 +63,8 @@ namespace gp {
 #define ABL_NO_XGATHER 256    // lattice: no gather from the x-1 / x+1 planes
 #define ABL_NO_YGATHER 512    // lattice: no gather from the y-1 / y+1 rows
 #define ABL_NO_ZGATHER 1024   // lattice: no gather from z-1 / z+1 (k_ps_tile2 only)
+#define ABL_NO_RFOLD 2048     // in-list: decide and gather, but the nodes do not walk their bitmap window
+#define ABL_FAKE_SRC 4096     // in-list: senders hashed from the edge index instead of loaded
 
 namespace {
 
@@ -117,9 +119,13 @@ static_assert(TILE != 1024 || (EW == (int)EDGE_WORDS && MSG_CAP == (int)EDGE_MSG
 // k_ps_edges' output).
 // The used in-edges' (s, w) are gathered by LDS-DMA straight into per-edge
 // slots (edge q's message at slot q -- lane-linear, so one global_load_lds per
-// edge batch, no registers, no compaction); edges past SLOTS (rare: a tile with
-// more than TILE + 64 in-edges) are gathered by the fold itself.
-constexpr int SLOTS = TILE + 64;
+// edge batch, no registers, no compaction).  A tile with more than SLOTS
+// in-edges (6 sigma above the mean TILE: ~1e-9 of tiles) takes the unstaged path,
+// so the node fold reads LDS only (no global fallback inside its loop, whose
+// join would cost a vmcnt(0) wait per message).
+constexpr int SLOTS = TILE + TILE / 8 + TILE / 16;  // 1216 at TILE = 1024: the LDS of 5 blocks per CU
+constexpr int SLOT_FU = (SLOTS + TPB - 1) / TPB;  // in-edges per thread in the in-edge pass
+constexpr int SLOT_W = (SLOTS + 63) / 64;         // bitmap words
 
 struct TileLdsP {
     uint32_t rows[W_ROWS + DMA_SLACK];
@@ -127,8 +133,8 @@ struct TileLdsP {
     uint32_t xp[W_PLANE + DMA_SLACK];
     uint32_t off[TILE + 1 + DMA_SLACK];
     uint32_t src[1];                  // unused: the senders go straight to registers
-    unsigned long long bits[EW + 1];  // bit q: in-edge q (tile order) was used by its sender; bits[EW] = 0
-    uint32_t bpre[1];                 // unused (EDGES layout)
+    unsigned long long bits[SLOT_FU * (TPB / 64) + 1];  // bit q: in-edge q (tile order) was used by its sender; then 0
+    uint32_t bpre[1];                                    // unused (EDGES layout)
     double2 msg[SLOTS];               // edge q's message at slot q
     uint32_t out[TILE / 4];
     uint32_t red[2][TPB / 64];
@@ -428,9 +434,9 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
             b_xp = dma_stage_bytes(L.xp, a.nbc, (int64_t)j0 + G.g2, (int64_t)j1 + G.g2, a.ext_lo, a.ext_hi);
         }
         const uint32_t cnt = e_hi - e_lo;
-        const bool staged = cnt <= (uint32_t)SRC_CAP;
+        const bool staged = cnt <= (uint32_t)(EDGES ? SRC_CAP : SLOTS);
         int o_off = 0;  // L.off[jl + o_off] = in_off[T + jl]
-        constexpr int FU = SRC_CAP / TPB;
+        constexpr int FU = SLOT_FU;
         uint32_t rawsrc[FU];  // staged senders (Imp3D, !EDGES)
         if (TOPO == IMP3D) {
             o_off = (int)dma_stage_words(L.off, a.in_off, j0, j1 + 1) - (int)(j0 - T);
@@ -445,7 +451,9 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
 #pragma unroll
                 for (int m = 0; m < FU; ++m) {
                     const uint32_t q = threadIdx.x + m * TPB;
-                    rawsrc[m] = q < cnt ? srcp[e_lo + q] : 0u;
+                    rawsrc[m] = q < cnt ? ((GP_ABLATE & ABL_FAKE_SRC) ? ((e_lo + q) * 2654435761u) % a.G.P | 0xC0000000u
+                                                                      : srcp[e_lo + q])
+                                        : 0u;
                 }
             }
             // prefetch the next tile's in-edge range
@@ -512,13 +520,13 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                     }
                     const unsigned long long bal = __ballot(sent);
                     if (lane == 0) L.bits[m * (TPB / 64) + wv] = bal;
-                    if (sent && q < (uint32_t)SLOTS && !(GP_ABLATE & ABL_NO_RGATHER)) {
+                    if (sent && !(GP_ABLATE & ABL_NO_RGATHER)) {
                         const double2* src = (REMOTE && i - a.lo >= a.nloc) ? a.rmsg + e_lo + q : swc + i;
                         __builtin_amdgcn_global_load_lds((gvoid_t*)src,
                                                          (lvoid_t*)(L.msg + (m * TPB + wv * 64)), 16, 0, DMA_ONCE);
                     }
                 }
-                if (threadIdx.x == 0) L.bits[EW] = 0ull;
+                if (threadIdx.x == 0) L.bits[FU * (TPB / 64)] = 0ull;
             }
             __syncthreads();
         }
@@ -611,28 +619,21 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                     for (uint32_t d = 0; d < ND; ++d) fold(m[d]);
                     if (TOPO == IMP3D && !(GP_ABLATE & ABL_NO_INLIST)) {
                         const uint32_t e_b = L.off[jl + o_off], e_e = L.off[jl + 1 + o_off];
-                        if (staged && !EDGES) {
-                            // the node's used in-edges: its window of the tile bitmap, walked set
-                            // bit by set bit (ascending sender = canonical order); message at slot q
-                            for (uint32_t q0 = e_b - e_lo; q0 < e_e - e_lo; q0 += 64u) {
-                                const uint32_t n = min(64u, e_e - e_lo - q0);
-                                const uint32_t w = q0 >> 6, sh = q0 & 63u;
-                                unsigned long long win = L.bits[w] >> sh;
-                                if (sh) win |= L.bits[w + 1] << (64u - sh);
-                                if (n < 64u) win &= (1ull << n) - 1ull;
+                        if (GP_ABLATE & ABL_NO_RFOLD) {
+                            recv = recv || L.bits[(e_b - e_lo) >> 6] != 0ull;
+                        } else if (staged && !EDGES) {
+                            // the node's used in-edges: its window of the tile bitmap, 32 bits at a
+                            // time (funnel shift of two LDS words), walked set bit by set bit
+                            // (ascending sender = canonical order); edge q's message is at slot q
+                            const uint32_t* bw = reinterpret_cast<const uint32_t*>(L.bits);
+                            const uint32_t qe = e_e - e_lo;
+                            for (uint32_t q0 = e_b - e_lo; q0 < qe; q0 += 32u) {
+                                uint32_t win = __builtin_amdgcn_alignbit(bw[(q0 >> 5) + 1], bw[q0 >> 5], q0 & 31u);
+                                if (qe - q0 < 32u) win &= (1u << (qe - q0)) - 1u;
                                 while (win) {
-                                    const uint32_t q = q0 + (uint32_t)__builtin_ctzll(win);
-                                    win &= win - 1ull;
-                                    double2 mi;
-                                    if (GP_ABLATE & ABL_NO_RGATHER) {
-                                        mi = make_double2(1.0, 1.0);
-                                    } else if (q < (uint32_t)SLOTS) {
-                                        mi = L.msg[q];
-                                    } else {  // rare: edge past the tile's slots
-                                        const uint32_t i = in_src[e_lo + q];
-                                        mi = (REMOTE && i - a.lo >= a.nloc) ? a.rmsg[e_lo + q] : ld_sw(swc + i);
-                                    }
-                                    fold(mi);
+                                    const uint32_t q = q0 + (uint32_t)__builtin_ctz(win);
+                                    win &= win - 1u;
+                                    fold((GP_ABLATE & ABL_NO_RGATHER) ? make_double2(1.0, 1.0) : L.msg[q]);
                                     recv = true;
                                 }
                             }
@@ -663,7 +664,7 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                                 fold(mi);
                             }
                             recv = recv || s1 > s0;
-                        } else {  // rare: tile in-degree above SRC_CAP (k_ps_edges skipped it)
+                        } else {  // rare: tile in-degree above SLOTS (SRC_CAP for k_ps_edges, which skipped it)
                             for (uint32_t e = e_b; e < e_e; ++e) {
                                 const uint32_t i = in_src[e];
                                 bool sent;

@@ -19,7 +19,9 @@ OUT = os.path.join(ROOT, "build", "ablate")
 VARIANTS = {  # name -> (NPT, GP_ABLATE mask[, GP_MINB[, GP_TPB[, extra -D flags]]])
     "base_npt4": (4, 0),
     "no_rgather": (4, 1), "no_lgather": (4, 2), "no_inlist": (4, 4), "no_nextdir": (4, 8),
-    "no_ephilox": (4, 16), "no_ratio": (4, 64),
+    "no_ephilox": (4, 16), "no_ratio": (4, 64), "no_gathers": (4, 1 | 2),
+    "no_xgather": (4, 256), "no_ygather": (4, 512), "no_rfold": (4, 2048), "fake_src": (4, 4096),
+    "no_rfold_rgather": (4, 2048 | 1),
     "cheap_decide": (4, 128), "cheap_no_nextdir": (4, 128 | 8),
     "minb6": (4, 0, 6), "tpb128": (4, 0, 10, 128),
     "prefetch": (4, 0, 5, 256, ["-DGP_PREFETCH=1"]), "sc1st": (4, 0, 5, 256, ["-DGP_NT_STORES=2"]),
