@@ -875,6 +875,8 @@ int build_sim(gp_sim* s) {
         sl.S.col_xsegs = col_xsegs;
         sl.S.tile_walk = walk;
         sl.S.tile_wx = wx;
+        sl.S.tile_stage_cap = 0xFFFFFFFFu;
+        if (const char* e = std::getenv("GP_STAGE_CAP")) sl.S.tile_stage_cap = (uint32_t)std::max(0, std::atoi(e));
         if ((rc = alloc_slab(s, sl, sl.rank))) return rc;
     }
     if (s->cfg.topology == GP_IMP3D && (rc = build_imp3d(s))) return rc;

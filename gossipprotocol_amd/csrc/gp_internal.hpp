@@ -80,6 +80,7 @@ struct DevState {
     uint32_t col_xsegs;
     uint32_t tile_walk;  // RoundArgs::walk
     uint32_t tile_wx;    // RoundArgs::wx
+    uint32_t tile_stage_cap;  // RoundArgs::stage_cap (GP_STAGE_CAP, tests only; default: no limit)
     // Imp3D push-sum, tile kernel: output of the in-edge pass (k_ps_edges) per
     // tile -- bitmap of used in-edges, message count, compact messages
     unsigned long long* ebits;
@@ -111,6 +112,7 @@ struct RoundArgs {
     uint32_t* etot;
     double2* emsg;
     uint32_t xs_len;  // k_ps_xtile: planes per x-segment
+    uint32_t stage_cap;  // k_ps_tile: tiles with more in-edges take the unstaged path (tests force it)
 };
 
 enum KernelVariant : int { KERNEL_WAVE = 0, KERNEL_TILE = 1, KERNEL_COL = 2, KERNEL_TILE2 = 3, KERNEL_XTILE = 4 };

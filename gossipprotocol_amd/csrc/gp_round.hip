@@ -419,44 +419,10 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                 if (EDGES) e_tot = a.etot[ti];
             }
         }
-        // own (s, w): issue first, consumed after staging
-        double2 own[NPT];
-#pragma unroll
-        for (int k = 0; k < NPT; ++k) {
-            const uint32_t j = T + k * TPB + threadIdx.x;
-            own[k] = (j >= j0 && j < j1) ? swc[j] : make_double2(0.0, 1.0);
-        }
-        // every staging copy of the tile in flight at once (LDS-DMA)
-        const uint32_t b_rows = dma_stage_bytes(L.rows, a.nbc, (int64_t)j0 - H, (int64_t)j1 + H, a.ext_lo, a.ext_hi);
-        uint32_t b_xm = 0, b_xp = 0;
-        if (TOPO != LINE) {
-            b_xm = dma_stage_bytes(L.xm, a.nbc, (int64_t)j0 - G.g2, (int64_t)j1 - G.g2, a.ext_lo, a.ext_hi);
-            b_xp = dma_stage_bytes(L.xp, a.nbc, (int64_t)j0 + G.g2, (int64_t)j1 + G.g2, a.ext_lo, a.ext_hi);
-        }
         const uint32_t cnt = e_hi - e_lo;
-        const bool staged = cnt <= (uint32_t)(EDGES ? SRC_CAP : SLOTS);
-        int o_off = 0;  // L.off[jl + o_off] = in_off[T + jl]
+        const bool staged = cnt <= min((uint32_t)(EDGES ? SRC_CAP : SLOTS), a.stage_cap);
         constexpr int FU = SLOT_FU;
-        uint32_t rawsrc[FU];  // staged senders (Imp3D, !EDGES)
-        if (TOPO == IMP3D) {
-            o_off = (int)dma_stage_words(L.off, a.in_off, j0, j1 + 1) - (int)(j0 - T);
-            if constexpr (EDGES) {
-                if (staged) {
-                    dma_copy(L.bits, reinterpret_cast<const char*>(a.ebits + (size_t)ti * EW), EW * 8u);
-                    dma_copy(L.msg, reinterpret_cast<const char*>(a.emsg + (size_t)ti * MSG_CAP),
-                             min(e_tot, (uint32_t)MSG_CAP) * 16u);
-                }
-            } else if (staged) {  // the senders straight to registers, consumed after the barrier
-                const uint32_t* srcp = packed ? a.in_srcd : in_src;
-#pragma unroll
-                for (int m = 0; m < FU; ++m) {
-                    const uint32_t q = threadIdx.x + m * TPB;
-                    rawsrc[m] = q < cnt ? ((GP_ABLATE & ABL_FAKE_SRC) ? ((e_lo + q) * 2654435761u) % a.G.P | 0xC0000000u
-                                                                      : srcp[e_lo + q])
-                                        : 0u;
-                }
-            }
-            // prefetch the next tile's in-edge range
+        if (TOPO == IMP3D) {  // prefetch the next tile's in-edge range
             TileWalk nw = tw;
             nw.t += nw.step;
             uint32_t nti;
@@ -470,34 +436,28 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                 pf_j1 = min(a.lo + a.nloc, nT + TILE);
             }
         }
-        __syncthreads();
-        if constexpr (EDGES) {
-            if (staged && threadIdx.x < 64) {  // sent edges before each bitmap word
-                const uint32_t c = threadIdx.x < (uint32_t)EW ? (uint32_t)__popcll(L.bits[threadIdx.x]) : 0u;
-                uint32_t incl = c;
-#pragma unroll
-                for (int o = 1; o < 32; o <<= 1) {
-                    const uint32_t t = __shfl_up(incl, o, 64);
-                    if (lane >= o) incl += t;
-                }
-                if (threadIdx.x <= (uint32_t)EW) L.bpre[threadIdx.x] = incl - c;
-                if (threadIdx.x == (uint32_t)EW) L.bits[EW] = 0ull;
-            }
-            __syncthreads();
-        } else if (TOPO == IMP3D) {
+        if constexpr (TOPO == IMP3D && !EDGES) {
             if (staged) {
-                // Flattened, lane-balanced pass over the tile's in-edges: decide
-                // whether each sender used its random edge (all FU Philox chains of a
-                // thread independent), record the answers as a bitmap (edge
+                // In-edge pass, ahead of the staging copies (its Philox chains wait for
+                // the senders only, and its gathers retire at the staging barrier):
+                // flattened, lane-balanced over the tile's in-edges, decide whether each
+                // sender used its random edge (all FU Philox chains of a thread
+                // independent), record the answers as a bitmap (edge
                 // q = m * TPB + wave * 64 + lane is bit lane of word m * 4 + wave), and
                 // gather the used edges' (s, w) by LDS-DMA into slot q (non-temporal:
-                // one line per message, never re-read).  The next barrier retires them.
+                // one line per message, never re-read).  The previous tile's node phase
+                // ended at a barrier and its byte output reads L.out only.
                 const uint32_t wv = threadIdx.x >> 6;
+                const uint32_t* srcp = packed ? a.in_srcd : in_src;
                 uint32_t isrc[FU], ideg[FU];
 #pragma unroll
                 for (int m = 0; m < FU; ++m) {
-                    isrc[m] = packed ? rawsrc[m] & 0x3FFFFFFFu : rawsrc[m];
-                    ideg[m] = (rawsrc[m] >> 30) + 4u;
+                    const uint32_t q = threadIdx.x + m * TPB;
+                    const uint32_t raw = q < cnt ? ((GP_ABLATE & ABL_FAKE_SRC) ? ((e_lo + q) * 2654435761u) % a.G.P | 0xC0000000u
+                                                                               : srcp[e_lo + q])
+                                                 : 0u;
+                    isrc[m] = packed ? raw & 0x3FFFFFFFu : raw;
+                    ideg[m] = (raw >> 30) + 4u;
                 }
 #pragma unroll
                 for (int m = 0; m < FU; ++m) {
@@ -527,6 +487,45 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                     }
                 }
                 if (threadIdx.x == 0) L.bits[FU * (TPB / 64)] = 0ull;
+            }
+        }
+        // own (s, w): consumed after staging
+        double2 own[NPT];
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            const uint32_t j = T + k * TPB + threadIdx.x;
+            own[k] = (j >= j0 && j < j1) ? swc[j] : make_double2(0.0, 1.0);
+        }
+        // every staging copy of the tile in flight at once (LDS-DMA)
+        const uint32_t b_rows = dma_stage_bytes(L.rows, a.nbc, (int64_t)j0 - H, (int64_t)j1 + H, a.ext_lo, a.ext_hi);
+        uint32_t b_xm = 0, b_xp = 0;
+        if (TOPO != LINE) {
+            b_xm = dma_stage_bytes(L.xm, a.nbc, (int64_t)j0 - G.g2, (int64_t)j1 - G.g2, a.ext_lo, a.ext_hi);
+            b_xp = dma_stage_bytes(L.xp, a.nbc, (int64_t)j0 + G.g2, (int64_t)j1 + G.g2, a.ext_lo, a.ext_hi);
+        }
+        int o_off = 0;  // L.off[jl + o_off] = in_off[T + jl]
+        if (TOPO == IMP3D) {
+            o_off = (int)dma_stage_words(L.off, a.in_off, j0, j1 + 1) - (int)(j0 - T);
+            if constexpr (EDGES) {
+                if (staged) {
+                    dma_copy(L.bits, reinterpret_cast<const char*>(a.ebits + (size_t)ti * EW), EW * 8u);
+                    dma_copy(L.msg, reinterpret_cast<const char*>(a.emsg + (size_t)ti * MSG_CAP),
+                             min(e_tot, (uint32_t)MSG_CAP) * 16u);
+                }
+            }
+        }
+        __syncthreads();  // staging copies, in-edge bitmap and gathered messages retired
+        if constexpr (EDGES) {
+            if (staged && threadIdx.x < 64) {  // sent edges before each bitmap word
+                const uint32_t c = threadIdx.x < (uint32_t)EW ? (uint32_t)__popcll(L.bits[threadIdx.x]) : 0u;
+                uint32_t incl = c;
+#pragma unroll
+                for (int o = 1; o < 32; o <<= 1) {
+                    const uint32_t t = __shfl_up(incl, o, 64);
+                    if (lane >= o) incl += t;
+                }
+                if (threadIdx.x <= (uint32_t)EW) L.bpre[threadIdx.x] = incl - c;
+                if (threadIdx.x == (uint32_t)EW) L.bits[EW] = 0ull;
             }
             __syncthreads();
         }
@@ -734,7 +733,9 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                     if (jw + b >= j0 && jw + b < j1) a.nbn[jw + b] = reinterpret_cast<const uint8_t*>(L.out)[w * 4 + b];
             }
         }
-        __syncthreads();
+        // no barrier here: the next tile's in-edge pass and staging copies write
+        // bits / msg / rows / xm / xp / off, none of which this byte output reads,
+        // and its node phase writes L.out only after its staging barrier
     }
     // block reduction of alerts / newly active
     uint32_t x = alerts, y = newly;
@@ -1377,6 +1378,7 @@ RoundArgs make_round_args(const DevState& S, uint32_t round) {
     a.seed_node = S.seed_node;
     a.ntiles = (S.lo + S.nloc + TILE - 1) / TILE - S.lo / TILE;
     a.walk = S.tile_walk;
+    a.stage_cap = S.tile_stage_cap;
     a.ebits = S.ebits;
     a.etot = S.etot;
     a.emsg = S.emsg;

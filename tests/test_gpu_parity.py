@@ -237,3 +237,23 @@ def test_seed_random_edge_round0(kernel, monkeypatch):
         assert np.array_equal(sim.state()["c"], orc.state()["c"]), f"seed {seed}: counters differ"
         sim.close()
         orc.close()
+
+
+@pytest.mark.parametrize("cap", ["0", "1000", "1024"])
+def test_tile_unstaged_path_parity(cap, monkeypatch):
+    """Push-sum Imp3D tile kernel with the staging cap lowered (GP_STAGE_CAP): tiles
+    with more in-edges than the cap take the unstaged path (per-edge decisions and
+    gathers from HBM) -- all of them at 0, a mix at 1000 / 1024 (mean in-degree
+    1024 per tile).  At the default cap (1216) that path runs for ~1e-9 of tiles."""
+    monkeypatch.setenv("GP_KERNEL", "tile")
+    monkeypatch.setenv("GP_STAGE_CAP", cap)
+    n, seed, rounds, chk = 512000, 4, 90, 45
+    sim, orc = Sim(n, "Imp3D", "push-sum", seed=seed), Oracle(n, "Imp3D", "push-sum", seed)
+    done = 0
+    while done < rounds:
+        k = min(chk, rounds - done)
+        ga, oa = sim.step(k), orc.step(k)
+        assert ga == oa, f"alerts differ in rounds {done}..{done + k}"
+        assert_same_state("push-sum", sim.state(), orc.state())
+        done += k
+    sim.close()
