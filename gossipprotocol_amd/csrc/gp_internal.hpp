@@ -75,6 +75,12 @@ struct DevState {
     // round tag (the round the message was delivered for) and the message
     uint32_t* rtag;
     double2* rmsg;
+    // Imp3D push-sum, tile kernel, one rank: random-edge sends tagged in edge order.
+    // lpos[i] = position of sender i's edge in the receiver-sorted in-edge array;
+    // ltag[b][e] = round the sender of edge e used it in (buffer b = that round's
+    // parity), written by the sender's node phase one round ahead (null: off)
+    uint32_t* ltag[2];
+    uint32_t* lpos;
     int kernel;  // KERNEL_* below
     // column kernels: x segments per patch (set at create from the resident grid)
     uint32_t col_xsegs;
@@ -101,6 +107,9 @@ struct RoundArgs {
     const uint32_t* in_srcd; // in_src with the sender's deg - 4 in bits 30-31, or null
     const uint32_t* rtag;    // per local in-edge: round of the delivered remote message
     const double2* rmsg;
+    const uint32_t* ltc;     // edge tags of this round (DevState::ltag), or null
+    uint32_t* ltn;           // edge tags of the next round
+    const uint32_t* lpos;    // sender -> its edge's position in the in-edge array
     int32_t* c;              // indexed by global id
     Ctl* ctl;
     Geom G;

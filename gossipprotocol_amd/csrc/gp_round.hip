@@ -379,9 +379,12 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* lds, u
 // ---------------------------------------------------------------- push-sum
 // REMOTE: some in-edge senders live on other ranks (multi-GPU slabs); the
 // single-GPU build of the kernel has no exchange-tag paths at all.
-template <int TOPO, bool REMOTE, bool EDGES>
+// LTAG: one-rank opt-in (GP_LTAG=1) -- the in-edge pass reads edge tags the senders
+// wrote last round instead of redrawing their Philox (DevState::ltag).
+template <int TOPO, bool REMOTE, bool EDGES, bool LTAG = false>
 __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t r) {
     static_assert(!EDGES || TOPO == IMP3D, "edge pass is Imp3D only");
+    static_assert(!LTAG || (TOPO == IMP3D && !REMOTE && !EDGES), "edge tags: one-rank Imp3D only");
     __shared__ typename TileLdsSel<EDGES>::type L;
     Ctl* ctl = a.ctl;
     if (ld_agent(&ctl->done)) return;
@@ -449,13 +452,18 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                 // ended at a barrier and its byte output reads L.out only.
                 const uint32_t wv = threadIdx.x >> 6;
                 const uint32_t* srcp = packed ? a.in_srcd : in_src;
-                uint32_t isrc[FU], ideg[FU];
+                // one rank, every node active, round > 0: the senders tagged this round's
+                // random-edge sends in edge order last round (coalesced read, no Philox
+                // redraw); round 0's directions come from k_init, which writes no tags
+                const bool tagged = LTAG && all_active && r > 0;
+                uint32_t isrc[FU], ideg[FU], itag[FU];
 #pragma unroll
                 for (int m = 0; m < FU; ++m) {
                     const uint32_t q = threadIdx.x + m * TPB;
                     const uint32_t raw = q < cnt ? ((GP_ABLATE & ABL_FAKE_SRC) ? ((e_lo + q) * 2654435761u) % a.G.P | 0xC0000000u
                                                                                : srcp[e_lo + q])
                                                  : 0u;
+                    if (LTAG) itag[m] = (tagged && q < cnt) ? a.ltc[e_lo + q] : ~0u;
                     isrc[m] = packed ? raw & 0x3FFFFFFFu : raw;
                     ideg[m] = (raw >> 30) + 4u;
                 }
@@ -469,6 +477,8 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                             sent = a.rtag[e_lo + q] == r;
                         } else if (GP_ABLATE & ABL_NO_EPHILOX) {
                             sent = false;
+                        } else if (LTAG && tagged) {
+                            sent = itag[m] == r;
                         } else if ((GP_ABLATE & ABL_CHEAP_DECIDE) && all_active) {
                             sent = ((i * 2654435761u + r * 40503u) >> 29) == 0u;
                         } else if (all_active && !(GP_ABLATE & ABL_BITMAP_ONLY)) {
@@ -710,6 +720,8 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                         dir = (GP_ABLATE & ABL_NO_NEXTDIR)
                                   ? (j % 7u) % (deg)
                                   : slot_to_dir_fast(mask, uniform(a.k0, a.k1, S_PUSHSUM, j, r + 1, deg));
+                    if (LTAG && dir == DIR_RANDOM)
+                        a.ltn[a.lpos[j]] = r + 1;  // tag the edge for its receiver's next in-edge pass
                     reinterpret_cast<uint8_t*>(L.out)[jl] = (uint8_t)(flags | dir);
                     st_stream(swn + j, make_double2(acc_s, acc_w));
                 }
@@ -1366,6 +1378,9 @@ RoundArgs make_round_args(const DevState& S, uint32_t round) {
     a.in_srcd = S.in_srcd;
     a.rtag = S.rtag;
     a.rmsg = S.rmsg;
+    a.ltc = S.ltag[cur];
+    a.ltn = S.ltag[cur ^ 1];
+    a.lpos = S.lpos;
     a.c = S.c ? S.c - S.lo : nullptr;
     a.lo = S.lo;
     a.nloc = S.nloc;
@@ -1421,6 +1436,8 @@ hipError_t launch_round_tile(const DevState& S, uint32_t round, int grid, hipStr
                     }
                 } else if (remote) {
                     hipLaunchKernelGGL((k_ps_tile<IMP3D, true, false>), g, b, 0, st, a, round);
+                } else if (S.ltag[0]) {
+                    hipLaunchKernelGGL((k_ps_tile<IMP3D, false, false, true>), g, b, 0, st, a, round);
                 } else {
                     hipLaunchKernelGGL((k_ps_tile<IMP3D, false, false>), g, b, 0, st, a, round);
                 }

@@ -198,16 +198,19 @@ WALK_CASES = [  # (num_nodes, topology, seed, rounds, checkpoint)
 ]
 
 
+@pytest.mark.parametrize("ltag", ["0", "1"])
 @pytest.mark.parametrize("edges", ["0", "1"])
 @pytest.mark.parametrize("pack", ["0", "1"])
 @pytest.mark.parametrize("walk", ["0", "1", "2"])
 @pytest.mark.parametrize("n,topo,seed,rounds,chk", WALK_CASES, ids=lambda v: str(v))
-def test_tile_walk_and_sender_packing_parity(n, topo, seed, rounds, chk, walk, pack, edges, monkeypatch):
+def test_tile_walk_and_sender_packing_parity(n, topo, seed, rounds, chk, walk, pack, edges, ltag, monkeypatch):
     """Push-sum tile kernel bit-exact vs the oracle for every tile walk (XCD eighths,
     global sweep, x-windows of 3 planes), with the senders' degree packed into the
-    staged ids or computed (the P > 2^30 path), and with the separate in-edge pass."""
-    if topo != "Imp3D" and (pack == "1" or edges == "1"):
-        pytest.skip("sender packing / edge pass are Imp3D only")
+    staged ids or computed (the P > 2^30 path), with the separate in-edge pass, and
+    with the in-edge pass reading the senders' edge tags or redrawing their Philox."""
+    if topo != "Imp3D" and (pack == "1" or edges == "1" or ltag == "0"):
+        pytest.skip("sender packing / edge pass / edge tags are Imp3D only")
+    monkeypatch.setenv("GP_LTAG", ltag)
     monkeypatch.setenv("GP_KERNEL", "tile")
     monkeypatch.setenv("GP_WALK", walk)
     monkeypatch.setenv("GP_WX", "3")
@@ -221,6 +224,8 @@ def test_tile_walk_and_sender_packing_parity(n, topo, seed, rounds, chk, walk, p
         assert ga == oa, f"alerts differ in rounds {done}..{done + k}"
         assert_same_state("push-sum", sim.state(), orc.state())
         done += k
+    if topo == "Imp3D":  # the steady-state (all nodes active) in-edge pass ran
+        assert sim.info().active == sim.population
     sim.close()
 
 
