@@ -10,8 +10,11 @@ import os
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "libgossip_hip.so")
-# experiments (tools/ablate.py) may point at an ablation build; the product uses the in-tree library
-LIB_PATH = os.environ.get("GOSSIP_HIP_LIB_EXPERIMENT", LIB_PATH)
+# The experiments build (-DGP_EXPERIMENTS: kernel variants and GP_* environment
+# overrides) -- loaded only by the kernel-variant tests and tools/, never by default.
+EXP_LIB_PATH = os.path.join(PKG_DIR, "libgossip_hip_exp.so")
+# tools/ablate.py may point the experiments slot at an ablation build
+EXP_LIB_PATH = os.environ.get("GOSSIP_HIP_LIB_EXPERIMENT", EXP_LIB_PATH)
 
 GP_LINE, GP_FULL, GP_3D, GP_IMP3D = 0, 1, 2, 3
 GP_GOSSIP, GP_PUSHSUM = 0, 1
@@ -63,7 +66,7 @@ SIGNATURES = [
     ("gp_destroy", None, [_vp]),
 ]
 
-_lib = None
+_libs = {}
 
 
 class GossipError(RuntimeError):
@@ -72,22 +75,24 @@ class GossipError(RuntimeError):
         self.code = code
 
 
-def lib():
-    """Load the in-tree HIP library (raises if it has not been built)."""
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise ImportError(f"{LIB_PATH} not built: run __graft_entry__.build() (no CPU fallback exists)")
-        L = C.CDLL(LIB_PATH)
+def lib(experimental: bool = False):
+    """Load the in-tree HIP library (raises if it has not been built).
+    experimental=True loads the experiments build instead (tests / tools only)."""
+    path = EXP_LIB_PATH if experimental else LIB_PATH
+    L = _libs.get(path)
+    if L is None:
+        if not os.path.exists(path):
+            raise ImportError(f"{path} not built: run __graft_entry__.build() (no CPU fallback exists)")
+        L = C.CDLL(path)
         for name, res, args in SIGNATURES:
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
-        _lib = L
-    return _lib
+        _libs[path] = L
+    return L
 
 
-def check(rc):
+def check(rc, L=None):
     if rc < 0:
-        raise GossipError(rc, lib().gp_last_error().decode(errors="replace"))
+        raise GossipError(rc, (L or lib()).gp_last_error().decode(errors="replace"))
     return rc

@@ -160,6 +160,22 @@ int dev_alloc_t(gp_sim* s, T** p, size_t count) {
     return rc;
 }
 
+// Setup temporaries: freed when the scope ends, on success and on every error return.
+struct Scratch {
+    std::vector<void*> ptrs;
+    template <typename T>
+    hipError_t alloc(T** p, size_t count) {
+        void* v = nullptr;
+        const hipError_t e = hipMalloc(&v, count * sizeof(T));
+        if (e == hipSuccess) ptrs.push_back(v);
+        *p = static_cast<T*>(v);
+        return e;
+    }
+    ~Scratch() {
+        for (void* v : ptrs) (void)hipFree(v);
+    }
+};
+
 void free_all(gp_sim* s) {
     for (void* p : s->allocs) (void)hipFree(p);
     s->allocs.clear();
@@ -256,8 +272,6 @@ int alloc_slab(gp_sim* s, Slab& sl, int r) {
     S.base = S.ext_lo & ~3u;  // 4-aligned: the tile kernels move node bytes as words
     S.rtag = nullptr;
     S.rmsg = nullptr;
-    S.ltag[0] = S.ltag[1] = nullptr;
-    S.lpos = nullptr;
     int rc;
     const size_t next = (size_t)(S.ext_hi - S.base) + 1024;  // node arrays (+ word-I/O padding)
     const size_t nl = S.nloc;
@@ -296,20 +310,6 @@ int alloc_slab(gp_sim* s, Slab& sl, int r) {
         S.sort_tmp_bytes = tb;
         if ((rc = dev_alloc(s, &S.sort_tmp, tb))) return rc;
     }
-    S.ebits = nullptr;
-    S.etot = nullptr;
-    S.emsg = nullptr;
-    // separate in-edge pass (k_ps_edges): opt-in, GP_EDGES=1 (measured slower than the
-    // in-tile pass: 17.9 vs 16.2 ms/round at P = 1e9, profiles/r01)
-    const char* ge = std::getenv("GP_EDGES");
-    if (S.topo == IMP3D && S.alg == PUSHSUM && S.kernel == KERNEL_TILE && ge && ge[0] == '1' &&
-        round_tiles(1024) == 1) {  // edge buffers are sized for 1024-node tiles
-        // in-edge pass output (k_ps_edges): per tile EDGE_WORDS bitmap words, a count, EDGE_MSGS slots
-        const size_t nt = (size_t)((S.lo + (uint64_t)S.nloc + 1023) / 1024 - S.lo / 1024);
-        if ((rc = dev_alloc_t(s, &S.ebits, nt * EDGE_WORDS)) || (rc = dev_alloc_t(s, &S.etot, nt)) ||
-            (rc = dev_alloc_t(s, &S.emsg, nt * EDGE_MSGS)))
-            return rc;
-    }
     if (S.topo == IMP3D) {
         S.rbits_words = S.kernel == KERNEL_COL ? col_rbits_words(S.nloc / S.G.g2, S.G.g)
                                                : rbits_words_for(S.lo, S.nloc);
@@ -329,31 +329,32 @@ int build_imp3d(gp_sim* s) {
     const uint32_t P = (uint32_t)s->P;
     const int W = s->world;
     DevState& S0 = s->slab[0].S;
+    Scratch tmp_mem;  // setup temporaries, freed on every exit path
     uint32_t *rnd_all = nullptr, *iota = nullptr, *keys_sorted = nullptr, *src_sorted = nullptr, *counts = nullptr,
              *off_all = nullptr, *inv = nullptr;
-    HIP_TRY(hipMalloc(&rnd_all, sizeof(uint32_t) * P));
-    HIP_TRY(hipMalloc(&iota, sizeof(uint32_t) * P));
-    HIP_TRY(hipMalloc(&keys_sorted, sizeof(uint32_t) * P));
-    HIP_TRY(hipMalloc(&src_sorted, sizeof(uint32_t) * P));
-    HIP_TRY(hipMalloc(&counts, sizeof(uint32_t) * ((size_t)P + 1)));
-    HIP_TRY(hipMalloc(&off_all, sizeof(uint32_t) * ((size_t)P + 1)));
+    HIP_TRY(tmp_mem.alloc(&rnd_all, P));
+    HIP_TRY(tmp_mem.alloc(&iota, P));
+    HIP_TRY(tmp_mem.alloc(&keys_sorted, P));
+    HIP_TRY(tmp_mem.alloc(&src_sorted, P));
+    HIP_TRY(tmp_mem.alloc(&counts, (size_t)P + 1));
+    HIP_TRY(tmp_mem.alloc(&off_all, (size_t)P + 1));
     HIP_TRY(launch_topo_rnd_range(S0.k0, S0.k1, P, 0, P, rnd_all, s->grid, s->stream));
     HIP_TRY(launch_iota(iota, P, s->grid, s->stream));
     const uint32_t bits = bits_for(P > 1 ? P - 2 : 0);
     size_t tmp_bytes = 0;
     HIP_TRY(sort_pairs(nullptr, tmp_bytes, rnd_all, keys_sorted, iota, src_sorted, P, bits, s->stream));
-    void* tmp = nullptr;
-    HIP_TRY(hipMalloc(&tmp, tmp_bytes ? tmp_bytes : 4));
+    uint8_t* tmp = nullptr;
+    HIP_TRY(tmp_mem.alloc(&tmp, tmp_bytes ? tmp_bytes : 4));
     HIP_TRY(sort_pairs(tmp, tmp_bytes, rnd_all, keys_sorted, iota, src_sorted, P, bits, s->stream));
     HIP_TRY(hipMemsetAsync(counts, 0, sizeof(uint32_t) * ((size_t)P + 1), s->stream));
     HIP_TRY(launch_histogram(rnd_all, P, counts, s->grid, s->stream));
     size_t scan_bytes = 0;
     HIP_TRY(exclusive_scan_u32(nullptr, scan_bytes, counts, off_all, P + 1, s->stream));
-    void* scan_tmp = nullptr;
-    HIP_TRY(hipMalloc(&scan_tmp, scan_bytes ? scan_bytes : 4));
+    uint8_t* scan_tmp = nullptr;
+    HIP_TRY(tmp_mem.alloc(&scan_tmp, scan_bytes ? scan_bytes : 4));
     HIP_TRY(exclusive_scan_u32(scan_tmp, scan_bytes, counts, off_all, P + 1, s->stream));
     if (W > 1) {
-        HIP_TRY(hipMalloc(&inv, sizeof(uint32_t) * P));
+        HIP_TRY(tmp_mem.alloc(&inv, P));
         HIP_TRY(launch_inverse(src_sorted, P, inv, s->grid, s->stream));
     }
     // first global edge of every rank
@@ -380,23 +381,13 @@ int build_imp3d(gp_sim* s) {
             HIP_TRY(hipMemcpyAsync(S.in_src, src_sorted + edge0[r], sizeof(uint32_t) * ne, hipMemcpyDeviceToDevice,
                                    s->stream));
         S.in_srcd = nullptr;
-        const char* np = std::getenv("GP_NO_PACK");  // tests: force the unpacked (P > 2^30) path
-        if (S.alg == PUSHSUM && S.kernel == KERNEL_TILE && s->P <= (1ll << 30) && s->g >= 2 && !(np && np[0] == '1')) {
+        bool pack = true;
+#ifdef GP_EXPERIMENTS
+        if (const char* np = std::getenv("GP_NO_PACK")) pack = np[0] != '1';  // force the unpacked (P > 2^30) path
+#endif
+        if (S.alg == PUSHSUM && S.kernel == KERNEL_TILE && s->P <= (1ll << 30) && s->g >= 2 && pack) {
             if ((rc = dev_alloc_t(s, &S.in_srcd, (size_t)ne + 4))) return rc;
             if (ne) HIP_TRY(launch_pack_src_deg(S.in_src, S.in_srcd, ne, S.G, s->grid, s->stream));
-        }
-        // opt-in (GP_LTAG=1, one rank): senders tag their random-edge sends in edge order
-        // one round ahead, so the tile kernel's in-edge pass reads a coalesced tag instead
-        // of redrawing every sender's Philox.  Bit-identical but slower (18.4 vs 14.7 ms
-        // at P = 1e9): the scattered 4-byte tag stores cost more than the redraw.
-        const char* lt = std::getenv("GP_LTAG");
-        if (W == 1 && S.alg == PUSHSUM && S.kernel == KERNEL_TILE && lt && lt[0] == '1') {
-            if ((rc = dev_alloc_t(s, &S.lpos, (size_t)S.nloc + 4)) ||
-                (rc = dev_alloc_t(s, &S.ltag[0], (size_t)ne + 4)) || (rc = dev_alloc_t(s, &S.ltag[1], (size_t)ne + 4)))
-                return rc;
-            HIP_TRY(hipMemsetAsync(S.ltag[0], 0xFF, sizeof(uint32_t) * ((size_t)ne + 4), s->stream));
-            HIP_TRY(hipMemsetAsync(S.ltag[1], 0xFF, sizeof(uint32_t) * ((size_t)ne + 4), s->stream));
-            HIP_TRY(launch_inverse(src_sorted, P, S.lpos, s->grid, s->stream));
         }
         if (W > 1) {
             if ((rc = dev_alloc_t(s, &sl.pos, S.nloc)) || (rc = dev_alloc_t(s, &S.rtag, ne)) ||
@@ -417,15 +408,6 @@ int build_imp3d(gp_sim* s) {
         }
     }
     HIP_TRY(hipStreamSynchronize(s->stream));
-    HIP_TRY(hipFree(scan_tmp));
-    HIP_TRY(hipFree(tmp));
-    if (inv) HIP_TRY(hipFree(inv));
-    HIP_TRY(hipFree(off_all));
-    HIP_TRY(hipFree(counts));
-    HIP_TRY(hipFree(src_sorted));
-    HIP_TRY(hipFree(keys_sorted));
-    HIP_TRY(hipFree(iota));
-    HIP_TRY(hipFree(rnd_all));
     return GP_OK;
 }
 
@@ -438,10 +420,11 @@ int setup_exchange(gp_sim* s) {
     const bool push = s->cfg.algorithm == GP_PUSHSUM;
     const bool full = s->cfg.topology == GP_FULL;
     std::vector<uint32_t> caps((size_t)W * W, 0);  // caps[a * W + b]: a -> b
+    Scratch tmp_mem;
     double* mu = nullptr;
     unsigned long long* n = nullptr;
-    HIP_TRY(hipMalloc(&mu, sizeof(double) * XMAXW));
-    HIP_TRY(hipMalloc(&n, sizeof(unsigned long long) * XMAXW));
+    HIP_TRY(tmp_mem.alloc(&mu, XMAXW));
+    HIP_TRY(tmp_mem.alloc(&n, XMAXW));
     if (full) {
         // every active sender picks a uniform target among P-1: messages a -> b are at
         // most Binomial(nloc_a, nloc_b / (P-1))
@@ -484,18 +467,21 @@ int setup_exchange(gp_sim* s) {
             caps[(size_t)sl.rank * W + b] = (uint32_t)std::min<double>(c, (double)hn[b]);
         }
     }
-    HIP_TRY(hipFree(mu));
-    HIP_TRY(hipFree(n));
+#ifdef GP_EXPERIMENTS
+    if (const char* e = std::getenv("GP_XCAP")) {  // tests: force tiny buffers (overflow handling)
+        const uint32_t cap = (uint32_t)std::max(1, std::atoi(e));
+        for (auto& c : caps) c = std::min(c, cap);
+    }
+#endif
     if (s->mode == MODE_RCCL) {
         // every rank learns the capacities of the buffers it will receive
         uint32_t* d = nullptr;
-        HIP_TRY(hipMalloc(&d, sizeof(uint32_t) * W * W));
+        HIP_TRY(tmp_mem.alloc(&d, (size_t)W * W));
         HIP_TRY(hipMemcpyAsync(d + (size_t)s->rank * W, caps.data() + (size_t)s->rank * W, sizeof(uint32_t) * W,
                                hipMemcpyHostToDevice, s->stream));
         NCCL_TRY(ncclAllGather(d + (size_t)s->rank * W, d, W, ncclUint32, s->comm, s->stream));
         HIP_TRY(hipMemcpyAsync(caps.data(), d, sizeof(uint32_t) * W * W, hipMemcpyDeviceToHost, s->stream));
         HIP_TRY(hipStreamSynchronize(s->stream));
-        HIP_TRY(hipFree(d));
     }
     int rc;
     for (Slab& sl : s->slab) {
@@ -748,6 +734,7 @@ int exchange(gp_sim* s, uint32_t rn) {
             ua.me = sl.rank;
             ua.push = push ? 1 : 0;
             for (int p = 0; p < W; ++p) ua.peer[p] = xpeer(sl.xrecv, sl.roff[p], sl.cap_in[p]);
+            ua.overflow = sl.overflow;
             HIP_TRY(launch_unpack(ua, rn, std::max(1, s->grid / 8), s->stream));
         }
     }
@@ -827,18 +814,21 @@ void choose_kernel(gp_sim* s, int64_t nloc_max, int& kernel, uint32_t& col_xsegs
     kernel = KERNEL_TILE;
     const bool lattice = cfg->topology == GP_3D || cfg->topology == GP_IMP3D;
     if (lattice && cfg->algorithm == GP_GOSSIP && g >= 200) kernel = KERNEL_COL;
+#ifdef GP_EXPERIMENTS
     if (const char* e = std::getenv("GP_KERNEL")) {
         if (!std::strcmp(e, "tile")) kernel = KERNEL_TILE;
-        else if (!std::strcmp(e, "tile2")) kernel = KERNEL_TILE2;
-        else if (!std::strcmp(e, "xtile") && lattice) kernel = KERNEL_XTILE;
         else if (!std::strcmp(e, "wave")) kernel = KERNEL_WAVE;
         else if (!std::strcmp(e, "col") && lattice) kernel = KERNEL_COL;
     }
+#endif
     col_xsegs = 1;
-    if (cfg->topology != GP_FULL && kernel != KERNEL_TILE && kernel != KERNEL_TILE2 && kernel != KERNEL_XTILE) {
+    if (cfg->topology != GP_FULL && kernel != KERNEL_TILE) {
         // exactly the resident grid (a persistent sweep), a multiple of the 8 XCDs
-        const int bpc = kernel == KERNEL_COL ? col_blocks_per_cu(cfg->topology, cfg->algorithm)
-                                             : wave_blocks_per_cu(cfg->topology, cfg->algorithm);
+        int bpc = 1;
+        if (kernel == KERNEL_COL) bpc = col_blocks_per_cu(cfg->topology, cfg->algorithm);
+#ifdef GP_EXPERIMENTS
+        else bpc = wave_blocks_per_cu(cfg->topology, cfg->algorithm);
+#endif
         cap = (int64_t)prop.multiProcessorCount * bpc;
         if (kernel == KERNEL_COL) {
             // x segments per patch: enough work items for every resident wave, >= 16 planes each
@@ -850,23 +840,19 @@ void choose_kernel(gp_sim* s, int64_t nloc_max, int& kernel, uint32_t& col_xsegs
             col_xsegs = (uint32_t)xs;
         }
     }
-    if (kernel == KERNEL_XTILE) {
-        // x-segments: about 16 (window, segment) items per CU slot, >= 8 planes per segment
-        const int64_t nwin = xtile_windows((uint32_t)(g * g));
-        const int64_t planes = std::max<int64_t>(1, g / s->world);
-        int64_t xs = std::max<int64_t>(1, (cap + nwin - 1) / nwin);
-        xs = std::min<int64_t>(xs, std::max<int64_t>(1, planes / 8));
-        col_xsegs = (uint32_t)xs;
-    }
+#ifdef GP_EXPERIMENTS
     if (const char* e = std::getenv("GP_GRID")) cap = std::max<int64_t>(1, std::atoll(e));
     if (const char* e = std::getenv("GP_XSEGS")) col_xsegs = (uint32_t)std::max(1, std::atoi(e));
+#endif
     s->grid = (int)std::max<int64_t>(1, std::min(kernel == KERNEL_COL ? cap : blocks, cap));
     // tile walk: x-windows of 8 planes once every XCD gets a few windows (measured,
     // profiles/r01: 18.2 -> 17.2 ms/round at P = 1e9), else XCD-contiguous eighths
     walk = (lattice && g / s->world >= 64) ? 2u : 0u;
-    if (const char* e = std::getenv("GP_WALK")) walk = (uint32_t)std::atoi(e);
     wx = 8;
+#ifdef GP_EXPERIMENTS
+    if (const char* e = std::getenv("GP_WALK")) walk = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("GP_WX")) wx = (uint32_t)std::max(1, std::atoi(e));
+#endif
 }
 
 // Everything after the handle exists: slabs, topology, initial state, round 0.
@@ -891,7 +877,9 @@ int build_sim(gp_sim* s) {
         sl.S.tile_walk = walk;
         sl.S.tile_wx = wx;
         sl.S.tile_stage_cap = 0xFFFFFFFFu;
+#ifdef GP_EXPERIMENTS
         if (const char* e = std::getenv("GP_STAGE_CAP")) sl.S.tile_stage_cap = (uint32_t)std::max(0, std::atoi(e));
+#endif
         if ((rc = alloc_slab(s, sl, sl.rank))) return rc;
     }
     if (s->cfg.topology == GP_IMP3D && (rc = build_imp3d(s))) return rc;
@@ -1030,7 +1018,7 @@ int gp_resolve(int64_t n, int32_t topology, int64_t* P, int64_t* T, int64_t* g) 
         set_err("unknown topology id %d", topology);
         return GP_EINVAL;
     }
-    if (*P > 0xFFFFFF00ll) {
+    if (*P > (int64_t)GP_MAX_POPULATION) {
         set_err("population %lld exceeds the 32-bit node-id range", (long long)*P);
         return GP_EINVAL;
     }
@@ -1067,10 +1055,13 @@ int gp_create_rank(const gp_config* cfg, int32_t rank, int32_t world, const uint
         set_err("gp_create_rank: bad argument (rank %d, world %d)", rank, world);
         return GP_EINVAL;
     }
-    // GP_FORCE_RCCL=1: a one-rank RCCL communicator (smoke test of the RCCL
-    // transport on a single GPU: init, bookkeeping all-reduce, teardown)
-    const char* force = std::getenv("GP_FORCE_RCCL");
-    if (world == 1 && !(force && force[0] == '1')) return create_common(cfg, MODE_SINGLE, 1, 0, nullptr, out);
+    bool force = false;
+#ifdef GP_EXPERIMENTS
+    // GP_FORCE_RCCL=1: a one-rank RCCL communicator (test of the RCCL transport
+    // on a single GPU: init, bookkeeping all-reduce, teardown)
+    if (const char* e = std::getenv("GP_FORCE_RCCL")) force = e[0] == '1';
+#endif
+    if (world == 1 && !force) return create_common(cfg, MODE_SINGLE, 1, 0, nullptr, out);
     if (!unique_id) {
         set_err("gp_create_rank: null unique id");
         return GP_EINVAL;

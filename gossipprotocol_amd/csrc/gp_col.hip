@@ -147,6 +147,9 @@ __device__ __forceinline__ void row_offsets(const WaveArgs& a, uint32_t rs, uint
 }  // namespace
 
 // ---------------------------------------------------------------- push-sum
+// Experiment variant (push-sum runs the tiled kernel):
+// experiments library only.
+#ifdef GP_EXPERIMENTS
 template <int TOPO>
 __global__ __launch_bounds__(BULK_THREADS) void k_ps_col(WaveArgs a, uint32_t r) {
     __shared__ WaveLds Lw[WPB];
@@ -345,6 +348,7 @@ __global__ __launch_bounds__(BULK_THREADS) void k_ps_col(WaveArgs a, uint32_t r)
     }
     block_add2(alerts, newly, &ctl->round_alerts, &ctl->round_active);
 }
+#endif  // GP_EXPERIMENTS
 
 // ---------------------------------------------------------------- gossip
 // Deliveries to j = lattice senders pointing here + Imp3D random-edge senders
@@ -498,8 +502,12 @@ uint32_t col_rbits_words(uint32_t planes, uint32_t g) { return planes * g * ((g 
 
 int col_blocks_per_cu(int topo, int alg) {
     const void* f;
+    f = topo == GRID3D ? (const void*)k_gossip_col<GRID3D> : (const void*)k_gossip_col<IMP3D>;
+#ifdef GP_EXPERIMENTS
     if (alg == PUSHSUM) f = topo == GRID3D ? (const void*)k_ps_col<GRID3D> : (const void*)k_ps_col<IMP3D>;
-    else f = topo == GRID3D ? (const void*)k_gossip_col<GRID3D> : (const void*)k_gossip_col<IMP3D>;
+#else
+    (void)alg;
+#endif
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, BULK_THREADS, 0) != hipSuccess || n < 1) n = 1;
     return n;
@@ -508,8 +516,12 @@ int col_blocks_per_cu(int topo, int alg) {
 hipError_t launch_round_col(const WaveArgs& a, int topo, int alg, uint32_t round, int grid, hipStream_t st) {
     const dim3 g(grid), b(BULK_THREADS);
     if (alg == PUSHSUM) {
+#ifdef GP_EXPERIMENTS
         if (topo == GRID3D) hipLaunchKernelGGL(k_ps_col<GRID3D>, g, b, 0, st, a, round);
         else hipLaunchKernelGGL(k_ps_col<IMP3D>, g, b, 0, st, a, round);
+#else
+        return hipErrorInvalidValue;
+#endif
     } else {
         if (topo == GRID3D) hipLaunchKernelGGL(k_gossip_col<GRID3D>, g, b, 0, st, a, round);
         else hipLaunchKernelGGL(k_gossip_col<IMP3D>, g, b, 0, st, a, round);

@@ -74,6 +74,49 @@ GP_HD void philox2(uint32_t node, uint32_t round, uint32_t stream, uint32_t k0, 
     y = c1;
 }
 
+// N independent Philox4x32-10 draws (same round and stream, nodes node[0..N))
+// in one straight-line block: the rounds of the N chains interleave, so their
+// multiply latencies overlap; the wave-uniform key schedule is computed once
+// per round for all chains.  Bit-identical to N calls of philox2.
+template <int N>
+GP_HD void philox2_batch(const uint32_t (&node)[N], uint32_t round, uint32_t stream, uint32_t k0, uint32_t k1,
+                         uint32_t (&x)[N], uint32_t (&y)[N]) {
+    uint32_t c0[N], c1[N], c2[N], c3[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        c0[i] = node[i];
+        c1[i] = round;
+        c2[i] = stream;
+        c3[i] = 0;
+    }
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+s"(k0), "+s"(k1));  // see philox2: keep the key schedule off the hoisting path
+#endif
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        if (r) {
+            k0 += 0x9E3779B9u;
+            k1 += 0xBB67AE85u;
+        }
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            const uint64_t p0 = (uint64_t)0xD2511F53u * c0[i];
+            const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2[i];
+            const uint32_t n0 = xor3((uint32_t)(p1 >> 32), c1[i], k0);
+            const uint32_t n2 = xor3((uint32_t)(p0 >> 32), c3[i], k1);
+            c1[i] = (uint32_t)p1;
+            c3[i] = (uint32_t)p0;
+            c0[i] = n0;
+            c2[i] = n2;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        x[i] = c0[i];
+        y[i] = c1[i];
+    }
+}
+
 // U(m) = floor(((y<<32)|x) * m / 2^64) for m < 2^32 (exact, no 128-bit type).
 GP_HD uint32_t uniform_from(uint32_t x, uint32_t y, uint32_t m) {
     const uint64_t lo = (uint64_t)x * m;

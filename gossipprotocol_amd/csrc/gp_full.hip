@@ -224,7 +224,9 @@ __global__ __launch_bounds__(256) void k_fullm_gossip_send(FullArgs a, uint32_t 
 __global__ __launch_bounds__(256) void k_fullm_gossip_unpack(FullArgs a) {
     const int p = blockIdx.y;
     if (p == a.me || !a.rpeer[p].cnt) return;
-    const uint32_t n = min(*a.rpeer[p].cnt, a.rpeer[p].cap);
+    const uint32_t sent = *a.rpeer[p].cnt;
+    if (sent > a.rpeer[p].cap && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.overflow, 1u);
+    const uint32_t n = min(sent, a.rpeer[p].cap);
     for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < n; k += gridDim.x * 256) {
         const uint32_t t = a.rpeer[p].slots[k];
         if (t < a.nloc) atomicAdd(&a.inc[t], 1);

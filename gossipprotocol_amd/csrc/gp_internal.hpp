@@ -75,23 +75,12 @@ struct DevState {
     // round tag (the round the message was delivered for) and the message
     uint32_t* rtag;
     double2* rmsg;
-    // Imp3D push-sum, tile kernel, one rank: random-edge sends tagged in edge order.
-    // lpos[i] = position of sender i's edge in the receiver-sorted in-edge array;
-    // ltag[b][e] = round the sender of edge e used it in (buffer b = that round's
-    // parity), written by the sender's node phase one round ahead (null: off)
-    uint32_t* ltag[2];
-    uint32_t* lpos;
     int kernel;  // KERNEL_* below
     // column kernels: x segments per patch (set at create from the resident grid)
     uint32_t col_xsegs;
     uint32_t tile_walk;  // RoundArgs::walk
     uint32_t tile_wx;    // RoundArgs::wx
-    uint32_t tile_stage_cap;  // RoundArgs::stage_cap (GP_STAGE_CAP, tests only; default: no limit)
-    // Imp3D push-sum, tile kernel: output of the in-edge pass (k_ps_edges) per
-    // tile -- bitmap of used in-edges, message count, compact messages
-    unsigned long long* ebits;
-    uint32_t* etot;
-    double2* emsg;
+    uint32_t tile_stage_cap;  // RoundArgs::stage_cap (experiments build only; default: no limit)
 };
 
 // Arguments of the tiled round kernels (gp_round.hip): only what they read.
@@ -107,9 +96,6 @@ struct RoundArgs {
     const uint32_t* in_srcd; // in_src with the sender's deg - 4 in bits 30-31, or null
     const uint32_t* rtag;    // per local in-edge: round of the delivered remote message
     const double2* rmsg;
-    const uint32_t* ltc;     // edge tags of this round (DevState::ltag), or null
-    uint32_t* ltn;           // edge tags of the next round
-    const uint32_t* lpos;    // sender -> its edge's position in the in-edge array
     int32_t* c;              // indexed by global id
     Ctl* ctl;
     Geom G;
@@ -117,14 +103,10 @@ struct RoundArgs {
     uint32_t lo, nloc, ext_lo, ext_hi;  // owned ids [lo, lo + nloc); arrays hold [ext_lo, ext_hi)
     uint32_t walk;  // 0: XCD-contiguous eighths, 1: one global sweep (tile t -> block t % grid), 2: x-windows
     uint32_t wx;    // walk 2: planes per x-window
-    unsigned long long* ebits;  // in-edge pass output (k_ps_edges -> k_ps_tile<IMP3D, *, true>)
-    uint32_t* etot;
-    double2* emsg;
-    uint32_t xs_len;  // k_ps_xtile: planes per x-segment
     uint32_t stage_cap;  // k_ps_tile: tiles with more in-edges take the unstaged path (tests force it)
 };
 
-enum KernelVariant : int { KERNEL_WAVE = 0, KERNEL_TILE = 1, KERNEL_COL = 2, KERNEL_TILE2 = 3, KERNEL_XTILE = 4 };
+enum KernelVariant : int { KERNEL_WAVE = 0, KERNEL_TILE = 1, KERNEL_COL = 2 };
 
 // Arguments of the wave-autonomous round kernels (gp_wave.hip, gp_col.hip).
 struct WaveArgs {
@@ -162,18 +144,11 @@ uint32_t col_rbits_words(uint32_t planes, uint32_t g);
 hipError_t launch_col_rbits_init(const DevState& S, hipStream_t st);
 
 // ---- tiled round kernels (gp_round.hip)
-uint32_t round_tiles(uint32_t P);
-// in-edge pass buffers per tile: bitmap words, message slots
-constexpr uint32_t EDGE_WORDS = 24, EDGE_MSGS = 384;
 uint32_t rbits_words_for(uint32_t lo, uint32_t nloc);
 hipError_t launch_round_tile(const DevState& S, uint32_t round, int grid, hipStream_t st);
 hipError_t launch_rbits_init(const DevState& S, int grid, hipStream_t st);
 hipError_t launch_pack_src_deg(const uint32_t* src, uint32_t* out, uint32_t n, const Geom& G, int grid,
                                hipStream_t st);
-
-// ---- x-marching tiled push-sum kernel (gp_xtile.hip): 3D / Imp3D
-hipError_t launch_round_xtile(const RoundArgs& a, int topo, bool remote, uint32_t round, int grid, hipStream_t st);
-uint32_t xtile_windows(uint32_t g2);
 
 // ---- kernels (gp_kernels.hip)
 hipError_t launch_init(const DevState& S, int grid, hipStream_t st);

@@ -392,7 +392,9 @@ __global__ __launch_bounds__(FIN_THREADS) void k_finalize_pre(DevState S, uint32
         ctl->xchg[0] = skip ? 0ull : atomicExch(&ctl->round_alerts, 0ull);
         ctl->xchg[1] = skip ? 0ull : atomicExch(&ctl->round_active, 0ull);
         ctl->xchg[2] = 0ull;
-        ctl->xchg[3] = 0ull;
+        // an exchange buffer of this rank overflowed (send or receive side): summed
+        // over ranks, so every rank fails the batch (gp_step), not only the sender
+        ctl->xchg[3] = ld_agent(&ctl->overflow) ? 1ull : 0ull;
         ctl->inj_pick = -1;
     }
     if (skip || !injector) return;
@@ -410,6 +412,7 @@ __global__ __launch_bounds__(FIN_THREADS) void k_finalize_pre(DevState S, uint32
 __global__ void k_finalize_post(DevState S, uint32_t round_done, int has_done, int injector) {
     Ctl* ctl = S.ctl;
     if (threadIdx.x != 0) return;
+    if (ctl->xchg[3]) ctl->overflow = 1u;  // some rank's exchange overflowed: this run is invalid
     if (ld_agent(&ctl->done)) return;
     if (has_done && close_round(S, round_done, ctl->xchg[0], ctl->xchg[1])) return;
     long long target = -1;
@@ -461,10 +464,13 @@ hipError_t launch_histogram(const uint32_t* keys, uint32_t n, uint32_t* counts, 
 hipError_t launch_bulk(const DevState& S, uint32_t round, int grid, hipStream_t st) {
     const dim3 g(grid), b(BULK_THREADS);
     if (S.topo != FULL) {
-        if (S.kernel == KERNEL_TILE || S.kernel == KERNEL_TILE2 || S.kernel == KERNEL_XTILE)
-            return launch_round_tile(S, round, grid, st);
+        if (S.kernel == KERNEL_TILE) return launch_round_tile(S, round, grid, st);
         if (S.kernel == KERNEL_COL) return launch_round_col(make_wave_args(S, round), S.topo, S.alg, round, grid, st);
+#ifdef GP_EXPERIMENTS
         return launch_round_wave(make_wave_args(S, round), S.topo, S.alg, round, grid, st);
+#else
+        return hipErrorInvalidValue;
+#endif
     }
     if (S.alg == PUSHSUM) {
         hipLaunchKernelGGL(k_full_ps_recv, g, b, 0, st, S, round);
@@ -476,26 +482,18 @@ hipError_t launch_bulk(const DevState& S, uint32_t round, int grid, hipStream_t 
 }
 
 const char* bulk_kernel_name(const DevState& S) {
-    static const char* ps[5][4] = {{"k_ps_wave<LINE>", "k_full_ps_send+sort+mark+recv", "k_ps_wave<GRID3D>",
+    static const char* ps[3][4] = {{"k_ps_wave<LINE>", "k_full_ps_send+bin+recv", "k_ps_wave<GRID3D>",
                                     "k_ps_wave<IMP3D>"},
-                                   {"k_ps_tile<LINE>", "k_full_ps_send+sort+mark+recv", "k_ps_tile<GRID3D>",
+                                   {"k_ps_tile<LINE>", "k_full_ps_send+bin+recv", "k_ps_tile<GRID3D>",
                                     "k_ps_tile<IMP3D>"},
-                                   {"k_ps_wave<LINE>", "k_full_ps_send+sort+mark+recv", "k_ps_col<GRID3D>",
-                                    "k_ps_col<IMP3D>"},
-                                   {"k_ps_tile2<LINE>", "k_full_ps_send+sort+mark+recv", "k_ps_tile2<GRID3D>",
-                                    "k_ps_tile2<IMP3D>"},
-                                   {"k_ps_tile<LINE>", "k_full_ps_send+sort+mark+recv", "k_ps_xtile<GRID3D>",
-                                    "k_ps_xtile<IMP3D>"}};
-    static const char* go[5][4] = {{"k_gossip_wave<LINE>", "k_full_gossip_send+recv", "k_gossip_wave<GRID3D>",
+                                   {"k_ps_wave<LINE>", "k_full_ps_send+bin+recv", "k_ps_col<GRID3D>",
+                                    "k_ps_col<IMP3D>"}};
+    static const char* go[3][4] = {{"k_gossip_wave<LINE>", "k_full_gossip_send+recv", "k_gossip_wave<GRID3D>",
                                     "k_gossip_wave<IMP3D>"},
                                    {"k_gossip_tile<LINE>", "k_full_gossip_send+recv", "k_gossip_tile<GRID3D>",
                                     "k_gossip_tile<IMP3D>"},
                                    {"k_gossip_wave<LINE>", "k_full_gossip_send+recv", "k_gossip_col<GRID3D>",
-                                    "k_gossip_col<IMP3D>"},
-                                   {"k_gossip_tile<LINE>", "k_full_gossip_send+recv", "k_gossip_tile<GRID3D>",
-                                    "k_gossip_tile<IMP3D>"},
-                                   {"k_gossip_tile<LINE>", "k_full_gossip_send+recv", "k_gossip_tile<GRID3D>",
-                                    "k_gossip_tile<IMP3D>"}};
+                                    "k_gossip_col<IMP3D>"}};
     const int v = S.kernel;
     return S.alg == PUSHSUM ? ps[v][S.topo] : go[v][S.topo];
 }

@@ -26,10 +26,15 @@
 
 namespace gp {
 namespace {
-
-using namespace wk;
 constexpr int WNPT = 4;                 // nodes per lane per chunk
 constexpr int CH = 64 * WNPT;           // nodes per chunk
+}  // namespace
+
+// The chunk kernels are an experiment variant (measured slower than the tiled
+// kernels): built into the experiments library only.
+#ifdef GP_EXPERIMENTS
+namespace {
+using namespace wk;
 
 // Did sender i use its random edge in round r?  (i local to this rank.)
 __device__ __forceinline__ bool local_sent_random(const WaveArgs& a, uint32_t i, uint32_t r, bool all_active,
@@ -356,8 +361,6 @@ __global__ __launch_bounds__(BULK_THREADS) void k_gossip_wave(WaveArgs a, uint32
     block_add2(alerts, 0u, &ctl->round_alerts, nullptr);
 }
 
-uint32_t wave_chunks(uint32_t lo, uint32_t nloc) { return (lo + nloc + CH - 1) / CH - lo / CH; }
-
 // Resident 256-thread blocks per CU of the round kernel (grid = this x CUs: one
 // continuous sweep, so the x-1 plane a chunk gathers from was just streamed).
 int wave_blocks_per_cu(int topo, int alg) {
@@ -371,6 +374,29 @@ int wave_blocks_per_cu(int topo, int alg) {
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, BULK_THREADS, 0) != hipSuccess || n < 1) n = 1;
     return n;
+}
+
+hipError_t launch_round_wave(const WaveArgs& a, int topo, int alg, uint32_t round, int grid, hipStream_t st) {
+    const dim3 g(grid), b(BULK_THREADS);
+    if (alg == PUSHSUM) {
+        switch (topo) {
+            case LINE: hipLaunchKernelGGL(k_ps_wave<LINE>, g, b, 0, st, a, round); break;
+            case GRID3D: hipLaunchKernelGGL(k_ps_wave<GRID3D>, g, b, 0, st, a, round); break;
+            default: hipLaunchKernelGGL(k_ps_wave<IMP3D>, g, b, 0, st, a, round); break;
+        }
+    } else {
+        switch (topo) {
+            case LINE: hipLaunchKernelGGL(k_gossip_wave<LINE>, g, b, 0, st, a, round); break;
+            case GRID3D: hipLaunchKernelGGL(k_gossip_wave<GRID3D>, g, b, 0, st, a, round); break;
+            default: hipLaunchKernelGGL(k_gossip_wave<IMP3D>, g, b, 0, st, a, round); break;
+        }
+    }
+    return hipGetLastError();
+}
+#endif  // GP_EXPERIMENTS
+
+uint32_t wave_chunks(uint32_t lo, uint32_t nloc) {
+    return (uint32_t)(((uint64_t)lo + nloc + CH - 1) / CH - lo / CH);
 }
 
 WaveArgs make_wave_args(const DevState& S, uint32_t round) {
@@ -410,24 +436,6 @@ WaveArgs make_wave_args(const DevState& S, uint32_t round) {
         a.nitems = a.zsegs * a.yblocks * nseg;
     }
     return a;
-}
-
-hipError_t launch_round_wave(const WaveArgs& a, int topo, int alg, uint32_t round, int grid, hipStream_t st) {
-    const dim3 g(grid), b(BULK_THREADS);
-    if (alg == PUSHSUM) {
-        switch (topo) {
-            case LINE: hipLaunchKernelGGL(k_ps_wave<LINE>, g, b, 0, st, a, round); break;
-            case GRID3D: hipLaunchKernelGGL(k_ps_wave<GRID3D>, g, b, 0, st, a, round); break;
-            default: hipLaunchKernelGGL(k_ps_wave<IMP3D>, g, b, 0, st, a, round); break;
-        }
-    } else {
-        switch (topo) {
-            case LINE: hipLaunchKernelGGL(k_gossip_wave<LINE>, g, b, 0, st, a, round); break;
-            case GRID3D: hipLaunchKernelGGL(k_gossip_wave<GRID3D>, g, b, 0, st, a, round); break;
-            default: hipLaunchKernelGGL(k_gossip_wave<IMP3D>, g, b, 0, st, a, round); break;
-        }
-    }
-    return hipGetLastError();
 }
 
 }  // namespace gp

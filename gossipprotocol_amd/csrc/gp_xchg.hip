@@ -69,7 +69,9 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
 __global__ __launch_bounds__(256) void k_unpack(UnpackArgs a, uint32_t round) {
     const int p = blockIdx.y;
     if (p == a.me || !a.peer[p].cnt) return;
-    const uint32_t n = min(*a.peer[p].cnt, a.peer[p].cap);
+    const uint32_t sent = *a.peer[p].cnt;
+    if (sent > a.peer[p].cap && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.overflow, 1u);
+    const uint32_t n = min(sent, a.peer[p].cap);
     for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < n; k += gridDim.x * 256) {
         const uint32_t slot = a.peer[p].slots[k];
         if (slot >= a.nedges) continue;  // never: slots are in-edge positions of this rank

@@ -34,6 +34,7 @@ struct UnpackArgs {
     uint32_t nedges;
     int W, me, push;
     XPeer peer[XMAXW];    // receive side
+    unsigned int* overflow;  // set when a sender packed more messages than the buffer holds
 };
 
 struct ZeroArgs {

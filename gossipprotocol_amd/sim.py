@@ -42,11 +42,14 @@ class Simulation:
 
     def __init__(self, num_nodes: int, topology: str, algorithm: str, seed: int = 1,
                  max_rounds: int = 0, device: int = 0, kernel_timing: bool = False,
-                 rank: int = 0, world: int = 1, dist=None, virtual_ranks: int = 1):
+                 rank: int = 0, world: int = 1, dist=None, virtual_ranks: int = 1, experimental: bool = False):
         """world > 1: this process is rank `rank` of a one-process-per-GPU run
         (RCCL; `dist` is a torch.distributed group used once to share the RCCL
         id).  virtual_ranks > 1: that many slabs in this process on `device`,
-        exchanging through device copies (the multi-GPU path on one GPU)."""
+        exchanging through device copies (the multi-GPU path on one GPU).
+        experimental: use the experiments build (kernel variants selected by
+        GP_* environment variables; tests and tools only)."""
+        self._L = L.lib(experimental)
         cfg = L.GpConfig()
         cfg.num_nodes = num_nodes
         cfg.topology = parse_topology(topology)
@@ -59,26 +62,29 @@ class Simulation:
             (L.GP_FLAG_VIRTUAL_RANKS if virtual_ranks > 1 else 0)
         self.topology, self.algorithm = topology, algorithm
         h = C.c_void_p()
-        if world > 1 or (world == 1 and dist is not None and os.environ.get("GP_FORCE_RCCL") == "1"):
+        if world > 1 or (world == 1 and dist is not None and experimental and os.environ.get("GP_FORCE_RCCL") == "1"):
             # one process per GPU: rank 0 makes the RCCL id, the caller's process
             # group (gloo is enough) broadcasts it, every rank joins its slab
             uid = C.create_string_buffer(128)
             if rank == 0:
-                L.check(L.lib().gp_get_unique_id(uid))
+                self._chk(self._L.gp_get_unique_id(uid))
             if dist is None:
                 raise ValueError("world > 1 needs a torch.distributed process group to share the RCCL id")
             box = [uid.raw if rank == 0 else None]
             dist.broadcast_object_list(box, src=0)
             uid = C.create_string_buffer(box[0], 128)
-            L.check(L.lib().gp_create_rank(C.byref(cfg), rank, world, uid, C.byref(h)))
+            self._chk(self._L.gp_create_rank(C.byref(cfg), rank, world, uid, C.byref(h)))
         else:
-            L.check(L.lib().gp_create(C.byref(cfg), C.byref(h)))
+            self._chk(self._L.gp_create(C.byref(cfg), C.byref(h)))
         self._h = h
+
+    def _chk(self, rc):
+        return L.check(rc, self._L)
 
     # -- lifecycle -------------------------------------------------------
     def close(self):
         if getattr(self, "_h", None):
-            L.lib().gp_destroy(self._h)
+            self._L.gp_destroy(self._h)
             self._h = None
 
     def __enter__(self):
@@ -94,22 +100,22 @@ class Simulation:
     def step(self, nrounds: int):
         """Run up to nrounds synchronous rounds; returns the per-round alert counts."""
         buf = (C.c_int64 * max(1, nrounds))()
-        n = L.check(L.lib().gp_step(self._h, nrounds, buf))
+        n = self._chk(self._L.gp_step(self._h, nrounds, buf))
         return [buf[i] for i in range(n)]
 
     def run(self) -> L.GpResult:
         """Run to convergence (or max_rounds): the reference's whole propagation."""
         res = L.GpResult()
-        L.check(L.lib().gp_run(self._h, C.byref(res)))
+        self._chk(self._L.gp_run(self._h, C.byref(res)))
         return res
 
     def sync(self):
-        L.check(L.lib().gp_sync(self._h))
+        self._chk(self._L.gp_sync(self._h))
 
     # -- inspection ------------------------------------------------------
     def info(self) -> L.GpInfo:
         out = L.GpInfo()
-        L.check(L.lib().gp_get_info(self._h, C.byref(out)))
+        self._chk(self._L.gp_get_info(self._h, C.byref(out)))
         return out
 
     @property
@@ -138,9 +144,9 @@ class Simulation:
         return self.info().alerts_total
 
     def neighbors(self, node: int):
-        deg = L.check(L.lib().gp_neighbors(self._h, node, None, 0))
+        deg = self._chk(self._L.gp_neighbors(self._h, node, None, 0))
         out = (C.c_int64 * max(1, deg))()
-        L.check(L.lib().gp_neighbors(self._h, node, out, deg))
+        self._chk(self._L.gp_neighbors(self._h, node, out, deg))
         return [out[k] for k in range(deg)]
 
     def state(self, first: int = 0, count: int | None = None):
@@ -149,18 +155,18 @@ class Simulation:
         s = np.zeros(count, np.float64)
         w = np.zeros(count, np.float64)
         f = np.zeros(count, np.uint8)
-        L.check(L.lib().gp_read_state(self._h, first, count, c.ctypes.data, s.ctypes.data,
+        self._chk(self._L.gp_read_state(self._h, first, count, c.ctypes.data, s.ctypes.data,
                                       w.ctypes.data, f.ctypes.data))
         return {"c": c, "s": s, "w": w, "flags": f}
 
     def kernel_stats(self, reset: bool = False):
         ms, n = C.c_double(), C.c_int64()
         name = C.create_string_buffer(128)
-        L.check(L.lib().gp_kernel_stats(self._h, C.byref(ms), C.byref(n), name, 128, int(reset)))
+        self._chk(self._L.gp_kernel_stats(self._h, C.byref(ms), C.byref(n), name, 128, int(reset)))
         return ms.value, n.value, name.value.decode()
 
     def alg_bytes_per_node(self) -> float:
-        return L.lib().gp_alg_bytes_per_node(self._h)
+        return self._L.gp_alg_bytes_per_node(self._h)
 
 
 def run(num_nodes: int, topology: str, algorithm: str, seed: int = 1, max_rounds: int = 0, device: int = 0):

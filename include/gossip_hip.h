@@ -28,7 +28,9 @@
 extern "C" {
 #endif
 
-#define GP_VERSION 10000 /* 1.0.0 */
+#define GP_VERSION 10100 /* 1.1.0 */
+/* Largest population (node ids are 32-bit; tiles of 1024 ids must not wrap). */
+#define GP_MAX_POPULATION 0xFFFFF000u
 
 /* topology strings "line" | "full" | "3D" | "Imp3D" (Program.fs:180,209,238,258) */
 enum { GP_LINE = 0, GP_FULL = 1, GP_3D = 2, GP_IMP3D = 3 };

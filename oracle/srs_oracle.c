@@ -78,7 +78,7 @@ int or_resolve(int64_t n, int topology, int64_t* P, int64_t* T, int64_t* g) {
     } else {
         return -1;
     }
-    if (*P > 0xFFFFFFF0ll) return -1; /* node ids are u32 */
+    if (*P > 0xFFFFF000ll) return -1; /* node ids are u32; same limit as GP_MAX_POPULATION */
     return 0;
 }
 
@@ -109,6 +109,9 @@ struct or_sim {
     uint32_t* bcount;   /* P+1 */
     uint32_t* bcursor;  /* P   */
     uint32_t* items;    /* P   */
+    /* full push-sum: (target << 32 | sender) keys and the radix sort's second buffer */
+    uint64_t* mkey2;
+    int64_t* rhist;     /* threads * 65536 digit counters */
 };
 
 static int nthreads(const or_sim* s) { return s->threads > 0 ? s->threads : 1; }
@@ -258,6 +261,11 @@ or_sim* or_create(int64_t num_nodes, int topology, int algorithm, uint64_t seed,
         s->items = (uint32_t*)malloc(sizeof(uint32_t) * P);
         ok &= s->s && s->w && s->s_msg && s->w_msg && s->active && s->conv && s->cnt &&
               s->mkey && s->bcount && s->bcursor && s->items;
+        if (topology == OR_FULL) {
+            s->mkey2 = (uint64_t*)malloc(sizeof(uint64_t) * P);
+            s->rhist = (int64_t*)malloc(sizeof(int64_t) * 65536 * (size_t)nt);
+            ok &= s->mkey2 && s->rhist;
+        }
     }
     if (!ok) { or_destroy(s); return NULL; }
 
@@ -303,6 +311,7 @@ void or_destroy(or_sim* s) {
     free(s->active); free(s->conv); free(s->cnt);
     free(s->rnd); free(s->tgt); free(s->mkey);
     free(s->bcount); free(s->bcursor); free(s->items);
+    free(s->mkey2); free(s->rhist);
     free(s);
 }
 
@@ -460,13 +469,107 @@ static int64_t pushsum_round(or_sim* s) {
     return alerts;
 }
 
+/* One stable LSD pass on the 16-bit digit at `shift` (parallel: every thread
+ * counts and then scatters its own contiguous slice, the per-(digit, thread)
+ * offsets keep slices in order, so equal digits keep their input order). */
+static void radix_pass(const uint64_t* in, uint64_t* out, int64_t n, int shift, int nt, int64_t* hist) {
+    #pragma omp parallel num_threads(nt)
+    {
+#ifdef _OPENMP
+        const int t = omp_get_thread_num();
+#else
+        const int t = 0;
+#endif
+        const int64_t a = n * t / nt, b = n * (t + 1) / nt;
+        int64_t* h = hist + (size_t)t * 65536;
+        memset(h, 0, sizeof(int64_t) * 65536);
+        for (int64_t i = a; i < b; ++i) h[(in[i] >> shift) & 0xFFFF] += 1;
+        #pragma omp barrier
+        #pragma omp single
+        {
+            int64_t run = 0;
+            for (int d = 0; d < 65536; ++d)
+                for (int q = 0; q < nt; ++q) {
+                    int64_t c = hist[(size_t)q * 65536 + d];
+                    hist[(size_t)q * 65536 + d] = run;
+                    run += c;
+                }
+        }
+        for (int64_t i = a; i < b; ++i) out[h[(in[i] >> shift) & 0xFFFF]++] = in[i];
+    }
+}
+
+/* Push-sum round on the full topology (SRS v1 B.4 with Program.fs:209-216's
+ * "every j != i"): same rules as pushsum_round, but the messages are grouped by
+ * receiver with a stable two-pass radix sort of (target << 32 | sender) keys --
+ * the keys are produced in ascending sender order, so every receiver's
+ * messages come out by ascending sender id (the canonical fold order) without
+ * per-bucket sorting.  Inactive senders carry target 0xFFFFFFFF and sort last. */
+static int64_t pushsum_round_full(or_sim* s) {
+    const int64_t P = s->P;
+    const uint32_t r = (uint32_t)s->round;
+    int nt = nthreads(s);
+    #pragma omp parallel for num_threads(nt) schedule(static)
+    for (int64_t i = 0; i < P; ++i) {
+        uint64_t t = NONE_U32;
+        if (s->active[i] && P > 1) {
+            uint32_t k = or_uniform(s->seed, OR_STREAM_PUSHSUM, (uint64_t)i, r, (uint32_t)(P - 1));
+            t = (int64_t)k < i ? k : (uint64_t)k + 1; /* Program.fs:213-215 */
+            s->s_msg[i] = s->s[i] * 0.5;
+            s->w_msg[i] = s->w[i] * 0.5;
+        }
+        s->mkey[i] = (t << 32) | (uint64_t)i;
+    }
+    radix_pass(s->mkey, s->mkey2, P, 32, nt, s->rhist);
+    radix_pass(s->mkey2, s->mkey, P, 48, nt, s->rhist);
+    uint32_t* head = s->bcount;
+    memset(head, 0xFF, sizeof(uint32_t) * P);
+    #pragma omp parallel for num_threads(nt) schedule(static)
+    for (int64_t p = 0; p < P; ++p) {
+        uint32_t t = (uint32_t)(s->mkey[p] >> 32);
+        if (t != NONE_U32 && (p == 0 || (uint32_t)(s->mkey[p - 1] >> 32) != t)) head[t] = (uint32_t)p;
+    }
+    int64_t alerts = 0;
+    #pragma omp parallel for num_threads(nt) schedule(static) reduction(+ : alerts)
+    for (int64_t j = 0; j < P; ++j) {
+        int halve = s->active[j] && P > 1;
+        double s0 = s->s[j], w0 = s->w[j];
+        double os = halve ? s0 * 0.5 : s0;
+        double ow = halve ? w0 * 0.5 : w0;
+        uint32_t b = head[j];
+        if (b == NONE_U32) {
+            s->s[j] = os; s->w[j] = ow;
+            continue;
+        }
+        double acc_s = os, acc_w = ow;
+        for (int64_t p = b; p < P && (uint32_t)(s->mkey[p] >> 32) == (uint32_t)j; ++p) {
+            uint32_t i = (uint32_t)s->mkey[p];
+            acc_s = acc_s + s->s_msg[i];
+            acc_w = acc_w + s->w_msg[i];
+        }
+        double r_old = s0 / w0;
+        double r_new = acc_s / acc_w;
+        if (!s->conv[j]) {
+            uint8_t cnt = s->cnt[j];
+            cnt = (fabs(r_new - r_old) > 1e-10) ? 0 : (uint8_t)(cnt + 1);
+            if (cnt == 3) { s->conv[j] = 1; alerts += 1; }
+            s->cnt[j] = cnt;
+        }
+        s->active[j] = 1;
+        s->s[j] = acc_s;
+        s->w[j] = acc_w;
+    }
+    return alerts;
+}
+
 /* ---------------------------------------------------------------- driver */
 /* scheduler (Program.fs:41-61): count Alerts, stop when counter = nodes. */
 int64_t or_step(or_sim* s, int64_t nrounds, int64_t* alerts_out) {
     int64_t done = 0;
     while (done < nrounds && !s->done) {
         if (s->max_rounds > 0 && s->round >= s->max_rounds) break;
-        int64_t a = (s->alg == OR_GOSSIP) ? gossip_round(s) : pushsum_round(s);
+        int64_t a = s->alg == OR_GOSSIP ? gossip_round(s)
+                    : s->topo == OR_FULL ? pushsum_round_full(s) : pushsum_round(s);
         if (alerts_out) alerts_out[done] = a;
         s->alerts_total += a;
         s->round += 1;

@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_version_and_parsers():
     lib = L.lib()
-    assert lib.gp_version() == 10000
+    assert lib.gp_version() == 10100
     assert [lib.gp_parse_topology(t) for t in (b"line", b"full", b"3D", b"Imp3D", b"imp3D")] == [0, 1, 2, 3, 3]
     assert lib.gp_parse_topology(b"3d") == -1  # case-sensitive like Program.fs:238
     assert b"unknown topology" in lib.gp_last_error()
@@ -83,3 +83,31 @@ def test_cli_invalid_option():
     assert r.returncode == 2 and r.stdout.strip() == "option invalid"
     r = subprocess.run([exe, "10", "ring", "gossip"], capture_output=True, text=True)
     assert r.returncode == 2 and "unknown topology" in r.stderr
+
+
+def test_population_cap_matches_oracle():
+    """GP_MAX_POPULATION (include/gossip_hip.h): the largest P both the product and
+    the oracle accept; one more is refused by both (tiles of 1024 ids never wrap)."""
+    from tests.oracle_ctypes import lib as olib
+    cap = 0xFFFFF000
+    assert resolve(cap - 1, "line")[0] == cap
+    with pytest.raises(L.GossipError):
+        resolve(cap, "line")
+    P, T, g = C.c_int64(), C.c_int64(), C.c_int64()
+    o = olib()
+    o.or_resolve.restype = C.c_int
+    o.or_resolve.argtypes = [C.c_int64, C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+    assert o.or_resolve(cap - 1, 0, C.byref(P), C.byref(T), C.byref(g)) == 0 and P.value == cap
+    assert o.or_resolve(cap, 0, C.byref(P), C.byref(T), C.byref(g)) == -1
+    assert resolve(1625**3, "Imp3D")[2] == 1625  # the largest lattice edge still fits
+
+
+def test_product_library_has_no_environment_switches():
+    """The product library reads no GP_* environment variable: kernel variants and
+    test overrides live only in the experiments build (-DGP_EXPERIMENTS)."""
+    prod = open(L.LIB_PATH, "rb").read()
+    exp = open(os.path.join(os.path.dirname(L.LIB_PATH), "libgossip_hip_exp.so"), "rb").read()
+    for knob in (b"GP_KERNEL", b"GP_GRID", b"GP_XSEGS", b"GP_WALK", b"GP_WX", b"GP_STAGE_CAP", b"GP_NO_PACK",
+                 b"GP_FORCE_RCCL", b"GP_XCAP"):
+        assert knob not in prod, knob
+        assert knob in exp, knob

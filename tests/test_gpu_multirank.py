@@ -41,15 +41,20 @@ CASES = [  # (num_nodes, topology, algorithm, seed, rounds, checkpoint, ranks)
 ]
 
 
-@pytest.mark.parametrize("kernel", ["tile", "tile2", "xtile", "wave", "col"])
+@pytest.mark.parametrize("kernel", ["default", "tile", "wave", "col"])
 @pytest.mark.parametrize("n,topo,alg,seed,rounds,chk,ranks", CASES, ids=lambda v: str(v))
 def test_virtual_ranks_parity(kernel, n, topo, alg, seed, rounds, chk, ranks, monkeypatch):
-    if kernel in ("col", "xtile") and topo == "line":
+    """default: the product library's own kernel choice; the others force a
+    variant through the experiments build (GP_KERNEL)."""
+    if kernel == "col" and topo == "line":
         pytest.skip("lattice kernel")
-    if topo == "full" and kernel != "tile":
+    if topo == "full" and kernel not in ("default", "tile"):
         pytest.skip("the full topology has one kernel set")
-    monkeypatch.setenv("GP_KERNEL", kernel)
-    sim, orc = Sim(n, topo, alg, seed=seed, virtual_ranks=ranks), Oracle(n, topo, alg, seed)
+    exp = kernel != "default"
+    if exp:
+        monkeypatch.setenv("GP_KERNEL", kernel)
+    sim = Sim(n, topo, alg, seed=seed, virtual_ranks=ranks, experimental=exp)
+    orc = Oracle(n, topo, alg, seed)
     assert sim.info().num_gpus == ranks
     done = 0
     while done < rounds:
@@ -77,3 +82,19 @@ def test_virtual_ranks_converge_like_single(topo):
             ref = key
         assert key == ref, f"{ranks} ranks differ from 1 rank"
         sim.close()
+
+
+@pytest.mark.parametrize("topo,alg", [("Imp3D", "push-sum"), ("Imp3D", "gossip"), ("full", "push-sum"),
+                                      ("full", "gossip")])
+def test_exchange_overflow_fails_every_rank(topo, alg, monkeypatch):
+    """An exchange buffer that overflows invalidates the round on every rank: the
+    flag is summed over ranks with the round's bookkeeping, so gp_step fails with
+    GP_ESTATE (never silently truncated messages).  GP_XCAP (experiments build)
+    caps every per-pair buffer at a few entries to force it."""
+    from gossipprotocol_amd._lib import GossipError
+    monkeypatch.setenv("GP_XCAP", "2")
+    sim = Sim(64000, topo, alg, seed=5, virtual_ranks=3, experimental=True)
+    with pytest.raises(GossipError) as e:
+        sim.step(200)
+    assert e.value.code == -5 and "overflow" in str(e.value)
+    sim.close()

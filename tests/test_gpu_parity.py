@@ -172,14 +172,15 @@ KERNEL_CASES = [  # (num_nodes, topology, algorithm, seed, rounds, checkpoint, x
 ]
 
 
-@pytest.mark.parametrize("kernel", ["wave", "col", "tile", "tile2", "xtile"])
+@pytest.mark.parametrize("kernel", ["wave", "col", "tile"])
 @pytest.mark.parametrize("n,topo,alg,seed,rounds,chk,xsegs", KERNEL_CASES, ids=lambda v: str(v))
 def test_kernel_variant_parity(kernel, n, topo, alg, seed, rounds, chk, xsegs, monkeypatch):
-    """Every round-kernel variant (chunk / column march / tiled) bit-exact vs the oracle,
-    the column march also with its x-segmentation forced."""
+    """Every round-kernel variant (chunk / column march / tiled; experiments build,
+    GP_KERNEL) bit-exact vs the oracle, the column march also with its
+    x-segmentation forced."""
     monkeypatch.setenv("GP_KERNEL", kernel)
     monkeypatch.setenv("GP_XSEGS", xsegs)
-    sim, orc = Sim(n, topo, alg, seed=seed), Oracle(n, topo, alg, seed)
+    sim, orc = Sim(n, topo, alg, seed=seed, experimental=True), Oracle(n, topo, alg, seed)
     done = 0
     while done < rounds:
         k = min(chk, rounds - done)
@@ -198,25 +199,20 @@ WALK_CASES = [  # (num_nodes, topology, seed, rounds, checkpoint)
 ]
 
 
-@pytest.mark.parametrize("ltag", ["0", "1"])
-@pytest.mark.parametrize("edges", ["0", "1"])
 @pytest.mark.parametrize("pack", ["0", "1"])
 @pytest.mark.parametrize("walk", ["0", "1", "2"])
 @pytest.mark.parametrize("n,topo,seed,rounds,chk", WALK_CASES, ids=lambda v: str(v))
-def test_tile_walk_and_sender_packing_parity(n, topo, seed, rounds, chk, walk, pack, edges, ltag, monkeypatch):
+def test_tile_walk_and_sender_packing_parity(n, topo, seed, rounds, chk, walk, pack, monkeypatch):
     """Push-sum tile kernel bit-exact vs the oracle for every tile walk (XCD eighths,
     global sweep, x-windows of 3 planes), with the senders' degree packed into the
-    staged ids or computed (the P > 2^30 path), with the separate in-edge pass, and
-    with the in-edge pass reading the senders' edge tags or redrawing their Philox."""
-    if topo != "Imp3D" and (pack == "1" or edges == "1" or ltag == "0"):
-        pytest.skip("sender packing / edge pass / edge tags are Imp3D only")
-    monkeypatch.setenv("GP_LTAG", ltag)
+    staged ids or computed (the P > 2^30 path); experiments build."""
+    if topo != "Imp3D" and pack == "0":
+        pytest.skip("sender packing is Imp3D only")
     monkeypatch.setenv("GP_KERNEL", "tile")
     monkeypatch.setenv("GP_WALK", walk)
     monkeypatch.setenv("GP_WX", "3")
     monkeypatch.setenv("GP_NO_PACK", "0" if pack == "1" else "1")
-    monkeypatch.setenv("GP_EDGES", edges)
-    sim, orc = Sim(n, topo, "push-sum", seed=seed), Oracle(n, topo, "push-sum", seed)
+    sim, orc = Sim(n, topo, "push-sum", seed=seed, experimental=True), Oracle(n, topo, "push-sum", seed)
     done = 0
     while done < rounds:
         k = min(chk, rounds - done)
@@ -237,7 +233,7 @@ def test_seed_random_edge_round0(kernel, monkeypatch):
     the seed's bit (lost about one time in four)."""
     monkeypatch.setenv("GP_KERNEL", kernel)
     for seed in range(1, 25):
-        sim, orc = Sim(27000, "Imp3D", "gossip", seed=seed), Oracle(27000, "Imp3D", "gossip", seed)
+        sim, orc = Sim(27000, "Imp3D", "gossip", seed=seed, experimental=True), Oracle(27000, "Imp3D", "gossip", seed)
         assert sim.step(12) == orc.step(12), f"seed {seed}: alerts differ"
         assert np.array_equal(sim.state()["c"], orc.state()["c"]), f"seed {seed}: counters differ"
         sim.close()
@@ -253,7 +249,7 @@ def test_tile_unstaged_path_parity(cap, monkeypatch):
     monkeypatch.setenv("GP_KERNEL", "tile")
     monkeypatch.setenv("GP_STAGE_CAP", cap)
     n, seed, rounds, chk = 512000, 4, 90, 45
-    sim, orc = Sim(n, "Imp3D", "push-sum", seed=seed), Oracle(n, "Imp3D", "push-sum", seed)
+    sim, orc = Sim(n, "Imp3D", "push-sum", seed=seed, experimental=True), Oracle(n, "Imp3D", "push-sum", seed)
     done = 0
     while done < rounds:
         k = min(chk, rounds - done)

@@ -1,5 +1,5 @@
 """GPU: the RCCL transport on the one GPU a test box has -- a one-rank RCCL
-communicator (GP_FORCE_RCCL=1) runs the split bookkeeping (pre / all-reduce /
+communicator (GP_FORCE_RCCL=1, experiments build) runs the split bookkeeping (pre / all-reduce /
 post) and must match the single-rank path bit for bit.  Multi-rank RCCL runs
 are the driver's multi-GPU bench (bench.py under torch.distributed.run)."""
 import os
@@ -20,7 +20,7 @@ def test_one_rank_rccl_matches_single(topo, alg, n, monkeypatch):
     if not dist.is_initialized():
         dist.init_process_group("gloo", rank=0, world_size=1)
     monkeypatch.setenv("GP_FORCE_RCCL", "1")
-    a = Simulation(n, topo, alg, seed=4, rank=0, world=1, dist=dist)
+    a = Simulation(n, topo, alg, seed=4, rank=0, world=1, dist=dist, experimental=True)
     monkeypatch.delenv("GP_FORCE_RCCL")
     b = Simulation(n, topo, alg, seed=4)
     assert a.step(400) == b.step(400)

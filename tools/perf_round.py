@@ -20,7 +20,9 @@ def main():
     alg = sys.argv[3] if len(sys.argv) > 3 else "push-sum"
     k = int(sys.argv[4]) if len(sys.argv) > 4 else 10
     t = time.perf_counter()
-    s = Simulation(n, topo, alg, kernel_timing=True)
+    # the experiments build (GP_* overrides, ablation builds) when asked for
+    exp = bool(os.environ.get("GOSSIP_HIP_LIB_EXPERIMENT") or os.environ.get("GP_EXP"))
+    s = Simulation(n, topo, alg, kernel_timing=True, experimental=exp)
     tc = time.perf_counter() - t
     P = s.population
     s.kernel_stats(reset=True)
