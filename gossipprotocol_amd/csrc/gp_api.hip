@@ -779,6 +779,7 @@ int launch_round(gp_sim* s, uint32_t r, hipEvent_t e0, hipEvent_t e1) {
     }
     int rc;
     if ((rc = exchange(s, r + 1))) return rc;
+    if (s->slab[0].S.fuse_finalize) return GP_OK;  // the round kernel closed its own round
     return finalize(s, r, r + 1);
 }
 
@@ -806,7 +807,7 @@ void choose_kernel(gp_sim* s, int64_t nloc_max, int& kernel, uint32_t& col_xsegs
     (void)hipGetDeviceProperties(&prop, s->device);
     const gp_config* cfg = &s->cfg;
     const int64_t g = s->g;
-    const int64_t blocks = (nloc_max + BULK_THREADS - 1) / BULK_THREADS;
+    int64_t blocks = (nloc_max + BULK_THREADS - 1) / BULK_THREADS;
     // 64 workgroups per CU: measured best for the tiled round kernels (tools/ablate.py:
     // 2048 -> 27.5, 8192 -> 22.1, 16384 -> 21.2 ms/round at P = 1e9)
     int64_t cap = (int64_t)prop.multiProcessorCount * 64;
@@ -840,6 +841,8 @@ void choose_kernel(gp_sim* s, int64_t nloc_max, int& kernel, uint32_t& col_xsegs
             col_xsegs = (uint32_t)xs;
         }
     }
+    if (kernel == KERNEL_TILE)  // 1024-node tiles (+1: a slab may start mid-tile), a multiple of the 8 XCDs
+        blocks = ((nloc_max + 1023) / 1024 + 1 + 7) / 8 * 8;
 #ifdef GP_EXPERIMENTS
     if (const char* e = std::getenv("GP_GRID")) cap = std::max<int64_t>(1, std::atoll(e));
     if (const char* e = std::getenv("GP_XSEGS")) col_xsegs = (uint32_t)std::max(1, std::atoi(e));
@@ -877,6 +880,10 @@ int build_sim(gp_sim* s) {
         sl.S.tile_walk = walk;
         sl.S.tile_wx = wx;
         sl.S.tile_stage_cap = 0xFFFFFFFFu;
+        // single-rank lattice push-sum: the round kernel's last block closes the
+        // round (no injector, nothing to exchange), saving a k_finalize launch per round
+        sl.S.fuse_finalize = (s->mode == MODE_SINGLE && s->cfg.algorithm == GP_PUSHSUM &&
+                              s->cfg.topology != GP_FULL && kernel == KERNEL_TILE) ? 1u : 0u;
 #ifdef GP_EXPERIMENTS
         if (const char* e = std::getenv("GP_STAGE_CAP")) sl.S.tile_stage_cap = (uint32_t)std::max(0, std::atoi(e));
 #endif
@@ -1097,6 +1104,12 @@ int64_t gp_step(gp_sim* s, int64_t nrounds, int64_t* alerts_out) {
         HIP_TRY(hipMemcpyAsync(s->host_ctl, s->slab[0].S.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, s->stream));
         HIP_TRY(hipStreamSynchronize(s->stream));
         const Ctl& hc = *s->host_ctl;
+        if (hc.tiny) {
+            set_err("a push-sum (s, w) value fell below 2^-1020, where the tile kernel's fused fold "
+                    "(v_fma_f64(m, 0.5, acc)) is no longer guaranteed to round like the specification's "
+                    "acc + m * 0.5; the rounds of this batch are invalid");
+            return GP_ESTATE;
+        }
         if (hc.overflow) {
             set_err("random-edge exchange buffer overflow (capacity = expected + 12 sigma was exceeded); "
                     "the rounds of this batch are invalid");

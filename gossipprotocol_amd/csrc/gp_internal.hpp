@@ -29,9 +29,51 @@ struct Ctl {
     unsigned long long xchg[4];       // multi-rank: {alerts, newly active, injector pick converged, 0}, summed over ranks
     long long inj_pick;               // multi-rank: the injector's pick for the next round (-1 none)
     unsigned int overflow;            // multi-rank: a random-edge exchange buffer overflowed (run is invalid)
+    unsigned int blocks_done;         // fused finalize: blocks of the current round kernel that have finished
+    unsigned int tiny;                // push-sum: some (s, w) fell below 2^-1020 (the FMA fold's exactness bound)
     unsigned int pad_;
     unsigned long long hist[HIST];    // alerts of round r at hist[r % HIST]
 };
+
+// Scheduler bookkeeping of round `round_done` from its global counts a (alerts)
+// and na (newly active) (Program.fs:51-56); returns 1 when the run is over.
+// One thread (the finalize kernel's, or the last block of a round kernel that
+// closes its own round).
+__device__ inline int close_round_ctl(Ctl* ctl, uint32_t P, uint32_t T, uint32_t round_done, unsigned long long a,
+                                      unsigned long long na) {
+    const unsigned long long tot =
+        __hip_atomic_load(&ctl->alerts_total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + a;
+    __hip_atomic_store(&ctl->alerts_total, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ctl->hist[round_done % HIST] = a;
+    const unsigned long long act =
+        __hip_atomic_load(&ctl->active_total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + na;
+    __hip_atomic_store(&ctl->active_total, act, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (act >= P) __hip_atomic_store(&ctl->all_active, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tot >= T) {
+        __hip_atomic_store(&ctl->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return 1;
+    }
+    return 0;
+}
+
+// Round kernels that close their own round (single rank, no injector): every
+// block counts itself out after its alert atomics; the last one moves the
+// round's counts into the bookkeeping (replaces a k_finalize launch).  Thread 0
+// of each block, after the block's round_alerts / round_active atomics.
+__device__ inline void block_done_close(Ctl* ctl, uint32_t P, uint32_t T, uint32_t round) {
+    // No fences (a release fence at agent scope writes back the XCD's L2): the
+    // block's round_* updates are atomics performed at the device coherence point,
+    // and the caller waits for their results before arriving here (see k_ps_tile),
+    // so they are complete before this arrival; the last block reads them with
+    // atomics too.  Everything else it writes reaches the next round's kernel
+    // through the kernel boundary.
+    const unsigned int prev = __hip_atomic_fetch_add(&ctl->blocks_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev != gridDim.x - 1) return;
+    __hip_atomic_store(&ctl->blocks_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long a = __hip_atomic_exchange(&ctl->round_alerts, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long na = __hip_atomic_exchange(&ctl->round_active, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    close_round_ctl(ctl, P, T, round, a, na);
+}
 
 // Node state in HBM (structure of arrays, single GPU / one slab).
 struct DevState {
@@ -81,6 +123,7 @@ struct DevState {
     uint32_t tile_walk;  // RoundArgs::walk
     uint32_t tile_wx;    // RoundArgs::wx
     uint32_t tile_stage_cap;  // RoundArgs::stage_cap (experiments build only; default: no limit)
+    uint32_t fuse_finalize;   // the round kernel closes its own round (single rank push-sum)
 };
 
 // Arguments of the tiled round kernels (gp_round.hip): only what they read.
@@ -104,6 +147,7 @@ struct RoundArgs {
     uint32_t walk;  // 0: XCD-contiguous eighths, 1: one global sweep (tile t -> block t % grid), 2: x-windows
     uint32_t wx;    // walk 2: planes per x-window
     uint32_t stage_cap;  // k_ps_tile: tiles with more in-edges take the unstaged path (tests force it)
+    uint32_t fuse;       // k_ps_tile: the last block closes the round (no k_finalize launch)
 };
 
 enum KernelVariant : int { KERNEL_WAVE = 0, KERNEL_TILE = 1, KERNEL_COL = 2 };

@@ -338,18 +338,7 @@ __device__ void inj_remove(const DevState& S, long long id, uint32_t live) {
 // Scheduler bookkeeping of round `round_done` from this round's global counts
 // (Program.fs:51-56); returns 1 when the run is over.  One thread.
 __device__ int close_round(const DevState& S, uint32_t round_done, unsigned long long a, unsigned long long na) {
-    Ctl* ctl = S.ctl;
-    const unsigned long long tot = ld_agent(&ctl->alerts_total) + a;
-    st_agent(&ctl->alerts_total, tot);
-    ctl->hist[round_done % HIST] = a;
-    const unsigned long long act = ld_agent(&ctl->active_total) + na;
-    st_agent(&ctl->active_total, act);
-    if (act >= S.G.P) st_agent(&ctl->all_active, 1u);
-    if (tot >= S.G.T) {
-        st_agent(&ctl->done, 1u);
-        return 1;
-    }
-    return 0;
+    return close_round_ctl(S.ctl, S.G.P, S.G.T, round_done, a, na);
 }
 
 // Single rank: closes round `round_done` (if has_done) and prepares round
@@ -394,7 +383,7 @@ __global__ __launch_bounds__(FIN_THREADS) void k_finalize_pre(DevState S, uint32
         ctl->xchg[2] = 0ull;
         // an exchange buffer of this rank overflowed (send or receive side): summed
         // over ranks, so every rank fails the batch (gp_step), not only the sender
-        ctl->xchg[3] = ld_agent(&ctl->overflow) ? 1ull : 0ull;
+        ctl->xchg[3] = (ld_agent(&ctl->overflow) ? 1ull : 0ull) + (ld_agent(&ctl->tiny) ? 65536ull : 0ull);
         ctl->inj_pick = -1;
     }
     if (skip || !injector) return;
@@ -412,7 +401,8 @@ __global__ __launch_bounds__(FIN_THREADS) void k_finalize_pre(DevState S, uint32
 __global__ void k_finalize_post(DevState S, uint32_t round_done, int has_done, int injector) {
     Ctl* ctl = S.ctl;
     if (threadIdx.x != 0) return;
-    if (ctl->xchg[3]) ctl->overflow = 1u;  // some rank's exchange overflowed: this run is invalid
+    if (ctl->xchg[3] & 0xFFFFull) ctl->overflow = 1u;  // some rank's exchange overflowed: this run is invalid
+    if (ctl->xchg[3] >> 16) ctl->tiny = 1u;            // some rank saw a value below the FMA fold's bound
     if (ld_agent(&ctl->done)) return;
     if (has_done && close_round(S, round_done, ctl->xchg[0], ctl->xchg[1])) return;
     long long target = -1;

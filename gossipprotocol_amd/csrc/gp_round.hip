@@ -46,7 +46,16 @@ namespace gp {
 #define GP_BATCH_DIR 1   // next-round direction draws of a thread as one interleaved batch
 #endif
 #ifndef GP_PF_SRC
-#define GP_PF_SRC 1      // the next tile's senders loaded during this tile
+#define GP_PF_SRC 0      // the next tile's senders loaded during this tile (measured slower: 14.9 vs 14.4 ms)
+#endif
+#ifndef GP_FMA_FOLD
+#define GP_FMA_FOLD 1    // fold as fma(m, 0.5, acc) (exact for |m| >= 2^-1021, guarded)
+#endif
+#ifndef GP_NGROUP
+#define GP_NGROUP 1      // nodes per thread whose lattice gathers are issued together
+#endif
+#ifndef GP_STAMPS
+#define GP_STAMPS 0      // diagnostics (experiments build): per-phase cycle counts of the push-sum tile kernel
 #endif
 #ifndef GP_MINB
 #define GP_MINB 5  // __launch_bounds__ minimum waves per SIMD (= resident 256-thread blocks per CU):
@@ -149,6 +158,15 @@ template <typename T>
 __device__ __forceinline__ T ld_agent(const T* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+
+#if GP_STAMPS
+// Phase cycle counters (block 0's wave 0 lane 0 of every block sums its own
+// tiles); read by gp_debug_stamps (experiments build only).
+__device__ unsigned long long gp_stamp_acc[8];
+#define GP_STAMP(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#else
+#define GP_STAMP(v)
+#endif
 
 // Tile walks (speed only -- any placement is correct; every tile of the slab
 // is visited exactly once).  Blocks with equal blockIdx % 8 share an XCD.
@@ -291,6 +309,7 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
     constexpr int FU = SLOT_FU;
     const uint32_t cap = min((uint32_t)SLOTS, a.stage_cap);
     uint32_t alerts = 0, newly = 0;
+    bool tiny = false;
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
 
     // loaded one tile ahead: the next tile's in-edge range (two uniform loads)
@@ -299,9 +318,13 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
     uint32_t raw[FU];
 #pragma unroll
     for (int m = 0; m < FU; ++m) raw[m] = 0u;
+#if GP_STAMPS
+    uint64_t ph[7] = {0, 0, 0, 0, 0, 0, 0};
+#endif
     for (TileWalk tw(a); tw.t < tw.end; tw.t += tw.step) {
         uint32_t ti;
         if (!tw.tile(ti)) continue;
+        GP_STAMP(t0);
         // tiles sit on global multiples of TILE (4-aligned word I/O, 64-aligned
         // ballot words); the slab's first and last tile may be partial
         const uint32_t T = (a.lo / TILE + ti) * TILE;
@@ -398,6 +421,7 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                 if (threadIdx.x == 0) L.bits[FU * (TPB / 64)] = 0ull;
             }
         }
+        GP_STAMP(t1);
         // own (s, w): consumed after staging
         double2 own[NPT];
 #pragma unroll
@@ -414,7 +438,9 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
         }
         int o_off = 0;  // L.off[jl + o_off] = in_off[T + jl]
         if (TOPO == IMP3D) o_off = (int)dma_stage_words(L.off, a.in_off, j0, j1 + 1) - (int)(j0 - T);
+        GP_STAMP(t2);
         __syncthreads();  // staging copies, in-edge bitmap and gathered messages retired
+        GP_STAMP(t3);
 
         // per node, 16 bits (two nodes per word): bits 0-5 lattice mask, bit 6 draw a
         // next-round direction, bits 7-10 the node byte's flag bits 3-6
@@ -431,48 +457,42 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                 cy = fastdiv(rem, G.div_g);
                 cz = rem - cy * G.g;
             }
+            constexpr uint32_t ND = TOPO == LINE ? 2 : 6;
+            constexpr int NG = GP_NGROUP;  // nodes whose lattice gathers are in flight together
+            static_assert(NPT % NG == 0, "node groups");
 #pragma unroll
-            for (int k = 0; k < NPT; ++k) {
-                const uint32_t jl = k * TPB + threadIdx.x;
-                const uint32_t j = T + jl;
-                const bool valid = j >= j0 && j < j1;
-                uint32_t dir = DIR_NONE;
-                if (TOPO != LINE && k > 0) {
-                    cz += TPB;
-                    if (cz >= G.g) {
-                        const uint32_t q = fastdiv(cz, G.div_g);
-                        cz -= q * G.g;
-                        cy += q;
-                        if (cy >= G.g) {
-                            const uint32_t q2 = fastdiv(cy, G.div_g);
-                            cy -= q2 * G.g;
-                            cx += q2;
+            for (int k0 = 0; k0 < NPT; k0 += NG) {
+                // phase A: node byte, present mask, lattice senders (from the staged
+                // direction bytes), one gather per direction -- a direction without a
+                // sender reads the zero sentinel swc[ext_hi] (adding +0.0 is exact)
+                uint32_t gb[NG], gmask[NG], gfrom[NG];
+                double2 m[NG][ND];
+#pragma unroll
+                for (int h = 0; h < NG; ++h) {
+                    const int k = k0 + h;
+                    const uint32_t j = T + k * TPB + threadIdx.x;
+                    if (TOPO != LINE && k > 0) {
+                        cz += TPB;
+                        if (cz >= G.g) {
+                            const uint32_t q = fastdiv(cz, G.div_g);
+                            cz -= q * G.g;
+                            cy += q;
+                            if (cy >= G.g) {
+                                const uint32_t q2 = fastdiv(cy, G.div_g);
+                                cy -= q2 * G.g;
+                                cx += q2;
+                            }
                         }
                     }
-                }
-                if (valid) {
                     const uint32_t jr = j - b_rows;
-                    const uint32_t b = lds_byte(L.rows, jr);
+                    gb[h] = lds_byte(L.rows, jr);
                     const uint32_t mask = TOPO == LINE ? present_mask<TOPO>(j, G) : mask_xyz(cx, cy, cz, G.g - 1u);
-                    const uint32_t deg = popc6(mask) + (TOPO == IMP3D ? 1u : 0u);
-                    bool active = (b & B_ACTIVE) != 0;
-                    const double2 sv = own[k];
-                    const bool halve = active && deg > 0;
-                    // canonical fold: own half, lattice slots in slot order, random edges by
-                    // ascending sender; every message contributes the sender's half
-                    double acc_s = halve ? sv.x * 0.5 : sv.x;
-                    double acc_w = halve ? sv.y * 0.5 : sv.y;
-                    auto fold = [&](const double2 mi) {
-                        acc_s = acc_s + mi.x * 0.5;
-                        acc_w = acc_w + mi.y * 0.5;
-                    };
-                    // lattice senders from the staged direction bytes (absent neighbours read
-                    // a harmless in-range byte and are masked out)
                     uint32_t from = 0;
                     if (TOPO == LINE) {
                         from |= ((mask & 1u) && (lds_byte(L.rows, (mask & 1u) ? jr - 1 : jr) & DIR_MASK) == 1u) ? 1u : 0u;
                         from |= ((mask & 2u) && (lds_byte(L.rows, (mask & 2u) ? jr + 1 : jr) & DIR_MASK) == 0u) ? 2u : 0u;
                     } else {
+                        // absent neighbours read a harmless in-range byte and are masked out
                         const uint32_t bxm = lds_byte(L.xm, (mask & 1u) ? j - G.g2 - b_xm : 0u);
                         const uint32_t bxp = lds_byte(L.xp, (mask & 2u) ? j + G.g2 - b_xp : 0u);
                         const uint32_t byp = lds_byte(L.rows, (mask & 4u) ? jr + G.g : jr);
@@ -484,93 +504,129 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                                ((bzp & DIR_MASK) == 5u ? 16u : 0u) | ((bzm & DIR_MASK) == 4u ? 32u : 0u);
                         from &= mask;
                     }
-                    // one gather per direction, all in flight together; a direction without a
-                    // sender reads the zero sentinel swc[ext_hi] (adding +0.0 is exact)
-                    constexpr uint32_t ND = TOPO == LINE ? 2 : 6;
-                    double2 m[ND];
+                    if (!(j >= j0 && j < j1)) from = 0u;
+                    gmask[h] = mask;
+                    gfrom[h] = from;
 #pragma unroll
-                    for (uint32_t d = 0; d < ND; ++d) m[d] = ld_sw(swc + ((from >> d) & 1u ? nbr<TOPO>(j, d, G) : a.ext_hi));
-                    bool recv = from != 0;
-#pragma unroll
-                    for (uint32_t d = 0; d < ND; ++d) fold(m[d]);
-                    if (TOPO == IMP3D) {
-                        const uint32_t e_b = L.off[jl + o_off], e_e = L.off[jl + 1 + o_off];
-                        if (staged) {
-                            // the node's used in-edges: its window of the tile bitmap, 32 bits at a
-                            // time (funnel shift of two LDS words), walked set bit by set bit
-                            // (ascending sender = canonical order); edge q's message is at slot q
-                            const uint32_t* bw = reinterpret_cast<const uint32_t*>(L.bits);
-                            const uint32_t qe = e_e - e_lo;
-                            for (uint32_t q0 = e_b - e_lo; q0 < qe; q0 += 32u) {
-                                uint32_t win = __builtin_amdgcn_alignbit(bw[(q0 >> 5) + 1], bw[q0 >> 5], q0 & 31u);
-                                if (qe - q0 < 32u) win &= (1u << (qe - q0)) - 1u;
-                                while (win) {
-                                    const uint32_t q = q0 + (uint32_t)__builtin_ctz(win);
-                                    win &= win - 1u;
-                                    fold(L.msg[q]);
-                                    recv = true;
-                                }
-                            }
-                        } else {  // rare: tile in-degree above SLOTS
-                            for (uint32_t e = e_b; e < e_e; ++e) {
-                                const uint32_t i = in_src[e];
-                                bool sent;
-                                double2 mi = make_double2(0.0, 0.0);
-                                if (REMOTE && i - a.lo >= a.nloc) {
-                                    sent = a.rtag[e] == r;
-                                    if (sent) mi = a.rmsg[e];
-                                } else {
-                                    if (all_active) {
-                                        const uint32_t di = popc6(present_mask<IMP3D>(i, G)) + 1u;
-                                        sent = uniform(a.k0, a.k1, S_PUSHSUM, i, r, di) == di - 1u;
-                                    } else {
-                                        sent = (rbc[(i >> 6) - (a.lo >> 6)] >> (i & 63)) & 1ull;
-                                    }
-                                    if (sent) mi = ld_sw(swc + i);
-                                }
-                                if (sent) {
-                                    fold(mi);
-                                    recv = true;
-                                }
-                            }
-                        }
-                    }
-                    uint32_t flags = b & (B_ACTIVE | B_CONV | (3u << CNT_SHIFT));
-                    if (recv) {
-                        if (!(b & B_CONV)) {
-                            const double r_old = sv.x / sv.y;
-                            const double r_new = acc_s / acc_w;
-                            uint32_t cnt3 = (b >> CNT_SHIFT) & 3u;
-                            cnt3 = fabs(r_new - r_old) > 1e-10 ? 0u : cnt3 + 1u;
-                            flags = (flags & ~(3u << CNT_SHIFT)) | (cnt3 << CNT_SHIFT);
-                            if (cnt3 == 3) {
-                                flags |= B_CONV;
-                                ++alerts;
-                            }
-                        }
-                        if (!active) {
-                            ++newly;
-                            flags |= B_ACTIVE;
-                            active = true;
-                        }
-                    }
-                    if (GP_BATCH_DIR) {
-                        pend[k >> 1] |= (mask | (active && deg > 0 ? 64u : 0u) | ((flags >> 3) << 7)) << (16 * (k & 1));
-                    } else {
-                        if (active && deg > 0) dir = slot_to_dir_fast(mask, uniform(a.k0, a.k1, S_PUSHSUM, j, r + 1, deg));
-                        reinterpret_cast<uint8_t*>(L.out)[jl] = (uint8_t)(flags | dir);
-                    }
-                    st_stream(swn + j, make_double2(acc_s, acc_w));
+                    for (uint32_t d = 0; d < ND; ++d)
+                        m[h][d] = ld_sw(swc + ((from >> d) & 1u ? nbr<TOPO>(j, d, G) : a.ext_hi));
                 }
-                if (TOPO == IMP3D && !GP_BATCH_DIR) {
-                    const unsigned long long bits = __ballot(valid && dir == DIR_RANDOM);
-                    if (lane == 0) {
-                        const int64_t wi = (int64_t)((T + k * TPB + (threadIdx.x & ~63u)) >> 6) - (int64_t)(a.lo >> 6);
-                        if (wi >= 0) a.rbn[wi] = bits;
+                // phase B: canonical fold (own half, lattice slots in slot order, random
+                // edges by ascending sender; every message contributes the sender's half),
+                // ratio test, next-round state
+#pragma unroll
+                for (int h = 0; h < NG; ++h) {
+                    const int k = k0 + h;
+                    const uint32_t jl = k * TPB + threadIdx.x;
+                    const uint32_t j = T + jl;
+                    const bool valid = j >= j0 && j < j1;
+                    uint32_t dir = DIR_NONE;
+                    if (valid) {
+                        const uint32_t b = gb[h], mask = gmask[h], from = gfrom[h];
+                        const uint32_t deg = popc6(mask) + (TOPO == IMP3D ? 1u : 0u);
+                        bool active = (b & B_ACTIVE) != 0;
+                        const double2 sv = own[k];
+                        const bool halve = active && deg > 0;
+                        double acc_s = halve ? sv.x * 0.5 : sv.x;
+                        double acc_w = halve ? sv.y * 0.5 : sv.y;
+                        // fused: fma(m, 0.5, acc) rounds once, exactly like the specification's
+                        // acc + m * 0.5 whenever m * 0.5 is exact, i.e. |m| >= 2^-1021; every
+                        // node checks its own round-start (s, w) -- the values its messages
+                        // carry this round -- against 2^-1020 (Ctl::tiny, gp_step fails)
+                        auto fold = [&](const double2 mi) {
+#if GP_FMA_FOLD
+                            acc_s = __builtin_fma(mi.x, 0.5, acc_s);
+                            acc_w = __builtin_fma(mi.y, 0.5, acc_w);
+#else
+                            acc_s = acc_s + mi.x * 0.5;
+                            acc_w = acc_w + mi.y * 0.5;
+#endif
+                        };
+                        tiny |= (sv.y < 0x1p-1020) | (sv.x != 0.0 && sv.x < 0x1p-1020);
+                        bool recv = from != 0;
+#pragma unroll
+                        for (uint32_t d = 0; d < ND; ++d) fold(m[h][d]);
+                        if (TOPO == IMP3D) {
+                            const uint32_t e_b = L.off[jl + o_off], e_e = L.off[jl + 1 + o_off];
+                            if (staged) {
+                                // the node's used in-edges: its window of the tile bitmap, 32 bits
+                                // at a time (funnel shift of two LDS words), walked set bit by set
+                                // bit (ascending sender = canonical order); edge q's message is at
+                                // slot q
+                                const uint32_t* bw = reinterpret_cast<const uint32_t*>(L.bits);
+                                const uint32_t qe = e_e - e_lo;
+                                for (uint32_t q0 = e_b - e_lo; q0 < qe; q0 += 32u) {
+                                    uint32_t win = __builtin_amdgcn_alignbit(bw[(q0 >> 5) + 1], bw[q0 >> 5], q0 & 31u);
+                                    if (qe - q0 < 32u) win &= (1u << (qe - q0)) - 1u;
+                                    while (win) {
+                                        const uint32_t q = q0 + (uint32_t)__builtin_ctz(win);
+                                        win &= win - 1u;
+                                        fold(L.msg[q]);
+                                        recv = true;
+                                    }
+                                }
+                            } else {  // rare: tile in-degree above SLOTS
+                                for (uint32_t e = e_b; e < e_e; ++e) {
+                                    const uint32_t i = in_src[e];
+                                    bool sent;
+                                    double2 mi = make_double2(0.0, 0.0);
+                                    if (REMOTE && i - a.lo >= a.nloc) {
+                                        sent = a.rtag[e] == r;
+                                        if (sent) mi = a.rmsg[e];
+                                    } else {
+                                        if (all_active) {
+                                            const uint32_t di = popc6(present_mask<IMP3D>(i, G)) + 1u;
+                                            sent = uniform(a.k0, a.k1, S_PUSHSUM, i, r, di) == di - 1u;
+                                        } else {
+                                            sent = (rbc[(i >> 6) - (a.lo >> 6)] >> (i & 63)) & 1ull;
+                                        }
+                                        if (sent) mi = ld_sw(swc + i);
+                                    }
+                                    if (sent) {
+                                        fold(mi);
+                                        recv = true;
+                                    }
+                                }
+                            }
+                        }
+                        uint32_t flags = b & (B_ACTIVE | B_CONV | (3u << CNT_SHIFT));
+                        if (recv) {
+                            if (!(b & B_CONV)) {
+                                const double r_old = sv.x / sv.y;
+                                const double r_new = acc_s / acc_w;
+                                uint32_t cnt3 = (b >> CNT_SHIFT) & 3u;
+                                cnt3 = fabs(r_new - r_old) > 1e-10 ? 0u : cnt3 + 1u;
+                                flags = (flags & ~(3u << CNT_SHIFT)) | (cnt3 << CNT_SHIFT);
+                                if (cnt3 == 3) {
+                                    flags |= B_CONV;
+                                    ++alerts;
+                                }
+                            }
+                            if (!active) {
+                                ++newly;
+                                flags |= B_ACTIVE;
+                                active = true;
+                            }
+                        }
+                        if (GP_BATCH_DIR) {
+                            pend[k >> 1] |= (mask | (active && deg > 0 ? 64u : 0u) | ((flags >> 3) << 7)) << (16 * (k & 1));
+                        } else {
+                            if (active && deg > 0) dir = slot_to_dir_fast(mask, uniform(a.k0, a.k1, S_PUSHSUM, j, r + 1, deg));
+                            reinterpret_cast<uint8_t*>(L.out)[jl] = (uint8_t)(flags | dir);
+                        }
+                        st_stream(swn + j, make_double2(acc_s, acc_w));
+                    }
+                    if (TOPO == IMP3D && !GP_BATCH_DIR) {
+                        const unsigned long long bits = __ballot(valid && dir == DIR_RANDOM);
+                        if (lane == 0) {
+                            const int64_t wi = (int64_t)((T + k * TPB + (threadIdx.x & ~63u)) >> 6) - (int64_t)(a.lo >> 6);
+                            if (wi >= 0) a.rbn[wi] = bits;
+                        }
                     }
                 }
             }
         }
+        GP_STAMP(t4);
         // next-round directions of this thread's nodes: one Philox batch
         if (GP_BATCH_DIR) {
             uint32_t node[NPT], x[NPT], y[NPT];
@@ -605,6 +661,7 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
             }
         }
         __syncthreads();
+        GP_STAMP(t5);
         // node bytes out as words (allocations are padded past P)
         for (uint32_t w = threadIdx.x; w < (uint32_t)(TILE / 4); w += TPB) {
             const uint32_t jw = T + w * 4;
@@ -615,10 +672,21 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                     if (jw + b >= j0 && jw + b < j1) a.nbn[jw + b] = reinterpret_cast<const uint8_t*>(L.out)[w * 4 + b];
             }
         }
+#if GP_STAMPS
+        GP_STAMP(t6);
+        ph[0] += t1 - t0;
+        ph[1] += t2 - t1;
+        ph[2] += t3 - t2;
+        ph[3] += t4 - t3;
+        ph[4] += t5 - t4;
+        ph[5] += t6 - t5;
+        ph[6] += 1;
+#endif
         // no barrier here: the next tile's in-edge pass and staging copies write
         // bits / msg / rows / xm / xp / off, none of which this byte output reads,
         // and its node phase writes L.out only after its staging barrier
     }
+    if (__ballot(tiny) && lane == 0) atomicOr(&ctl->tiny, 1u);
     // block reduction of alerts / newly active
     uint32_t x = alerts, y = newly;
 #pragma unroll
@@ -638,8 +706,23 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
             x += L.red[0][w];
             y += L.red[1][w];
         }
-        if (x) atomicAdd(&ctl->round_alerts, (unsigned long long)x);
-        if (y) atomicAdd(&ctl->round_active, (unsigned long long)y);
+        if (a.fuse) {
+            // returning atomics: both counts are performed before the block arrives
+            unsigned long long d = 0;
+            if (x) d += __hip_atomic_fetch_add(&ctl->round_alerts, (unsigned long long)x, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+            if (y) d += __hip_atomic_fetch_add(&ctl->round_active, (unsigned long long)y, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("" ::"v"(d));
+            __builtin_amdgcn_s_waitcnt(0);
+            block_done_close(ctl, a.G.P, a.G.T, r);
+        } else {
+            if (x) atomicAdd(&ctl->round_alerts, (unsigned long long)x);
+            if (y) atomicAdd(&ctl->round_active, (unsigned long long)y);
+        }
+#if GP_STAMPS
+        for (int q = 0; q < 7; ++q) atomicAdd(&gp_stamp_acc[q], (unsigned long long)ph[q]);
+#endif
     }
 }
 
@@ -844,6 +927,7 @@ RoundArgs make_round_args(const DevState& S, uint32_t round) {
     a.walk = S.tile_walk;
     a.stage_cap = S.tile_stage_cap;
     a.wx = S.tile_wx;
+    a.fuse = S.fuse_finalize;
     return a;
 }
 
@@ -898,3 +982,21 @@ hipError_t launch_rbits_init(const DevState& S, int grid, hipStream_t st) {
 }
 
 }  // namespace gp
+
+#if GP_STAMPS
+// Experiments build, diagnostics: mean cycles per tile of each push-sum tile
+// phase since the last reset (in-edge pass, staging issue, staging wait, node
+// phase, direction batch, byte-out barrier), out[6] = tiles counted.
+extern "C" int gp_debug_stamps(double* out, int reset) {
+    unsigned long long h[8] = {0};
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(gp::gp_stamp_acc), sizeof(h)) != hipSuccess) return -3;
+    const double n = h[6] ? (double)h[6] : 1.0;
+    for (int q = 0; q < 6; ++q) out[q] = (double)h[q] / n;
+    out[6] = (double)h[6];
+    if (reset) {
+        unsigned long long z[8] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(gp::gp_stamp_acc), z, sizeof(z)) != hipSuccess) return -3;
+    }
+    return 0;
+}
+#endif

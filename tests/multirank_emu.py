@@ -16,7 +16,14 @@ ranks only through the library's exchange plan:
     the receiver tags rtag[slot] = round (gp_xchg.hip k_pack / k_unpack);
   * bookkeeping: {alerts, newly active, injector pick converged} summed over
     ranks (k_finalize_pre / all-reduce / k_finalize_post); the gossip
-    injector's live list is replicated on every rank.
+    injector's live list is replicated on every rank;
+  * full topology (gp_full.hip): contiguous id slabs, no halo; every round each
+    rank stably sorts its senders' messages by target, cuts them into one
+    segment per destination rank (fixed per-pair capacity: expected + 12 sigma
+    + 64, an overflow fails), the destination concatenates the segments in
+    ascending source rank and sorts stably by target again -- every receiver's
+    messages then come by ascending sender id (push-sum); gossip deliveries
+    are counts added by the owner.
 
 It never calls the HIP library: it checks the decomposition itself (slab
 plan, slot arithmetic, fold order with remote messages, replicated injector)
@@ -117,7 +124,21 @@ def slab_bounds(P, g, topo, W):
     """gp_api.hip make_bounds."""
     if topo == "line":
         return [P * w // W for w in range(W + 1)], 1
+    if topo == "full":
+        return [P * w // W for w in range(W + 1)], 0
     return [(g * w // W) * g * g for w in range(W + 1)], g * g
+
+
+def full_capacity(na, nb, P):
+    """Per-pair message capacity of the full-topology exchange (gp_api.hip
+    setup_exchange): messages a -> b are at most Binomial(na, nb / (P - 1))."""
+    m = na * nb / (P - 1)
+    return int(min(np.ceil(m + 12.0 * np.sqrt(m) + 64.0), na))
+
+
+def full_target(i, k):
+    """Slot k of node i on the full topology: the k-th of all j != i (Program.fs:211-216)."""
+    return np.where(k < i, k, k + 1)
 
 
 class RankSim:
@@ -148,11 +169,12 @@ class RankSim:
             self.conv = np.zeros(self.hi - self.lo, dtype=bool)
             if self.lo <= self.seed_node < self.hi:
                 self.active[self.seed_node - self.ext_lo] = True
-                self.dir[self.seed_node - self.ext_lo] = self.G.draw_dir(np.array([self.seed_node]), S_PUSHSUM, 0)[0]
+                if topo != "full":
+                    self.dir[self.seed_node - self.ext_lo] = self.G.draw_dir(np.array([self.seed_node]), S_PUSHSUM, 0)[0]
             self.active_total = 1
         else:
             self.c = np.zeros(self.hi - self.lo, dtype=np.int64)
-            if self.lo <= self.seed_node < self.hi:
+            if self.lo <= self.seed_node < self.hi and topo != "full":
                 self.dir[self.seed_node - self.ext_lo] = self.G.draw_dir(np.array([self.seed_node]), S_GOSSIP, 0)[0]
             self.live = list(range(self.T)) if topo != "full" else None
         self._exchange(0)
@@ -187,6 +209,8 @@ class RankSim:
     def _exchange(self, rn):
         """Halo refresh + random-edge messages for round rn (state already in place)."""
         import torch
+        if self.topo == "full":  # the full topology's exchange is inside the round
+            return
         d = self.dist
         fields = [self.dir] + ([self.s, self.w, self.active.astype(np.float64)] if self.alg == "push-sum" else [])
         H = self.H
@@ -346,10 +370,90 @@ class RankSim:
         self._prepare_injector(r + 1)
         return alerts
 
+    # ---------------------------------------------------------------- full topology
+    def _full_exchange(self, targets, payload):
+        """Messages (targets ascending-sender order) -> this rank's receivers: the
+        per-destination segments of a stable sort by target, capacity-checked,
+        concatenated by ascending source rank and stably sorted by target again."""
+        order = np.argsort(targets, kind="stable")
+        t = targets[order]
+        pl = [p[order] for p in payload]
+        cuts = np.searchsorted(t, np.array(self.bounds), side="left")
+        packets = {}
+        for b in range(self.W):
+            seg = slice(cuts[b], cuts[b + 1])
+            if b != self.rank:
+                cap = full_capacity(self.hi - self.lo, self.bounds[b + 1] - self.bounds[b], self.P)
+                assert cuts[b + 1] - cuts[b] <= cap, "full-topology exchange capacity exceeded"
+            packets[b] = (t[seg] - self.bounds[b],) + tuple(x[seg] for x in pl)
+        got = [None] * self.W
+        if self.W > 1:
+            self.dist.all_gather_object(got, packets)
+        else:
+            got = [packets]
+        parts = [got[src][self.rank] for src in range(self.W)]  # ascending source rank
+        tt = np.concatenate([p[0] for p in parts])
+        cols = [np.concatenate([p[1 + q] for p in parts]) for q in range(len(payload))]
+        o2 = np.argsort(tt, kind="stable")
+        return tt[o2], [c[o2] for c in cols]
+
+    def _full_pushsum_round(self):
+        r = self.round
+        j = self.ids
+        lj = self._local(j)
+        act = self.active[lj]
+        snd = j[act] if self.P > 1 else j[:0]
+        t = full_target(snd, uniform(self.seed, S_PUSHSUM, snd, r, self.P - 1))
+        li = self._local(snd)
+        tt, (ms, mw, src) = self._full_exchange(t, [self.s[li] * 0.5, self.w[li] * 0.5, snd])
+        halve = act & (self.P > 1)
+        acc_s = np.where(halve, self.s[lj] * 0.5, self.s[lj])
+        acc_w = np.where(halve, self.w[lj] * 0.5, self.w[lj])
+        recv = np.zeros(len(j), dtype=bool)
+        if len(tt):
+            same = np.concatenate([[False], tt[1:] == tt[:-1]])
+            assert np.all(src[1:][same[1:]] > src[:-1][same[1:]]), "senders not ascending per receiver"
+            first = np.concatenate([[True], tt[1:] != tt[:-1]])
+            rank_in = np.arange(len(tt)) - np.maximum.accumulate(np.where(first, np.arange(len(tt)), 0))
+            for k in range(int(rank_in.max()) + 1):     # k-th message of every receiver, in order
+                sel = rank_in == k
+                rcv = tt[sel]
+                acc_s[rcv] = acc_s[rcv] + ms[sel]
+                acc_w[rcv] = acc_w[rcv] + mw[sel]
+                recv[rcv] = True
+        r_old = self.s[lj] / self.w[lj]
+        r_new = acc_s / acc_w
+        upd = recv & ~self.conv
+        self.cnt = np.where(upd, np.where(np.abs(r_new - r_old) > 1e-10, 0, self.cnt + 1), self.cnt)
+        newc = upd & (self.cnt == 3)
+        self.conv |= newc
+        newly = recv & ~act
+        self.active[lj] |= recv
+        self.s[lj], self.w[lj] = acc_s, acc_w
+        alerts, na, _ = self._allreduce([int(newc.sum()), int(newly.sum()), 0])
+        self.active_total += na
+        return alerts
+
+    def _full_gossip_round(self):
+        r = self.round
+        j = self.ids
+        active = ((j == self.seed_node) | (self.c >= 1)) & (self.c <= 10)
+        snd = j[active] if self.P > 1 else j[:0]
+        t = full_target(snd, uniform(self.seed, S_GOSSIP, snd, r, self.P - 1))
+        tt, _ = self._full_exchange(t, [])
+        inc = np.bincount(tt, minlength=len(j)).astype(np.int64)
+        inc[self.c >= 11] = 0                           # dropped at converged receivers (Program.fs:87)
+        alerts_local = int(((self.c <= 10) & (self.c + inc > 10) & (inc > 0)).sum())
+        self.c += inc
+        return self._allreduce([alerts_local, 0, 0])[0]
+
     def step(self, nrounds):
         out = []
         while len(out) < nrounds and not self.done:
-            a = self._gossip_round() if self.alg == "gossip" else self._pushsum_round()
+            if self.topo == "full":
+                a = self._full_gossip_round() if self.alg == "gossip" else self._full_pushsum_round()
+            else:
+                a = self._gossip_round() if self.alg == "gossip" else self._pushsum_round()
             out.append(a)
             self.alerts_total += a
             self.round += 1

@@ -1,0 +1,144 @@
+"""CPU: the one-node 8-GPU plan of BASELINE's multi-GPU configurations, computed on
+the host (no GPU, no RCCL).  The library's slab plan (gp_api.hip make_bounds)
+and exchange capacities (gp_api.hip setup_exchange: expected messages per rank
+pair + 12 sigma + 64) are restated here; the tests check that
+
+  * C5 (Imp3D push-sum, n = 1e9) and C4 (full push-sum, n = 1e8) fit one
+    MI355X's 288 GB per rank at world 8, setup temporaries included;
+  * the fixed capacities leave a 12-sigma margin over the per-round message
+    count, so an overflow (which fails the run loudly, tests/test_gpu_multirank)
+    is not a practical event over a convergence run;
+  * at a size the emulation can draw exactly (world 8, P = 64,000), the realised
+    per-pair counts of every round stay below the capacities the formula gives.
+"""
+import math
+
+import numpy as np
+
+from tests.multirank_emu import DIR_RANDOM, Geometry, S_PUSHSUM, S_TOPO, full_capacity, resolve, slab_bounds, uniform
+
+HBM_BYTES = 288e9
+GAUSS_12SIGMA_TAIL = 1.8e-33  # P(Z > 12)
+
+
+def imp3d_pair_stats(P, g, W):
+    """Expected random-edge messages per round for every rank pair a -> b and their
+    variance, from the degree distribution of the lattice (rnd[i] uniform in
+    [0, P-2], a sender uses its random edge with probability 1/deg)."""
+    bounds, _ = slab_bounds(P, g, "Imp3D", W)
+    # 1/deg summed over a slab's senders: interior 1/7, face 1/6, edge 1/5, corner 1/4
+    def inv_deg_sum(x0, x1):
+        tot = 0.0
+        for x in (x0, x1 - 1) if x1 - x0 > 1 else (x0,):
+            pass
+        n_int_x = max(0, min(x1, g - 1) - max(x0, 1))  # planes with both x neighbours
+        n_bnd_x = (x1 - x0) - n_int_x
+        # per plane: g^2 nodes; y/z boundary counts
+        inner = (g - 2) ** 2
+        faces = 4 * (g - 2)
+        corners = 4
+        for planes, xb in ((n_int_x, 0), (n_bnd_x, 1)):
+            # degree = 1 (random) + 6 lattice - boundary count
+            tot += planes * (inner / (7 - xb) + faces / (6 - xb) + corners / (5 - xb))
+        return tot
+    mu = np.zeros((W, W))
+    var = np.zeros((W, W))
+    for a in range(W):
+        x0, x1 = bounds[a] // (g * g), bounds[a + 1] // (g * g)
+        s = inv_deg_sum(x0, x1)
+        for b in range(W):
+            if a == b:
+                continue
+            frac = (bounds[b + 1] - bounds[b]) / (P - 1)  # share of targets on rank b
+            mu[a, b] = s * frac
+            var[a, b] = mu[a, b] * (1 - 1 / 7)
+    return bounds, mu, var
+
+
+def cap_of(mu):
+    return math.ceil(mu + 12.0 * math.sqrt(mu) + 64.0)
+
+
+def imp3d_rank_bytes(nloc, halo, nedges, W, caps_out, caps_in, P):
+    """Device bytes of one Imp3D push-sum rank (alloc_slab + build_imp3d +
+    setup_exchange), and the peak with build_imp3d's global temporaries."""
+    next_ = nloc + 2 * halo + 1024
+    node = next_ * (2 * 16 + 2) + nloc * 4 + (nloc + 5) * 4 + 2 * (nloc // 64 + 64) * 8  # sw, nb, rnd, in_off, rbits
+    edges = (nedges + 4) * 4 * 2 + nedges * (4 + 4 + 16)                                # in_src, in_srcd, pos, rtag, rmsg
+    xbuf = sum(16 + 4 * c + 16 * c for c in caps_out) + sum(16 + 4 * c + 16 * c for c in caps_in)
+    steady = node + edges + xbuf
+    temporaries = P * 4 * 7 + 64e6  # rnd_all, iota, keys, src_sorted, counts, off_all, inv + sort scratch
+    return steady, steady + temporaries
+
+
+def test_c5_imp3d_pushsum_1e9_world8_plan():
+    P, T, g = resolve(10**9, "Imp3D")
+    W = 8
+    bounds, mu, var = imp3d_pair_stats(P, g, W)
+    assert [(bounds[w + 1] - bounds[w]) // (g * g) for w in range(W)] == [125] * 8  # planes per rank
+    for a in range(W):
+        caps_out = [cap_of(mu[a, b]) if b != a else 0 for b in range(W)]
+        caps_in = [cap_of(mu[b, a]) if b != a else 0 for b in range(W)]
+        for b in range(W):
+            if b == a:
+                continue
+            margin = (caps_out[b] - mu[a, b]) / math.sqrt(var[a, b])
+            assert margin >= 12.0  # per-round overflow probability below GAUSS_12SIGMA_TAIL
+            assert 2.0e6 < mu[a, b] < 2.5e6  # ~2.2 M messages per pair per round
+        nloc = bounds[a + 1] - bounds[a]
+        steady, peak = imp3d_rank_bytes(nloc, g * g, nloc, W, caps_out, caps_in, P)
+        assert peak < 0.8 * HBM_BYTES, f"rank {a}: {peak / 1e9:.1f} GB"
+        assert steady < 0.1 * HBM_BYTES
+    # a convergence run of 10^5 rounds x 56 pairs stays far from an overflow
+    assert 1e5 * W * (W - 1) * GAUSS_12SIGMA_TAIL < 1e-25
+
+
+def test_c4_full_pushsum_1e8_world8_plan():
+    P, T, _ = resolve(10**8, "full")
+    W = 8
+    bounds, halo = slab_bounds(P, 0, "full", W)
+    assert halo == 0 and bounds[-1] == P
+    for a in range(W):
+        na = bounds[a + 1] - bounds[a]
+        caps_in = [full_capacity(bounds[b + 1] - bounds[b], na, P) for b in range(W) if b != a]
+        for b in range(W):
+            if b == a:
+                continue
+            nb = bounds[b + 1] - bounds[b]
+            m = na * nb / (P - 1)
+            sd = math.sqrt(m * (1 - nb / (P - 1)))
+            assert (full_capacity(na, nb, P) - m) / sd >= 12.0
+        ccap = na + sum(caps_in)  # staged messages of the receive-side sort (gp_api.hip setup_exchange)
+        assert ccap < 0xFFFFFF00
+        # node arrays + send sort (key/val x2) + receive staging (ckey/cidx x2, cval) + buffers + sort scratch
+        steady = na * (2 * 16 + 1 + 4 * 4 + 4) + ccap * (4 * 4 + 16) + 2 * sum(20 * c for c in caps_in) + 2e9
+        assert steady < 0.5 * HBM_BYTES
+
+
+def test_realised_imp3d_counts_stay_below_capacity_world8():
+    """Exact per-round counts at P = 64,000 (g = 40, 5 planes per rank), every
+    node active: the messages each rank pair carries in 40 rounds, drawn from
+    the same Philox streams as the library, against the capacity formula fed
+    with the realised expectation (as setup_exchange computes it)."""
+    n, W, seed = 64000, 8, 5
+    P, T, g = resolve(n, "Imp3D")
+    geo = Geometry(P, g, "Imp3D", seed)
+    bounds, _ = slab_bounds(P, g, "Imp3D", W)
+    ids = np.arange(P)
+    rnd = uniform(seed, S_TOPO, ids, 0, P - 1)
+    src_rank = np.searchsorted(np.array(bounds[1:-1]), ids, side="right")
+    dst_rank = np.searchsorted(np.array(bounds[1:-1]), rnd, side="right")
+    inv_deg = 1.0 / geo.degree(ids)
+    mu = np.zeros((W, W))
+    np.add.at(mu, (src_rank, dst_rank), inv_deg)
+    cap = np.vectorize(lambda m: min(cap_of(m), 10**9))(mu)
+    worst = 0.0
+    for r in range(40):
+        d = geo.draw_dir(ids, S_PUSHSUM, r)
+        sent = d == DIR_RANDOM
+        cnt = np.zeros((W, W), dtype=np.int64)
+        np.add.at(cnt, (src_rank[sent], dst_rank[sent]), 1)
+        off = ~np.eye(W, dtype=bool)
+        assert np.all(cnt[off] <= cap[off])
+        worst = max(worst, float(np.max((cnt[off] - mu[off]) / np.sqrt(mu[off]))))
+    assert worst < 6.0  # realised fluctuations are a few sigma; the capacity allows 12

@@ -45,6 +45,10 @@ CASES = [  # (num_nodes, topology, algorithm, seed, rounds, world)
     (300, "line", "gossip", 6, 1500, 2),
     (200, "line", "push-sum", 2, 200, 3),
     (2197, "Imp3D", "push-sum", 11, 50, 3),
+    (3000, "full", "push-sum", 8, 200, 2),
+    (2000, "full", "push-sum", 5, 150, 3),
+    (1500, "full", "gossip", 3, 3000, 2),
+    (999, "full", "gossip", 9, 3000, 3),
 ]
 
 

@@ -20,10 +20,15 @@ OUT = os.path.join(ROOT, "build", "ablate")
 OBJ = os.path.join(ROOT, "build", "obj_exp")
 VARIANTS = {  # name -> extra -D flags for gp_round.hip
     "base": [],
-    "nobe": ["-DGP_BATCH_EDGE=0"],
-    "nobd": ["-DGP_BATCH_DIR=0"],
-    "nopf": ["-DGP_PF_SRC=0"],
-    "none": ["-DGP_BATCH_EDGE=0", "-DGP_BATCH_DIR=0", "-DGP_PF_SRC=0"],
+    "stamps": ["-DGP_STAMPS=1"],
+    "nofma": ["-DGP_FMA_FOLD=0"],
+    "ng2": ["-DGP_NGROUP=2"],
+    "n2m6": ["-DGP_NPT=2", "-DGP_MINB=6"],
+    "n2m5": ["-DGP_NPT=2", "-DGP_MINB=5"],
+    "n2m6g2": ["-DGP_NPT=2", "-DGP_MINB=6", "-DGP_NGROUP=2"],
+    "ng2m4": ["-DGP_NGROUP=2", "-DGP_MINB=4"],
+    "ng4m4": ["-DGP_NGROUP=4", "-DGP_MINB=4"],
+    "ng1m4": ["-DGP_MINB=4"],
     "minb4": ["-DGP_MINB=4"],
     "minb6": ["-DGP_MINB=6"],
     "npt2": ["-DGP_NPT=2"],
@@ -61,7 +66,10 @@ def run(n, only=None):
                 "s=Simulation(%d,%r,'push-sum',kernel_timing=True,experimental=True)\n"
                 "P=s.population\n"
                 "pre=0\nwhile s.info().active < P and pre < 300: pre += len(s.step(8))\n"
-                "s.sync(); s.kernel_stats(reset=True); s.step(10); s.sync()\n"
+                "import ctypes as C\nL=s._L\nst=hasattr(L,'gp_debug_stamps')\nbuf=(C.c_double*8)()\n"
+                "s.sync()\nif st: L.gp_debug_stamps(buf,1)\n"
+                "s.kernel_stats(reset=True); s.step(10); s.sync()\n"
+                "if st: L.gp_debug_stamps(buf,1); print('stamps', [round(buf[q]) for q in range(7)], file=sys.stderr)\n"
                 "ms,k,_=s.kernel_stats(); print(json.dumps(ms/k))\n") % (ROOT, n, topo)
         env = dict(os.environ, GOSSIP_HIP_LIB_EXPERIMENT=so)
         out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
@@ -70,6 +78,10 @@ def run(n, only=None):
             sys.exit(1)
         res[name] = float(out.stdout.strip().splitlines()[-1])
         print(f"{name:14s} {res[name]:8.2f} ms/round", flush=True)
+        for line in out.stderr.splitlines():
+            if line.startswith("stamps"):
+                print(f"{'':14s} {line}  (cycles/tile: in-edge, stage issue, stage wait, nodes, dirs, bytes; tiles)",
+                      flush=True)
     return res
 
 
