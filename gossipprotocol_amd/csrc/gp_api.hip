@@ -34,6 +34,7 @@
 #include "../../include/gossip_hip.h"
 #include "gp_internal.hpp"
 #include "gp_full.hpp"
+#include "gp_fullbin.hpp"
 #include "gp_xchg.hpp"
 
 using namespace gp;
@@ -297,18 +298,18 @@ int alloc_slab(gp_sim* s, Slab& sl, int r) {
                 return rc;
         }
     }
-    if (S.topo == FULL && S.alg == PUSHSUM && W == 1) {
-        const uint32_t P = S.G.P;
-        if ((rc = dev_alloc_t(s, &S.key[0], P)) || (rc = dev_alloc_t(s, &S.key[1], P)) ||
-            (rc = dev_alloc_t(s, &S.val[0], P)) || (rc = dev_alloc_t(s, &S.val[1], P)) ||
-            (rc = dev_alloc_t(s, &S.head, P)))
+    if (S.topo == FULL && S.alg == PUSHSUM && W == 1) {  // LDS-binned message staging (gp_fullbin.hip)
+        const FullBinPlan fp = full_bin_plan(S.G.P);
+        S.fb_s1 = fp.s1;
+        S.fb_nb1 = fp.nb1;
+        S.fb_nb2 = fp.nb2;
+        S.fb_cap1 = fp.cap1;
+        S.fb_cap2 = fp.cap2;
+        const size_t m1 = (size_t)fp.nb1 * fp.cap1, m2 = (size_t)fp.nb2 * fp.cap2;
+        if ((rc = dev_alloc_t(s, &S.fb_cnt1, fp.nb1)) || (rc = dev_alloc_t(s, &S.fb_cnt2, fp.nb2)) ||
+            (rc = dev_alloc_t(s, &S.fb_hdr1, m1)) || (rc = dev_alloc_t(s, &S.fb_pay1, m1)) ||
+            (rc = dev_alloc_t(s, &S.fb_hdr2, m2)) || (rc = dev_alloc_t(s, &S.fb_pay2, m2)))
             return rc;
-        S.key_bits = bits_for((uint64_t)P);
-        HIP_TRY(launch_iota(S.val[0], P, s->grid, s->stream));
-        size_t tb = 0;
-        HIP_TRY(sort_pairs(nullptr, tb, S.key[0], S.key[1], S.val[0], S.val[1], P, S.key_bits, s->stream));
-        S.sort_tmp_bytes = tb;
-        if ((rc = dev_alloc(s, &S.sort_tmp, tb))) return rc;
     }
     if (S.topo == IMP3D) {
         S.rbits_words = S.kernel == KERNEL_COL ? col_rbits_words(S.nloc / S.G.g2, S.G.g)
@@ -389,6 +390,17 @@ int build_imp3d(gp_sim* s) {
             if ((rc = dev_alloc_t(s, &S.in_srcd, (size_t)ne + 4))) return rc;
             if (ne) HIP_TRY(launch_pack_src_deg(S.in_src, S.in_srcd, ne, S.G, s->grid, s->stream));
         }
+        S.nedges = ne;
+        S.eb = nullptr;
+        // separate dense edge-decision pass (k_edge_decide): measured slower than the
+        // tile kernel's own batched redraw (1.4 + 14.9 vs 14.5 ms/round at P = 1e9), opt-in
+        bool edge_pass = false;
+#ifdef GP_EXPERIMENTS
+        if (const char* e = std::getenv("GP_EDGE_PASS")) edge_pass = e[0] == '1';
+#endif
+        if (S.alg == PUSHSUM && S.kernel == KERNEL_TILE && edge_pass &&
+            (rc = dev_alloc_t(s, &S.eb, (size_t)ne / 64 + 8)))
+            return rc;
         if (W > 1) {
             if ((rc = dev_alloc_t(s, &sl.pos, S.nloc)) || (rc = dev_alloc_t(s, &S.rtag, ne)) ||
                 (S.alg == PUSHSUM && (rc = dev_alloc_t(s, &S.rmsg, ne))))
@@ -767,13 +779,6 @@ int launch_round(gp_sim* s, uint32_t r, hipEvent_t e0, hipEvent_t e1) {
     for (size_t q = 0; q < s->slab.size(); ++q) {
         DevState& S = s->slab[q].S;
         if (q == 0 && e0) HIP_TRY(hipEventRecord(e0, s->stream));
-        if (S.topo == FULL && S.alg == PUSHSUM) {
-            HIP_TRY(launch_full_pushsum_send(S, r, s->grid, s->stream));
-            HIP_TRY(sort_pairs(S.sort_tmp, S.sort_tmp_bytes, S.key[0], S.key[1], S.val[0], S.val[1], S.G.P,
-                               S.key_bits, s->stream));
-            HIP_TRY(hipMemsetAsync(S.head, 0xFF, sizeof(uint32_t) * S.G.P, s->stream));
-            HIP_TRY(launch_full_pushsum_mark(S, s->grid, s->stream));
-        }
         HIP_TRY(launch_bulk(S, r, s->grid, s->stream));
         if (q == 0 && e1) HIP_TRY(hipEventRecord(e1, s->stream));
     }
@@ -789,10 +794,9 @@ double alg_bytes(const gp_sim* s) {
         // sw r+w 32, node byte r+w 2 (+ Imp3D in-list: offset 4 + sender 4)
         if (S.topo == IMP3D) return 42.0;
         if (S.topo != FULL) return 34.0;
-        // send: byte 1 + key 4; sort: (key+val) r+w per pass; mark: key 4 + head 4;
-        // recv: sw r+w 32 + byte 1 + head 4 + key/val 8 + gathered sw 16
-        const double passes = (S.key_bits + 7) / 8;
-        return 5.0 + 16.0 * passes + 8.0 + 4.0 + 61.0;
+        // send: byte 1 + own (s, w) 16 + message write 24; split: message r+w 48; fold: header
+        // 8 twice + payload 16 + own (s, w) r+w 32 + byte r+w 2 (gp_fullbin.hip)
+        return 1.0 + 16.0 + 24.0 + 48.0 + 16.0 + 16.0 + 32.0 + 2.0;
     }
     // gossip: counter r+w 8, direction byte r+w 2 (+ Imp3D in-list 8)
     if (S.topo == IMP3D) return 18.0;
@@ -1111,8 +1115,8 @@ int64_t gp_step(gp_sim* s, int64_t nrounds, int64_t* alerts_out) {
             return GP_ESTATE;
         }
         if (hc.overflow) {
-            set_err("random-edge exchange buffer overflow (capacity = expected + 12 sigma was exceeded); "
-                    "the rounds of this batch are invalid");
+            set_err("message buffer overflow (an exchange buffer or a message bin exceeded its capacity = "
+                    "expected + 12 sigma); the rounds of this batch are invalid");
             return GP_ESTATE;
         }
         int64_t cum = s->alerts_total, ex = 0;

@@ -1,0 +1,323 @@
+// gp_fullbin.hip -- push-sum on the full topology, one rank (gfx950): the
+// scattered receives of a round are staged and binned through LDS, then folded
+// per receiver tile in the canonical order.
+//
+// Reference: every node's neighbour list is all j != i (Program.fs:209-216);
+// an active node halves (sum, weight) and sends the halves to one uniform
+// neighbour (Program.fs:104-106,125-128); a receiver folds its messages (SRS v1
+// B.4: own half, then messages by ascending sender id) and runs the ratio test
+// (Program.fs:114-123).
+//
+// Per round, three kernels:
+//   A  k_fb_send   senders in chunks of FB_CHUNK: target t = U(P-1) mapped past i
+//                  (Philox), LDS counting by coarse bin (t >> s1), one global
+//                  reservation per (chunk, bin), each message {t, i | s/2, w/2}
+//                  written into its coarse bin's run;
+//   B  k_fb_split  each coarse bin's messages in chunks: LDS counting by fine
+//                  tile (t >> FB_TB, FB_TILE receivers), reservation, copy;
+//   C  k_fb_fold   one fine tile per block: LDS counting sort of the tile's
+//                  messages by receiver, each receiver's (few) messages put in
+//                  ascending sender order, folded, ratio test, next state.
+// Order inside a bin is whatever the LDS atomics produce; the fold restores the
+// canonical order by sender id, so results do not depend on it.  Every message
+// is moved as 24 bytes (header 8 + payload 16), each pass coalesced -- no
+// random 16-byte gather of a sender's (s, w) anywhere.  Bin capacities are the
+// expected load + 12 sigma + slack; an overflow is flagged (Ctl::overflow) and
+// fails the batch in gp_step.
+#include <algorithm>
+#include <cmath>
+
+#include "gp_fullbin.hpp"
+
+namespace gp {
+namespace {
+
+constexpr int FB_THREADS = 256;
+#ifndef GP_FB_PER
+#define GP_FB_PER 16
+#endif
+constexpr int FB_PER = GP_FB_PER;                  // senders / messages per thread per chunk
+constexpr int FB_CHUNK = FB_THREADS * FB_PER;      // 4096
+constexpr int FB_MAXBINS = 4096;                   // LDS counters of A and B
+
+template <typename T>
+__device__ __forceinline__ T ld_agent(const T* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Exclusive scan of cnt[0..n) in LDS (n <= FB_MAXBINS), one block; returns the total.
+__device__ uint32_t lds_excl_scan(uint32_t* cnt, uint32_t n, uint32_t* tmp) {
+    constexpr int PER = FB_MAXBINS / FB_THREADS;  // 16 counters per thread
+    uint32_t v[PER], s = 0;
+    const uint32_t b = threadIdx.x * PER;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        v[k] = b + k < n ? cnt[b + k] : 0u;
+        s += v[k];
+    }
+    // block scan of the per-thread sums
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t incl = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+    }
+    if (lane == 63) tmp[wid] = incl;
+    __syncthreads();
+    uint32_t wbase = 0, total = 0;
+    for (int w = 0; w < FB_THREADS / 64; ++w) {
+        if (w < wid) wbase += tmp[w];
+        total += tmp[w];
+    }
+    uint32_t run = wbase + incl - s;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        if (b + k < n) cnt[b + k] = run;
+        run += v[k];
+    }
+    __syncthreads();
+    return total;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- A: send + coarse bins
+__global__ __launch_bounds__(FB_THREADS) void k_fb_send(FullBinArgs a, uint32_t r) {
+    __shared__ uint32_t cnt[FB_MAXBINS];       // per bin: count, then the chunk's global base
+    __shared__ uint32_t tgt[FB_CHUNK];         // target per sender of the chunk (~0: inactive)
+    __shared__ uint16_t rank[FB_CHUNK];        // its position in the chunk's run of its bin
+    if (ld_agent(&a.ctl->done)) return;
+    const uint32_t P = a.P;
+    for (uint64_t c0 = (uint64_t)blockIdx.x * FB_CHUNK; c0 < P; c0 += (uint64_t)gridDim.x * FB_CHUNK) {
+        for (uint32_t b = threadIdx.x; b < a.nb1; b += FB_THREADS) cnt[b] = 0u;
+        __syncthreads();
+        constexpr int PB = 8;  // Philox chains interleaved per batch
+#pragma unroll
+        for (int k0 = 0; k0 < FB_PER; k0 += PB) {
+            uint32_t node[PB], x[PB], y[PB];
+#pragma unroll
+            for (int k = 0; k < PB; ++k) node[k] = (uint32_t)(c0 + (k0 + k) * FB_THREADS + threadIdx.x);
+            philox2_batch<PB>(node, r, S_PUSHSUM, a.k0, a.k1, x, y);
+#pragma unroll
+            for (int k = 0; k < PB; ++k) {
+                const uint32_t i = node[k], q = (k0 + k) * FB_THREADS + threadIdx.x;
+                uint32_t t = 0xFFFFFFFFu;
+                if (i < P && (a.nb[i] & B_ACTIVE) && P > 1) {
+                    t = full_target(i, uniform_from(x[k], y[k], P - 1));  // Program.fs:213-215
+                    rank[q] = (uint16_t)atomicAdd(&cnt[t >> a.s1], 1u);
+                }
+                tgt[q] = t;
+            }
+        }
+        __syncthreads();
+        // reserve the chunk's run in every coarse bin it touches
+        for (uint32_t b = threadIdx.x; b < a.nb1; b += FB_THREADS) {
+            const uint32_t n = cnt[b];
+            cnt[b] = n ? atomicAdd(&a.cnt1[b], n) : 0u;
+        }
+        __syncthreads();
+#pragma unroll 4
+        for (int k = 0; k < FB_PER; ++k) {
+            const uint32_t q = k * FB_THREADS + threadIdx.x, t = tgt[q];
+            if (t == 0xFFFFFFFFu) continue;
+            const uint32_t i = (uint32_t)(c0 + q), b = t >> a.s1;
+            const uint32_t pos = cnt[b] + rank[q];
+            if (pos >= a.cap1) {
+                atomicOr(a.overflow, 1u);
+                continue;
+            }
+            const double2 sv = a.swc[i];
+            const size_t o = (size_t)b * a.cap1 + pos;
+            a.hdr1[o] = make_uint2(t, i);
+            a.pay1[o] = make_double2(sv.x * 0.5, sv.y * 0.5);
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------- B: coarse -> fine bins
+// Work item w = (coarse bin, chunk of FB_CHUNK of its messages).
+__global__ __launch_bounds__(FB_THREADS) void k_fb_split(FullBinArgs a) {
+    __shared__ uint32_t cnt[FB_MAXBINS];
+    __shared__ uint16_t rank[FB_CHUNK];
+    __shared__ uint16_t fine[FB_CHUNK];
+    if (ld_agent(&a.ctl->done)) return;
+    const uint32_t per_bin = (a.cap1 + FB_CHUNK - 1) / FB_CHUNK;  // chunk slots per coarse bin
+    const uint32_t nfine = 1u << (a.s1 - FB_TB);                 // fine tiles per coarse bin
+    for (uint32_t w = blockIdx.x; w < a.nb1 * per_bin; w += gridDim.x) {
+        const uint32_t b = w / per_bin, c = w % per_bin;
+        const uint32_t n_bin = min(ld_agent(&a.cnt1[b]), a.cap1);
+        const uint32_t q0 = c * FB_CHUNK;
+        if (q0 >= n_bin) continue;  // block-uniform
+        const uint32_t n = min((uint32_t)FB_CHUNK, n_bin - q0);
+        for (uint32_t f = threadIdx.x; f < nfine; f += FB_THREADS) cnt[f] = 0u;
+        __syncthreads();
+        const size_t base = (size_t)b * a.cap1 + q0;
+        for (uint32_t q = threadIdx.x; q < n; q += FB_THREADS) {
+            const uint32_t f = (a.hdr1[base + q].x >> FB_TB) & (nfine - 1u);
+            fine[q] = (uint16_t)f;
+            rank[q] = (uint16_t)atomicAdd(&cnt[f], 1u);
+        }
+        __syncthreads();
+        const uint32_t f0 = b << (a.s1 - FB_TB);  // first fine tile of the coarse bin
+        for (uint32_t f = threadIdx.x; f < nfine; f += FB_THREADS) {
+            const uint32_t m = cnt[f];
+            cnt[f] = m && f0 + f < a.nb2 ? atomicAdd(&a.cnt2[f0 + f], m) : 0u;
+        }
+        __syncthreads();
+        for (uint32_t q = threadIdx.x; q < n; q += FB_THREADS) {
+            const uint32_t f = fine[q], pos = cnt[f] + rank[q];
+            if (f0 + f >= a.nb2 || pos >= a.cap2) {
+                atomicOr(a.overflow, 1u);
+                continue;
+            }
+            const size_t o = (size_t)(f0 + f) * a.cap2 + pos;
+            a.hdr2[o] = a.hdr1[base + q];
+            a.pay2[o] = a.pay1[base + q];
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------- C: fold per fine tile
+__global__ __launch_bounds__(FB_THREADS) void k_fb_fold(FullBinArgs a, uint32_t r) {
+    constexpr int TILE = 1 << FB_TB;
+    constexpr int NPT = TILE / FB_THREADS;
+    __shared__ uint32_t cnt[TILE + 1];            // per receiver: count, then start
+    __shared__ uint32_t src[FB_CAP2];             // message sender ids in receiver order
+    __shared__ uint16_t idx[FB_CAP2];             // message index in the fine bin, receiver order
+    __shared__ uint16_t rnk[FB_CAP2];
+    __shared__ uint32_t tmp[FB_THREADS / 64];
+    __shared__ uint32_t red[2][FB_THREADS / 64];
+    Ctl* ctl = a.ctl;
+    if (ld_agent(&ctl->done)) return;
+    const uint32_t P = a.P;
+    uint32_t alerts = 0, newly = 0;
+    for (uint32_t f = blockIdx.x; f < a.nb2; f += gridDim.x) {
+        const uint32_t n = min(ld_agent(&a.cnt2[f]), (uint32_t)a.cap2);
+        const size_t base = (size_t)f * a.cap2;
+        for (uint32_t v = threadIdx.x; v < TILE; v += FB_THREADS) cnt[v] = 0u;
+        __syncthreads();
+        for (uint32_t q = threadIdx.x; q < n; q += FB_THREADS)
+            rnk[q] = (uint16_t)atomicAdd(&cnt[a.hdr2[base + q].x & (TILE - 1)], 1u);
+        __syncthreads();
+        lds_excl_scan(cnt, TILE, tmp);
+        if (threadIdx.x == 0) cnt[TILE] = n;
+        for (uint32_t q = threadIdx.x; q < n; q += FB_THREADS) {
+            const uint2 h = a.hdr2[base + q];
+            const uint32_t p = cnt[h.x & (TILE - 1)] + rnk[q];
+            src[p] = h.y;
+            idx[p] = (uint16_t)q;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            const uint32_t v = k * FB_THREADS + threadIdx.x;
+            const uint32_t j = f * TILE + v;
+            if (j >= P) continue;
+            const uint32_t p0 = cnt[v], p1 = cnt[v + 1];
+            // this receiver's messages in ascending sender id (canonical order):
+            // insertion sort of its (few) entries in place
+            for (uint32_t p = p0 + 1; p < p1; ++p) {
+                const uint32_t s = src[p];
+                const uint16_t x = idx[p];
+                uint32_t q = p;
+                while (q > p0 && src[q - 1] > s) {
+                    src[q] = src[q - 1];
+                    idx[q] = idx[q - 1];
+                    --q;
+                }
+                src[q] = s;
+                idx[q] = x;
+            }
+            const uint8_t b = a.nb[j];
+            const double2 sv = a.swc[j];
+            const bool active = (b & B_ACTIVE) != 0;
+            double acc_s = active && P > 1 ? sv.x * 0.5 : sv.x;
+            double acc_w = active && P > 1 ? sv.y * 0.5 : sv.y;
+            for (uint32_t p = p0; p < p1; ++p) {
+                const double2 m = a.pay2[base + idx[p]];  // already halved by the sender
+                acc_s = acc_s + m.x;
+                acc_w = acc_w + m.y;
+            }
+            if (p1 > p0) {
+                uint32_t flags = b;
+                if (!(b & B_CONV)) {
+                    const double r_old = sv.x / sv.y;
+                    const double r_new = acc_s / acc_w;
+                    uint32_t c = (b >> CNT_SHIFT) & 3u;
+                    c = fabs(r_new - r_old) > 1e-10 ? 0u : c + 1u;
+                    flags = (flags & ~(3u << CNT_SHIFT)) | (c << CNT_SHIFT);
+                    if (c == 3) {
+                        flags |= B_CONV;
+                        ++alerts;
+                    }
+                }
+                if (!active) {
+                    ++newly;
+                    flags |= B_ACTIVE;
+                }
+                a.nb[j] = (uint8_t)flags;
+            }
+            a.swn[j] = make_double2(acc_s, acc_w);
+        }
+        __syncthreads();
+    }
+    uint32_t x = alerts, y = newly;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        x += __shfl_xor(x, o, 64);
+        y += __shfl_xor(y, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = x;
+        red[1][threadIdx.x >> 6] = y;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        x = y = 0;
+        for (int w = 0; w < FB_THREADS / 64; ++w) {
+            x += red[0][w];
+            y += red[1][w];
+        }
+        if (x) atomicAdd(&ctl->round_alerts, (unsigned long long)x);
+        if (y) atomicAdd(&ctl->round_active, (unsigned long long)y);
+    }
+}
+
+// ---------------------------------------------------------------- host side
+FullBinPlan full_bin_plan(uint32_t P) {
+    FullBinPlan p{};
+    uint32_t bits = 1;
+    while (bits < 32 && ((uint64_t)1 << bits) < P) ++bits;
+    // coarse bins ~ sqrt(P / TILE) so both passes write runs of ~10-20 messages;
+    // at most FB_MAXBINS coarse bins and FB_MAXBINS fine tiles per coarse bin
+    uint32_t s1 = (bits + FB_TB + 1) / 2;
+    if (s1 < FB_TB) s1 = FB_TB;
+    while (((uint64_t)P >> s1) >= FB_MAXBINS) ++s1;
+    while (s1 - FB_TB > 12) --s1;
+    p.s1 = s1;
+    p.nb1 = (uint32_t)(((uint64_t)P + (1ull << s1) - 1) >> s1);
+    p.nb2 = (uint32_t)(((uint64_t)P + (1u << FB_TB) - 1) >> FB_TB);
+    const double m1 = (double)(1ull << s1) * ((double)P / (double)(P > 1 ? P - 1 : 1));
+    p.cap1 = (uint32_t)(m1 + 12.0 * std::sqrt(m1) + 1024.0);
+    p.cap2 = FB_CAP2;
+    return p;
+}
+
+hipError_t launch_full_bin_round(const FullBinArgs& a, uint32_t round, int grid, hipStream_t st) {
+    hipError_t e;
+    if ((e = hipMemsetAsync(a.cnt1, 0, sizeof(uint32_t) * a.nb1, st)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(a.cnt2, 0, sizeof(uint32_t) * a.nb2, st)) != hipSuccess) return e;
+    const uint32_t chunks = (a.P + FB_CHUNK - 1) / FB_CHUNK;
+    hipLaunchKernelGGL(k_fb_send, dim3(std::min<uint32_t>(chunks, (uint32_t)grid)), dim3(FB_THREADS), 0, st, a,
+                       round);
+    const uint32_t items = a.nb1 * ((a.cap1 + FB_CHUNK - 1) / FB_CHUNK);
+    hipLaunchKernelGGL(k_fb_split, dim3(std::min<uint32_t>(items, (uint32_t)grid)), dim3(FB_THREADS), 0, st, a);
+    hipLaunchKernelGGL(k_fb_fold, dim3(std::min<uint32_t>(a.nb2, (uint32_t)grid)), dim3(FB_THREADS), 0, st, a,
+                       round);
+    return hipGetLastError();
+}
+
+}  // namespace gp

@@ -1,0 +1,39 @@
+// gp_fullbin.hpp -- single-rank full-topology push-sum round by two-level LDS
+// binning (gp_fullbin.hip).  Not part of the C-ABI.
+#pragma once
+
+#include "gp_internal.hpp"
+
+namespace gp {
+
+constexpr int FB_TB = 10;        // fine tile = 2^FB_TB receivers (one fold block)
+constexpr int FB_CAP2 = 1536;    // messages per fine tile: 1024 expected + 12 sigma (384) + 128
+
+struct FullBinPlan {
+    uint32_t s1;    // coarse bin = target >> s1
+    uint32_t nb1;   // coarse bins
+    uint32_t nb2;   // fine tiles
+    uint32_t cap1;  // message capacity per coarse bin
+    uint32_t cap2;  // message capacity per fine tile
+};
+
+struct FullBinArgs {
+    const double2* swc;  // (s, w) at round start
+    double2* swn;        // (s, w) after the round
+    uint8_t* nb;         // node byte (active / converged / count), single buffer
+    Ctl* ctl;
+    unsigned int* overflow;
+    uint32_t P, k0, k1;
+    uint32_t s1, nb1, nb2, cap1, cap2;
+    uint32_t* cnt1;      // [nb1] messages per coarse bin (zeroed every round)
+    uint32_t* cnt2;      // [nb2] messages per fine tile
+    uint2* hdr1;         // [nb1 * cap1] {target, sender}
+    double2* pay1;       // [nb1 * cap1] {s / 2, w / 2}
+    uint2* hdr2;         // [nb2 * cap2]
+    double2* pay2;
+};
+
+FullBinPlan full_bin_plan(uint32_t P);
+hipError_t launch_full_bin_round(const FullBinArgs& a, uint32_t round, int grid, hipStream_t st);
+
+}  // namespace gp

@@ -102,12 +102,11 @@ struct DevState {
     uint32_t nchunks;
     // full topology scratch
     int32_t* inc;          // gossip deliveries per node
-    uint32_t* key[2];      // push-sum: target per sender / sorted
-    uint32_t* val[2];      // push-sum: sender ids / sorted
-    uint32_t* head;        // push-sum: first sorted position per receiver
-    void* sort_tmp;
-    size_t sort_tmp_bytes;
-    uint32_t key_bits;
+    // push-sum, one rank: two-level LDS binning of the round's messages (gp_fullbin.hip)
+    uint32_t fb_s1, fb_nb1, fb_nb2, fb_cap1, fb_cap2;
+    uint32_t *fb_cnt1, *fb_cnt2;
+    uint2 *fb_hdr1, *fb_hdr2;
+    double2 *fb_pay1, *fb_pay2;
     // slab of this rank (single GPU: lo = 0, nloc = P, base = 0): node ids
     // [lo, lo + nloc) are owned; per-node arrays (sw, nb) start at id `base`
     // (= lo - halo); c, in_off and rbits are indexed from lo
@@ -124,6 +123,10 @@ struct DevState {
     uint32_t tile_wx;    // RoundArgs::wx
     uint32_t tile_stage_cap;  // RoundArgs::stage_cap (experiments build only; default: no limit)
     uint32_t fuse_finalize;   // the round kernel closes its own round (single rank push-sum)
+    // Imp3D push-sum, tile kernel: the rank's in-edge count and the steady-state
+    // edge-decision bitmap (k_edge_decide), one bit per in-edge
+    uint32_t nedges;
+    uint64_t* eb;
 };
 
 // Arguments of the tiled round kernels (gp_round.hip): only what they read.
@@ -148,6 +151,7 @@ struct RoundArgs {
     uint32_t wx;    // walk 2: planes per x-window
     uint32_t stage_cap;  // k_ps_tile: tiles with more in-edges take the unstaged path (tests force it)
     uint32_t fuse;       // k_ps_tile: the last block closes the round (no k_finalize launch)
+    const uint64_t* eb;  // Imp3D: this round's edge decisions (k_edge_decide), or null
 };
 
 enum KernelVariant : int { KERNEL_WAVE = 0, KERNEL_TILE = 1, KERNEL_COL = 2 };
@@ -201,9 +205,7 @@ hipError_t launch_bulk(const DevState& S, uint32_t round, int grid, hipStream_t 
 hipError_t launch_finalize(const DevState& S, uint32_t round_done, uint32_t round_next, hipStream_t st);
 hipError_t launch_finalize_pre(const DevState& S, uint32_t round_next, hipStream_t st);
 hipError_t launch_finalize_post(const DevState& S, uint32_t round_done, uint32_t round_next, hipStream_t st);
-hipError_t launch_full_pushsum_send(const DevState& S, uint32_t round, int grid, hipStream_t st);
-hipError_t launch_full_pushsum_mark(const DevState& S, int grid, hipStream_t st);
-hipError_t launch_full_pushsum_recv(const DevState& S, uint32_t round, int grid, hipStream_t st);
+hipError_t launch_full_pushsum_round(const DevState& S, uint32_t round, int grid, hipStream_t st);
 hipError_t launch_iota(uint32_t* v, uint32_t n, int grid, hipStream_t st);
 hipError_t launch_histogram(const uint32_t* keys, uint32_t n, uint32_t* counts, int grid, hipStream_t st);
 const char* bulk_kernel_name(const DevState& S);

@@ -13,6 +13,7 @@
 // Built with -ffp-contract=off: the push-sum fold must round exactly like the
 // CPU oracle.
 #include "gp_internal.hpp"
+#include "gp_fullbin.hpp"
 
 namespace gp {
 
@@ -155,82 +156,6 @@ __global__ __launch_bounds__(BULK_THREADS) void k_full_gossip_recv(DevState S, u
     }
     block_sum2(alerts, unused, red);
     if (threadIdx.x == 0 && alerts) atomicAdd(&ctl->round_alerts, (unsigned long long)alerts);
-}
-
-// Push-sum full: stage (target, sender) pairs; a stable radix sort by target
-// then yields every receiver's senders in ascending order.
-__global__ __launch_bounds__(BULK_THREADS) void k_full_ps_send(DevState S, uint32_t r) {
-    if (ld_agent(&S.ctl->done)) return;
-    const uint32_t P = S.G.P;
-    for (uint32_t i = blockIdx.x * BULK_THREADS + threadIdx.x; i < P; i += gridDim.x * BULK_THREADS) {
-        const bool act = (S.nb[0][i] & B_ACTIVE) != 0;
-        S.key[0][i] = act ? full_target(i, uniform(S.k0, S.k1, S_PUSHSUM, i, r, P - 1)) : P;
-    }
-}
-
-__global__ __launch_bounds__(BULK_THREADS) void k_full_ps_mark(DevState S) {
-    if (ld_agent(&S.ctl->done)) return;
-    const uint32_t P = S.G.P;
-    const uint32_t* __restrict__ ks = S.key[1];
-    for (uint32_t p = blockIdx.x * BULK_THREADS + threadIdx.x; p < P; p += gridDim.x * BULK_THREADS) {
-        const uint32_t k = ks[p];
-        if (k < P && (p == 0 || ks[p - 1] != k)) S.head[k] = p;
-    }
-}
-
-__global__ __launch_bounds__(BULK_THREADS) void k_full_ps_recv(DevState S, uint32_t r) {
-    __shared__ uint32_t red[2][BULK_THREADS / 64];
-    Ctl* ctl = S.ctl;
-    if (ld_agent(&ctl->done)) return;
-    const int cur = r & 1;
-    const double2* __restrict__ swc = S.sw[cur];
-    double2* __restrict__ swn = S.sw[cur ^ 1];
-    const uint32_t* __restrict__ ks = S.key[1];
-    const uint32_t* __restrict__ vs = S.val[1];
-    const uint32_t P = S.G.P;
-    uint32_t alerts = 0, newly = 0;
-    for (uint32_t j = blockIdx.x * BULK_THREADS + threadIdx.x; j < P; j += gridDim.x * BULK_THREADS) {
-        const uint8_t b = S.nb[0][j];
-        const double2 sv = swc[j];
-        const bool active = (b & B_ACTIVE) != 0;
-        double acc_s = active ? sv.x * 0.5 : sv.x;
-        double acc_w = active ? sv.y * 0.5 : sv.y;
-        uint32_t p = S.head[j];
-        bool recv = false;
-        if (p != 0xFFFFFFFFu) {
-            for (; p < P && ks[p] == j; ++p) {
-                const double2 m = swc[vs[p]];
-                acc_s = acc_s + m.x * 0.5;
-                acc_w = acc_w + m.y * 0.5;
-                recv = true;
-            }
-        }
-        uint32_t flags = b;
-        if (recv) {
-            if (!(b & B_CONV)) {
-                const double r_old = sv.x / sv.y;
-                const double r_new = acc_s / acc_w;
-                uint32_t cnt = (b >> CNT_SHIFT) & 3u;
-                cnt = fabs(r_new - r_old) > 1e-10 ? 0u : cnt + 1u;
-                flags = (flags & ~(3u << CNT_SHIFT)) | (cnt << CNT_SHIFT);
-                if (cnt == 3) {
-                    flags |= B_CONV;
-                    ++alerts;
-                }
-            }
-            if (!active) {
-                ++newly;
-                flags |= B_ACTIVE;
-            }
-            S.nb[0][j] = (uint8_t)flags;
-        }
-        swn[j] = make_double2(acc_s, acc_w);
-    }
-    block_sum2(alerts, newly, red);
-    if (threadIdx.x == 0) {
-        if (alerts) atomicAdd(&ctl->round_alerts, (unsigned long long)alerts);
-        if (newly) atomicAdd(&ctl->round_active, (unsigned long long)newly);
-    }
 }
 
 // ---------------------------------------------------------------- finalize
@@ -463,7 +388,7 @@ hipError_t launch_bulk(const DevState& S, uint32_t round, int grid, hipStream_t 
 #endif
     }
     if (S.alg == PUSHSUM) {
-        hipLaunchKernelGGL(k_full_ps_recv, g, b, 0, st, S, round);
+        return launch_full_pushsum_round(S, round, grid, st);
     } else {
         hipLaunchKernelGGL(k_full_gossip_send, g, b, 0, st, S, round);
         hipLaunchKernelGGL(k_full_gossip_recv, g, b, 0, st, S, round);
@@ -472,11 +397,11 @@ hipError_t launch_bulk(const DevState& S, uint32_t round, int grid, hipStream_t 
 }
 
 const char* bulk_kernel_name(const DevState& S) {
-    static const char* ps[3][4] = {{"k_ps_wave<LINE>", "k_full_ps_send+bin+recv", "k_ps_wave<GRID3D>",
+    static const char* ps[3][4] = {{"k_ps_wave<LINE>", "k_fb_send+split+fold", "k_ps_wave<GRID3D>",
                                     "k_ps_wave<IMP3D>"},
-                                   {"k_ps_tile<LINE>", "k_full_ps_send+bin+recv", "k_ps_tile<GRID3D>",
+                                   {"k_ps_tile<LINE>", "k_fb_send+split+fold", "k_ps_tile<GRID3D>",
                                     "k_ps_tile<IMP3D>"},
-                                   {"k_ps_wave<LINE>", "k_full_ps_send+bin+recv", "k_ps_col<GRID3D>",
+                                   {"k_ps_wave<LINE>", "k_fb_send+split+fold", "k_ps_col<GRID3D>",
                                     "k_ps_col<IMP3D>"}};
     static const char* go[3][4] = {{"k_gossip_wave<LINE>", "k_full_gossip_send+recv", "k_gossip_wave<GRID3D>",
                                     "k_gossip_wave<IMP3D>"},
@@ -509,19 +434,32 @@ hipError_t launch_finalize(const DevState& S, uint32_t round_done, uint32_t roun
     return hipGetLastError();
 }
 
-hipError_t launch_full_pushsum_send(const DevState& S, uint32_t round, int grid, hipStream_t st) {
-    hipLaunchKernelGGL(k_full_ps_send, dim3(grid), dim3(BULK_THREADS), 0, st, S, round);
-    return hipGetLastError();
-}
+}  // namespace gp
 
-hipError_t launch_full_pushsum_mark(const DevState& S, int grid, hipStream_t st) {
-    hipLaunchKernelGGL(k_full_ps_mark, dim3(grid), dim3(BULK_THREADS), 0, st, S);
-    return hipGetLastError();
+namespace gp {
+// Full-topology push-sum round on one rank (gp_fullbin.hip).
+hipError_t launch_full_pushsum_round(const DevState& S, uint32_t round, int grid, hipStream_t st) {
+    FullBinArgs a{};
+    const int cur = round & 1;
+    a.swc = S.sw[cur];
+    a.swn = S.sw[cur ^ 1];
+    a.nb = S.nb[0];
+    a.ctl = S.ctl;
+    a.overflow = &S.ctl->overflow;
+    a.P = S.G.P;
+    a.k0 = S.k0;
+    a.k1 = S.k1;
+    a.s1 = S.fb_s1;
+    a.nb1 = S.fb_nb1;
+    a.nb2 = S.fb_nb2;
+    a.cap1 = S.fb_cap1;
+    a.cap2 = S.fb_cap2;
+    a.cnt1 = S.fb_cnt1;
+    a.cnt2 = S.fb_cnt2;
+    a.hdr1 = S.fb_hdr1;
+    a.pay1 = S.fb_pay1;
+    a.hdr2 = S.fb_hdr2;
+    a.pay2 = S.fb_pay2;
+    return launch_full_bin_round(a, round, grid, st);
 }
-
-hipError_t launch_full_pushsum_recv(const DevState& S, uint32_t round, int grid, hipStream_t st) {
-    hipLaunchKernelGGL(k_full_ps_recv, dim3(grid), dim3(BULK_THREADS), 0, st, S, round);
-    return hipGetLastError();
-}
-
 }  // namespace gp

@@ -20,6 +20,7 @@
 // Tiles are walked XCD-contiguously (blocks b and b+8 share an XCD on
 // MI355X), so the +-g rows a tile gathers from were just read by its XCD.
 // Built with -ffp-contract=off: the fold must round exactly like the oracle.
+#include <algorithm>
 #include <type_traits>
 
 #include "gp_internal.hpp"
@@ -53,6 +54,12 @@ namespace gp {
 #endif
 #ifndef GP_NGROUP
 #define GP_NGROUP 1      // nodes per thread whose lattice gathers are issued together
+#endif
+#ifndef GP_LMASK
+#define GP_LMASK 0       // lattice gathers exec-masked to the lanes with a sender (else: zero sentinel)
+#endif
+#ifndef GP_ABL_NOZ
+#define GP_ABL_NOZ 0     // ablation (wrong results, timing only): skip the z+-1 lattice gathers
 #endif
 #ifndef GP_STAMPS
 #define GP_STAMPS 0      // diagnostics (experiments build): per-phase cycle counts of the push-sum tile kernel
@@ -372,7 +379,16 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                 bool sent[FU];
 #pragma unroll
                 for (int m = 0; m < FU; ++m) isrc[m] = packed ? raw[m] & 0x3FFFFFFFu : raw[m];
-                if (all_active && GP_BATCH_EDGE) {
+                if (all_active && a.eb) {
+                    // decided by k_edge_decide (this round's Philox redraws, one dense
+                    // pass): bit e_lo + q of the rank's edge bitmap
+#pragma unroll
+                    for (int m = 0; m < FU; ++m) {
+                        const uint32_t q = threadIdx.x + m * TPB;
+                        const uint32_t e = e_lo + q;
+                        sent[m] = q < cnt && ((a.eb[e >> 6] >> (e & 63u)) & 1ull);
+                    }
+                } else if (all_active && GP_BATCH_EDGE) {
                     uint32_t x[FU], y[FU];
                     philox2_batch<FU>(isrc, r, S_PUSHSUM, a.k0, a.k1, x, y);
 #pragma unroll
@@ -392,12 +408,20 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                         }
                     }
                 } else {
+                    // activation: the sender sends on its random edge iff its draw picks
+                    // that slot AND it is active -- redraw first, then read the ballot
+                    // bitmap (bit = dir == random, i.e. both) only for the ~1/7 of edges
+                    // the draw selects, instead of a random bitmap read per edge
+                    uint32_t x[FU], y[FU];
+                    philox2_batch<FU>(isrc, r, S_PUSHSUM, a.k0, a.k1, x, y);
 #pragma unroll
                     for (int m = 0; m < FU; ++m) {
                         const uint32_t q = threadIdx.x + m * TPB;
                         const uint32_t i = isrc[m];
-                        sent[m] = q < cnt && (!REMOTE || i - a.lo < a.nloc) &&
-                                  ((rbc[(i >> 6) - (a.lo >> 6)] >> (i & 63)) & 1ull);
+                        const uint32_t di = packed ? (raw[m] >> 30) + 4u : popc6(present_mask<IMP3D>(i, G)) + 1u;
+                        sent[m] = false;
+                        if (q < cnt && (!REMOTE || i - a.lo < a.nloc) && uniform_from(x[m], y[m], di) == di - 1u)
+                            sent[m] = (rbc[(i >> 6) - (a.lo >> 6)] >> (i & 63)) & 1ull;
                     }
                 }
                 if (REMOTE) {  // sender on another rank: the exchange tagged its message
@@ -509,7 +533,14 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                     gfrom[h] = from;
 #pragma unroll
                     for (uint32_t d = 0; d < ND; ++d)
-                        m[h][d] = ld_sw(swc + ((from >> d) & 1u ? nbr<TOPO>(j, d, G) : a.ext_hi));
+                        if (GP_ABL_NOZ && d >= 4) {  // ablation (timing only): no z+-1 gathers
+                            m[h][d] = make_double2(0.0, 0.0);
+                        } else if (GP_LMASK) {  // only lanes with a sender load (exec-masked gather)
+                            m[h][d] = make_double2(0.0, 0.0);
+                            if ((from >> d) & 1u) m[h][d] = ld_sw(swc + nbr<TOPO>(j, d, G));
+                        } else {
+                            m[h][d] = ld_sw(swc + ((from >> d) & 1u ? nbr<TOPO>(j, d, G) : a.ext_hi));
+                        }
                 }
                 // phase B: canonical fold (own half, lattice slots in slot order, random
                 // edges by ascending sender; every message contributes the sender's half),
@@ -574,7 +605,9 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                                         sent = a.rtag[e] == r;
                                         if (sent) mi = a.rmsg[e];
                                     } else {
-                                        if (all_active) {
+                                        if (all_active && a.eb) {
+                                            sent = (a.eb[e >> 6] >> (e & 63u)) & 1ull;
+                                        } else if (all_active) {
                                             const uint32_t di = popc6(present_mask<IMP3D>(i, G)) + 1u;
                                             sent = uniform(a.k0, a.k1, S_PUSHSUM, i, r, di) == di - 1u;
                                         } else {
@@ -723,6 +756,41 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
 #if GP_STAMPS
         for (int q = 0; q < 7; ++q) atomicAdd(&gp_stamp_acc[q], (unsigned long long)ph[q]);
 #endif
+    }
+}
+
+// ---------------------------------------------------------------- push-sum, edge decisions (Imp3D)
+// Steady-state in-edge decisions of round r for one rank: bit e of `eb` = "the
+// sender of in-edge e (receiver-sorted CSR) uses its random edge in round r",
+// i.e. the sender's own Philox draw U(deg) == deg - 1 (SRS v1 B.4,
+// Program.fs:125-128).  One dense pass over the in-lists (coalesced sender
+// loads, 4 interleaved Philox chains per lane, one ballot word per 64 edges),
+// so the round kernel's in-edge pass reads bits instead of redrawing on its
+// latency-critical path.  Exits at once while some node is inactive (the round
+// kernel then reads the ballot bitmap of the senders' directions).
+template <bool PACKED>
+__global__ __launch_bounds__(256) void k_edge_decide(const uint32_t* __restrict__ src, uint32_t nedges,
+                                                     uint64_t* __restrict__ eb, Geom G, uint32_t k0, uint32_t k1,
+                                                     const Ctl* ctl, uint32_t r) {
+    if (ld_agent(&ctl->done) || !ld_agent(&ctl->all_active)) return;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = (blockIdx.x * 256u + threadIdx.x) >> 6, nwaves = gridDim.x * 4u;
+    for (uint64_t base = (uint64_t)wave * 256u; base < nedges; base += (uint64_t)nwaves * 256u) {
+        uint32_t raw[4], node[4], x[4], y[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint64_t e = base + k * 64u + lane;
+            raw[k] = e < nedges ? __builtin_nontemporal_load(src + e) : 0u;
+            node[k] = PACKED ? raw[k] & 0x3FFFFFFFu : raw[k];
+        }
+        philox2_batch<4>(node, r, S_PUSHSUM, k0, k1, x, y);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint64_t e = base + k * 64u + lane;
+            const uint32_t di = PACKED ? (raw[k] >> 30) + 4u : popc6(present_mask<IMP3D>(node[k], G)) + 1u;
+            const unsigned long long bal = __ballot(e < nedges && uniform_from(x[k], y[k], di) == di - 1u);
+            if (lane == (uint32_t)k) eb[(base >> 6) + k] = bal;
+        }
     }
 }
 
@@ -928,6 +996,7 @@ RoundArgs make_round_args(const DevState& S, uint32_t round) {
     a.stage_cap = S.tile_stage_cap;
     a.wx = S.tile_wx;
     a.fuse = S.fuse_finalize;
+    a.eb = S.eb;
     return a;
 }
 
@@ -935,6 +1004,16 @@ hipError_t launch_round_tile(const DevState& S, uint32_t round, int grid, hipStr
     const RoundArgs a = make_round_args(S, round);
     const dim3 g(grid), b(TPB);
     const bool remote = S.rtag != nullptr;  // Imp3D slabs of a multi-rank run
+    if (S.alg == PUSHSUM && S.topo == IMP3D && S.eb) {  // this round's edge decisions first
+        const uint32_t* src = S.in_srcd ? S.in_srcd : S.in_src;
+        const dim3 ge(std::min<uint32_t>(4096u, (S.nedges + 1023u) / 1024u + 1u));
+        if (S.in_srcd)
+            hipLaunchKernelGGL((k_edge_decide<true>), ge, dim3(256), 0, st, src, S.nedges, S.eb, S.G, S.k0, S.k1, S.ctl,
+                               round);
+        else
+            hipLaunchKernelGGL((k_edge_decide<false>), ge, dim3(256), 0, st, src, S.nedges, S.eb, S.G, S.k0, S.k1,
+                               S.ctl, round);
+    }
     if (S.alg == PUSHSUM) {
         switch (S.topo) {
             case LINE: hipLaunchKernelGGL((k_ps_tile<LINE, false>), g, b, 0, st, a, round); break;

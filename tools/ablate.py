@@ -22,6 +22,8 @@ VARIANTS = {  # name -> extra -D flags for gp_round.hip
     "base": [],
     "stamps": ["-DGP_STAMPS=1"],
     "nofma": ["-DGP_FMA_FOLD=0"],
+    "lmask": ["-DGP_LMASK=1"],
+    "noz": ["-DGP_ABL_NOZ=1"],
     "ng2": ["-DGP_NGROUP=2"],
     "n2m6": ["-DGP_NPT=2", "-DGP_MINB=6"],
     "n2m5": ["-DGP_NPT=2", "-DGP_MINB=5"],
