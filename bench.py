@@ -12,9 +12,10 @@ then W warmup rounds; convergence is never reached inside the timed window.
 
 One JSON line on stdout (rank 0).  `roofline` is measured live: HIP events on
 the library's stream bracket every round kernel (k_pushsum_round<IMP3D>); its
-algorithmic bytes per node-round are DESIGN.md §4's figure.  `traffic` comes
-from the committed rocprofv3 PMC summary (profiles/) when it matches the
-workload.  `cpu_baseline` times the SRS v1 C oracle on the host cores over a
+algorithmic bytes per node-round are DESIGN.md §4's figure.  `traffic` is
+measured in the same run: before the bench, the workload is re-run as a child
+under three rocprofv3 --pmc passes and the round kernel's HBM bytes are read
+from the L2's request-size counters (tools/hbm_traffic.py).  `cpu_baseline` times the SRS v1 C oracle on the host cores over a
 bounded sample of the same workload (steady state, smaller lattice).
 
 Multi-GPU (N > 1, launched by torch.distributed.run): one process per GPU,
@@ -50,17 +51,34 @@ def preroll(sim, population, cap=2000):
     raise RuntimeError("activation did not complete within %d rounds" % cap)
 
 
-def traffic_from_profiles(workload_key):
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(path):
-        return None
+def measure_traffic(args):
+    """HBM bytes per launch of the round kernel, measured in this run: the same
+    workload re-run as a child under three rocprofv3 --pmc passes (request-size
+    counters, tools/hbm_traffic.py; calibrated on known byte counts in
+    profiles/r02/calib/).  Runs before this process touches the GPU.  Returns
+    (record, None) or (None, reason)."""
+    import shutil
+    import tempfile
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import hbm_traffic
+    if shutil.which("rocprofv3") is None:
+        return None, "rocprofv3 not found"
+    steps = 6
+    cmd = [sys.executable, os.path.abspath(__file__), "--no-cpu", "--no-traffic", "--steps", str(steps), "--warmup",
+           "0", "--nodes", str(args.nodes), "--topology", args.topology, "--algorithm", args.algorithm,
+           "--seed", str(args.seed)]
+    root = tempfile.mkdtemp(prefix="gp_traffic_", dir=os.environ.get("TMPDIR", "/tmp"))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     try:
-        with open(path) as f:
-            d = json.load(f)
-    except (OSError, ValueError):
-        return None
-    rec = d.get(workload_key)
-    return rec.get("hbm_bytes_per_launch") if rec else None
+        dirs = hbm_traffic.run_passes(cmd, root, timeout=args.traffic_timeout, env=env)
+        rec = hbm_traffic.bytes_per_dispatch(dirs, args.traffic_kernel, last=steps)
+    except Exception as e:  # noqa: BLE001 -- reported in the JSON line, never fatal
+        return None, f"{type(e).__name__}: {e}"
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
+    if rec is None:
+        return None, f"no '{args.traffic_kernel}' dispatches in the counter output"
+    return rec, None
 
 
 def cpu_baseline(args):
@@ -107,6 +125,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--converge", action="store_true", help="also run a fresh simulation to convergence")
+    ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 HBM-traffic passes")
+    ap.add_argument("--traffic-kernel", default="k_ps_tile", help="round-kernel name substring in the counters")
+    ap.add_argument("--traffic-timeout", type=float, default=240.0)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -114,6 +135,12 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    traffic, traffic_note = None, "not measured (multi-GPU run)" if world > 1 else "not measured (--no-traffic)"
+    if world == 1 and not args.no_traffic:
+        t_tr = time.perf_counter()
+        traffic, traffic_note = measure_traffic(args)
+        log(f"[bench] HBM traffic passes: {time.perf_counter() - t_tr:.1f} s, "
+            f"{'ok' if traffic else traffic_note}")
     from gossipprotocol_amd import Simulation
     from gossipprotocol_amd import _lib as L
 
@@ -162,8 +189,6 @@ def main():
     value = P * args.steps / elapsed
     avg_ms = kms / max(1, launches)
     achieved = bytes_per_node * local_nodes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-    key = f"{args.topology}-{args.algorithm}-{args.nodes}-gpus{world}"
-    traffic = traffic_from_profiles(key)
     out = {
         "metric": METRIC,
         "value": value,
@@ -190,12 +215,24 @@ def main():
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBPS,
-            "traffic": traffic,
+            "traffic": traffic["total_bytes"] if traffic else None,
             "alg_bytes_per_node_round": bytes_per_node,
             "kernel_avg_ms": avg_ms,
         },
         "cpu_baseline": None,
     }
+    if traffic:
+        alg = bytes_per_node * local_nodes
+        out["roofline"]["traffic_detail"] = {
+            "method": "this run: rocprofv3 --pmc request-size counters (128/64/32-B TCC_EA0_RDREQ) + WRITE_SIZE, "
+                      "3 passes over the same workload, last %d round kernels (tools/hbm_traffic.py)" % traffic["dispatches"],
+            "read_bytes": traffic["read_bytes"], "write_bytes": traffic["write_bytes"],
+            "traffic_over_algorithmic": traffic["total_bytes"] / alg,
+            "traffic_gbps": traffic["total_bytes"] / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else None,
+            "fetch_size_equivalent_bytes": traffic["fetch_size_equivalent_bytes"],
+        }
+    else:
+        out["roofline"]["traffic_detail"] = {"method": traffic_note}
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args)
     if rank == 0 and world == 1 and args.converge:

@@ -886,9 +886,13 @@ int build_sim(gp_sim* s) {
         sl.S.tile_stage_cap = 0xFFFFFFFFu;
         // single-rank lattice push-sum: the round kernel's last block closes the
         // round (no injector, nothing to exchange), saving a k_finalize launch per round
+        // (2: arrivals sharded over 8 counters; a single counter -- 1, experiments
+        // only -- serialises ~16k returning atomics per round: measured 1.93 vs
+        // 0.40 ms/round at P = 2.7e7, profiles/r02/round_close.txt)
         sl.S.fuse_finalize = (s->mode == MODE_SINGLE && s->cfg.algorithm == GP_PUSHSUM &&
-                              s->cfg.topology != GP_FULL && kernel == KERNEL_TILE) ? 1u : 0u;
+                              s->cfg.topology != GP_FULL && kernel == KERNEL_TILE) ? 2u : 0u;
 #ifdef GP_EXPERIMENTS
+        if (const char* e = std::getenv("GP_FUSE")) sl.S.fuse_finalize = sl.S.fuse_finalize ? (uint32_t)(e[0] - '0') : 0u;
         if (const char* e = std::getenv("GP_STAGE_CAP")) sl.S.tile_stage_cap = (uint32_t)std::max(0, std::atoi(e));
 #endif
         if ((rc = alloc_slab(s, sl, sl.rank))) return rc;

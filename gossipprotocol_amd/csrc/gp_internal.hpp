@@ -32,6 +32,12 @@ struct Ctl {
     unsigned int blocks_done;         // fused finalize: blocks of the current round kernel that have finished
     unsigned int tiny;                // push-sum: some (s, w) fell below 2^-1020 (the FMA fold's exactness bound)
     unsigned int pad_;
+    // fused round close, sharded: blocks b with b % 8 == k count into shard k
+    // (one 256-byte line each, so the shards' atomics do not queue on one line)
+    struct alignas(256) Shard {
+        unsigned long long alerts, active;
+        unsigned int done, pad_[3];
+    } shard[8];
     unsigned long long hist[HIST];    // alerts of round r at hist[r % HIST]
 };
 
@@ -73,6 +79,42 @@ __device__ inline void block_done_close(Ctl* ctl, uint32_t P, uint32_t T, uint32
     const unsigned long long a = __hip_atomic_exchange(&ctl->round_alerts, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long na = __hip_atomic_exchange(&ctl->round_active, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     close_round_ctl(ctl, P, T, round, a, na);
+}
+
+// block_done_close with the arrivals spread over 8 shards (block b counts into
+// shard b % 8 -- on MI355X the blocks of one XCD): one word takes ~88 returning
+// atomics per microsecond, so a grid of 16384 blocks queued on a single word
+// holds its blocks' CU slots for a large part of a round.  The last block of a
+// shard forwards the shard's sums and arrives at the global counter; the last
+// of those closes the round.  Thread 0, with the block's counts x (alerts) and
+// y (newly active).
+__device__ inline void block_done_close_sharded(Ctl* ctl, uint32_t P, uint32_t T, uint32_t round, uint32_t x,
+                                                uint32_t y) {
+    const uint32_t G = gridDim.x, k = blockIdx.x & 7u;
+    Ctl::Shard* sh = &ctl->shard[k];
+    unsigned long long d = 0;
+    if (x) d += __hip_atomic_fetch_add(&sh->alerts, (unsigned long long)x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (y) d += __hip_atomic_fetch_add(&sh->active, (unsigned long long)y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("" ::"v"(d));
+    __builtin_amdgcn_s_waitcnt(0);
+    const uint32_t members = (G - k + 7u) / 8u;  // blocks with b % 8 == k
+    const unsigned int prev = __hip_atomic_fetch_add(&sh->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev != members - 1) return;
+    __hip_atomic_store(&sh->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long a = __hip_atomic_exchange(&sh->alerts, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long na = __hip_atomic_exchange(&sh->active, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    d = 0;
+    if (a) d += __hip_atomic_fetch_add(&ctl->round_alerts, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (na) d += __hip_atomic_fetch_add(&ctl->round_active, na, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("" ::"v"(d));
+    __builtin_amdgcn_s_waitcnt(0);
+    const uint32_t shards = G < 8u ? G : 8u;
+    const unsigned int p2 = __hip_atomic_fetch_add(&ctl->blocks_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (p2 != shards - 1) return;
+    __hip_atomic_store(&ctl->blocks_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long ga = __hip_atomic_exchange(&ctl->round_alerts, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long gna = __hip_atomic_exchange(&ctl->round_active, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    close_round_ctl(ctl, P, T, round, ga, gna);
 }
 
 // Node state in HBM (structure of arrays, single GPU / one slab).

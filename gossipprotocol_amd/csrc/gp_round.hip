@@ -58,8 +58,8 @@ namespace gp {
 #ifndef GP_LMASK
 #define GP_LMASK 0       // lattice gathers exec-masked to the lanes with a sender (else: zero sentinel)
 #endif
-#ifndef GP_ABL_NOZ
-#define GP_ABL_NOZ 0     // ablation (wrong results, timing only): skip the z+-1 lattice gathers
+#ifndef GP_ABL_DIRS
+#define GP_ABL_DIRS 0    // ablation (wrong results, timing only): bit d set = skip the lattice gathers of slot d
 #endif
 #ifndef GP_STAMPS
 #define GP_STAMPS 0      // diagnostics (experiments build): per-phase cycle counts of the push-sum tile kernel
@@ -300,11 +300,8 @@ __device__ __forceinline__ void st_stream(uint32_t* p, uint32_t v) {
 //   4. next-round directions of the thread's NPT nodes as one Philox batch;
 //      node bytes out as words, random-edge bits as one ballot per wave.
 template <int TOPO, bool REMOTE>
-__global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t r) {
-    __shared__ TileLdsP L;
-    Ctl* ctl = a.ctl;
-    if (ld_agent(&ctl->done)) return;
-    const bool all_active = ld_agent(&ctl->all_active) != 0;
+__device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLdsP& L, bool all_active, uint32_t& alerts,
+                                         uint32_t& newly, bool& tiny) {
     const double2* __restrict__ swc = a.swc;
     double2* __restrict__ swn = a.swn;
     const uint64_t* __restrict__ rbc = a.rbc;
@@ -315,8 +312,6 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
     const uint32_t H = TOPO == LINE ? 1u : G.g;
     constexpr int FU = SLOT_FU;
     const uint32_t cap = min((uint32_t)SLOTS, a.stage_cap);
-    uint32_t alerts = 0, newly = 0;
-    bool tiny = false;
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
 
     // loaded one tile ahead: the next tile's in-edge range (two uniform loads)
@@ -533,7 +528,7 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
                     gfrom[h] = from;
 #pragma unroll
                     for (uint32_t d = 0; d < ND; ++d)
-                        if (GP_ABL_NOZ && d >= 4) {  // ablation (timing only): no z+-1 gathers
+                        if ((GP_ABL_DIRS >> d) & 1) {  // ablation (timing only): no gathers in slot d
                             m[h][d] = make_double2(0.0, 0.0);
                         } else if (GP_LMASK) {  // only lanes with a sender load (exec-masked gather)
                             m[h][d] = make_double2(0.0, 0.0);
@@ -719,43 +714,71 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
         // bits / msg / rows / xm / xp / off, none of which this byte output reads,
         // and its node phase writes L.out only after its staging barrier
     }
-    if (__ballot(tiny) && lane == 0) atomicOr(&ctl->tiny, 1u);
-    // block reduction of alerts / newly active
-    uint32_t x = alerts, y = newly;
+#if GP_STAMPS
+    if (threadIdx.x == 0)
+        for (int q = 0; q < 7; ++q) atomicAdd(&gp_stamp_acc[q], (unsigned long long)ph[q]);
+#endif
+}
+
+// Block sums of this block's alerts / newly active nodes (valid in thread 0).
+// Uses L.red; the barrier also orders the block's last byte output before any
+// later LDS reuse.
+__device__ __forceinline__ void block_counts(uint32_t (*red)[TPB / 64], uint32_t& x, uint32_t& y) {
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         x += __shfl_xor(x, o, 64);
         y += __shfl_xor(y, o, 64);
     }
     if (lane == 0) {
-        L.red[0][wv] = x;
-        L.red[1][wv] = y;
+        red[0][wv] = x;
+        red[1][wv] = y;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         x = 0;
         y = 0;
         for (int w = 0; w < TPB / 64; ++w) {
-            x += L.red[0][w];
-            y += L.red[1][w];
+            x += red[0][w];
+            y += red[1][w];
         }
-        if (a.fuse) {
-            // returning atomics: both counts are performed before the block arrives
-            unsigned long long d = 0;
-            if (x) d += __hip_atomic_fetch_add(&ctl->round_alerts, (unsigned long long)x, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-            if (y) d += __hip_atomic_fetch_add(&ctl->round_active, (unsigned long long)y, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-            asm volatile("" ::"v"(d));
-            __builtin_amdgcn_s_waitcnt(0);
+    }
+}
+
+// Thread 0: add the block's counts to the round accumulators with returning
+// atomics and wait for them, so they are performed before the block arrives
+// at the round close.
+__device__ __forceinline__ void add_round_counts(Ctl* ctl, uint32_t x, uint32_t y) {
+    unsigned long long d = 0;
+    if (x) d += __hip_atomic_fetch_add(&ctl->round_alerts, (unsigned long long)x, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+    if (y) d += __hip_atomic_fetch_add(&ctl->round_active, (unsigned long long)y, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("" ::"v"(d));
+    __builtin_amdgcn_s_waitcnt(0);
+}
+
+template <int TOPO, bool REMOTE>
+__global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t r) {
+    __shared__ TileLdsP L;
+    Ctl* ctl = a.ctl;
+    if (ld_agent(&ctl->done)) return;
+    const bool all_active = ld_agent(&ctl->all_active) != 0;
+    uint32_t alerts = 0, newly = 0;
+    bool tiny = false;
+    ps_tiles<TOPO, REMOTE>(a, r, L, all_active, alerts, newly, tiny);
+    if (__ballot(tiny) && (threadIdx.x & 63u) == 0) atomicOr(&ctl->tiny, 1u);
+    block_counts(L.red, alerts, newly);
+    if (threadIdx.x == 0) {
+        if (a.fuse == 2) {
+            block_done_close_sharded(ctl, a.G.P, a.G.T, r, alerts, newly);
+        } else if (a.fuse) {
+            add_round_counts(ctl, alerts, newly);
             block_done_close(ctl, a.G.P, a.G.T, r);
         } else {
-            if (x) atomicAdd(&ctl->round_alerts, (unsigned long long)x);
-            if (y) atomicAdd(&ctl->round_active, (unsigned long long)y);
+            if (alerts) atomicAdd(&ctl->round_alerts, (unsigned long long)alerts);
+            if (newly) atomicAdd(&ctl->round_active, (unsigned long long)newly);
         }
-#if GP_STAMPS
-        for (int q = 0; q < 7; ++q) atomicAdd(&gp_stamp_acc[q], (unsigned long long)ph[q]);
-#endif
     }
 }
 

@@ -258,3 +258,33 @@ def test_tile_unstaged_path_parity(cap, monkeypatch):
         assert_same_state("push-sum", sim.state(), orc.state())
         done += k
     sim.close()
+
+
+
+CLOSE_CASES = [  # (num_nodes, topology, seed, rounds, checkpoint): push-sum, one rank
+    (2000000, "3D", 3, 120, 60),      # ~2000 blocks: uneven shard sizes (blockIdx % 8)
+    (343000, "Imp3D", 6, 300, 100),
+    (5000, "line", 8, 2000, 1000),    # one tile, a grid of 8 blocks (one per shard)
+]
+
+
+@pytest.mark.parametrize("n,topo,seed,rounds,chk", CLOSE_CASES, ids=lambda v: str(v))
+@pytest.mark.parametrize("fuse", ["0", "1", "2"])
+def test_round_close_parity(fuse, n, topo, seed, rounds, chk, monkeypatch):
+    """Single-rank lattice push-sum closes its rounds three ways (experiments build,
+    GP_FUSE): 0 a separate k_finalize launch, 1 the round kernel's last block via
+    one arrival counter, 2 (product default) arrivals sharded over 8 counters whose
+    last blocks forward to the global one.  Per-round alerts and full state
+    bit-exact vs the oracle at every checkpoint, through convergence for line."""
+    monkeypatch.setenv("GP_FUSE", fuse)
+    sim, orc = Sim(n, topo, "push-sum", seed=seed, experimental=True), Oracle(n, topo, "push-sum", seed)
+    done = 0
+    while done < rounds and orc.alerts_total < orc.T:
+        k = min(chk, rounds - done)
+        ga, oa = sim.step(k), orc.step(k)
+        assert ga == oa, f"alerts differ in rounds {done}..{done + k}"
+        assert_same_state("push-sum", sim.state(), orc.state())
+        done += k
+    assert sim.rounds == orc.rounds
+    sim.close()
+    orc.close()

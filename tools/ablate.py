@@ -23,7 +23,10 @@ VARIANTS = {  # name -> extra -D flags for gp_round.hip
     "stamps": ["-DGP_STAMPS=1"],
     "nofma": ["-DGP_FMA_FOLD=0"],
     "lmask": ["-DGP_LMASK=1"],
-    "noz": ["-DGP_ABL_NOZ=1"],
+    "noz": ["-DGP_ABL_DIRS=48"],
+    "nox": ["-DGP_ABL_DIRS=3"],
+    "noy": ["-DGP_ABL_DIRS=12"],
+    "nolat": ["-DGP_ABL_DIRS=63"],
     "ng2": ["-DGP_NGROUP=2"],
     "n2m6": ["-DGP_NPT=2", "-DGP_MINB=6"],
     "n2m5": ["-DGP_NPT=2", "-DGP_MINB=5"],

@@ -45,6 +45,21 @@ def main():
     print(f"{topo} {alg} P={P} create {tc:.2f}s preroll {pre} rounds {tp:.2f}s ({pms / max(pk, 1):.2f} ms/kernel) | "
           f"{name}: {ms / kk:.3f} ms/round kernel, wall {wall * 1e3 / len(got):.3f} ms/round, "
           f"{P * len(got) / wall:.3e} node-updates/s, alg {bpn * P / (ms / kk * 1e-3) / 1e9:.0f} GB/s", flush=True)
+    s.close()
+    if P <= 2 * 10**7 and os.environ.get("GP_NOEV", "1") != "0":
+        # small populations: wall per round without per-round HIP events (their
+        # recording is itself a visible share of a tens-of-microseconds round)
+        s = Simulation(n, topo, alg, experimental=exp)
+        pre2 = 0
+        while pre2 < pre:
+            pre2 += len(s.step(min(8, pre - pre2)))
+        s.sync()
+        t = time.perf_counter()
+        got = s.step(k)
+        s.sync()
+        wall = time.perf_counter() - t
+        print(f"  no events: wall {wall * 1e3 / len(got):.4f} ms/round over {len(got)} rounds", flush=True)
+        s.close()
 
 
 if __name__ == "__main__":
