@@ -277,6 +277,8 @@ int alloc_slab(gp_sim* s, Slab& sl, int r) {
     const size_t next = (size_t)(S.ext_hi - S.base) + 1024;  // node arrays (+ word-I/O padding)
     const size_t nl = S.nloc;
     if ((rc = dev_alloc_t(s, &S.ctl, 1))) return rc;
+    if ((rc = dev_alloc_t(s, &S.tq, 2 * 8 * TQ_STRIDE))) return rc;
+    HIP_TRY(hipMemsetAsync(S.tq, 0, sizeof(uint32_t) * 2 * 8 * TQ_STRIDE, s->stream));
     if (S.alg == PUSHSUM) {
         if ((rc = dev_alloc_t(s, &S.sw[0], next)) || (rc = dev_alloc_t(s, &S.sw[1], next)) ||
             (rc = dev_alloc_t(s, &S.nb[0], next)))
@@ -855,11 +857,20 @@ void choose_kernel(gp_sim* s, int64_t nloc_max, int& kernel, uint32_t& col_xsegs
     // tile walk: x-windows of 8 planes once every XCD gets a few windows (measured,
     // profiles/r01: 18.2 -> 17.2 ms/round at P = 1e9), else XCD-contiguous eighths
     walk = (lattice && g / s->world >= 64) ? 2u : 0u;
+    // push-sum: the same x-windows claimed from per-XCD counters on exactly the
+    // resident grid (walk 3; measured, profiles/r02/walk3.txt)
+    if (walk == 2 && kernel == KERNEL_TILE && cfg->algorithm == GP_PUSHSUM) walk = 3;
     wx = 8;
 #ifdef GP_EXPERIMENTS
     if (const char* e = std::getenv("GP_WALK")) walk = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("GP_WX")) wx = (uint32_t)std::max(1, std::atoi(e));
 #endif
+    if (walk == 3) {
+        const int topo = cfg->topology == GP_LINE ? LINE : cfg->topology == GP_3D ? GRID3D : IMP3D;
+        const int64_t res = ps_tile_resident_blocks(topo, s->world > 1 && topo == IMP3D, s->device) / 8 * 8;
+        if (res >= 8) s->grid = (int)std::min<int64_t>(s->grid, res);
+        else walk = 2;
+    }
 }
 
 // Everything after the handle exists: slabs, topology, initial state, round 0.

@@ -169,7 +169,11 @@ struct DevState {
     // edge-decision bitmap (k_edge_decide), one bit per in-edge
     uint32_t nedges;
     uint64_t* eb;
+    // walk 3 (dynamic tile queue): per round parity, 8 per-XCD item counters,
+    // TQ_STRIDE words apart (one 256-byte line each)
+    uint32_t* tq;
 };
+constexpr int TQ_STRIDE = 64;
 
 // Arguments of the tiled round kernels (gp_round.hip): only what they read.
 struct RoundArgs {
@@ -189,11 +193,14 @@ struct RoundArgs {
     Geom G;
     uint32_t k0, k1, seed_node, ntiles;
     uint32_t lo, nloc, ext_lo, ext_hi;  // owned ids [lo, lo + nloc); arrays hold [ext_lo, ext_hi)
-    uint32_t walk;  // 0: XCD-contiguous eighths, 1: one global sweep (tile t -> block t % grid), 2: x-windows
+    uint32_t walk;  // 0: XCD-contiguous eighths, 1: one global sweep (tile t -> block t % grid), 2: x-windows,
+                    // 3: x-windows claimed from per-XCD counters (k_ps_tile)
     uint32_t wx;    // walk 2: planes per x-window
     uint32_t stage_cap;  // k_ps_tile: tiles with more in-edges take the unstaged path (tests force it)
     uint32_t fuse;       // k_ps_tile: the last block closes the round (no k_finalize launch)
     const uint64_t* eb;  // Imp3D: this round's edge decisions (k_edge_decide), or null
+    uint32_t* tq;        // walk 3: this round's 8 per-XCD tile-item counters (TQ_STRIDE apart)
+    uint32_t* tq_next;   // walk 3: the next round's counters, zeroed by block 0 this round
 };
 
 enum KernelVariant : int { KERNEL_WAVE = 0, KERNEL_TILE = 1, KERNEL_COL = 2 };
@@ -236,6 +243,7 @@ hipError_t launch_col_rbits_init(const DevState& S, hipStream_t st);
 // ---- tiled round kernels (gp_round.hip)
 uint32_t rbits_words_for(uint32_t lo, uint32_t nloc);
 hipError_t launch_round_tile(const DevState& S, uint32_t round, int grid, hipStream_t st);
+int ps_tile_resident_blocks(int topo, bool remote, int device);
 hipError_t launch_rbits_init(const DevState& S, int grid, hipStream_t st);
 hipError_t launch_pack_src_deg(const uint32_t* src, uint32_t* out, uint32_t n, const Geom& G, int grid,
                                hipStream_t st);

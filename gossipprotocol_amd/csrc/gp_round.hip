@@ -111,6 +111,7 @@ struct TileLdsP {
     double2 msg[SLOTS];               // edge q's message at slot q
     uint32_t out[TILE / 4];
     uint32_t red[2][TPB / 64];
+    uint32_t qn[2];                   // walk 3: the block's next item, by iteration parity
 };
 
 
@@ -186,14 +187,23 @@ __device__ unsigned long long gp_stamp_acc[8];
 //     in-plane position of ~wx consecutive planes (x+-1 neighbours) and of a few
 //     consecutive k (y+-1 rows), so lattice gathers and the x+-1 byte planes hit
 //     the XCD's L2 instead of HBM.
+//   walk 3 (k_ps_tile): walk 2's items, claimed in order from a per-XCD counter
+//     (one returning atomic per tile, issued a tile ahead) instead of the
+//     static stride, on a grid of exactly the resident blocks.  The tiles an XCD
+//     has in flight are then always ~160 consecutive items (20 in-plane
+//     positions of 8 planes), and the tiles just finished are their y-1 / x+-1
+//     neighbours; the static stride keeps items 2048 apart in flight.
 struct TileWalk {
     uint32_t t, end, step;
-    // walk 2 only
+    // walk 2 / 3
     uint32_t mode, tb, tend, g2, x0, xa, nxa, kp, nwin;
+    uint32_t* qc;  // walk 3: this XCD's item counter
     __device__ TileWalk(const RoundArgs& a) {
         const uint32_t G = gridDim.x;
         mode = a.walk;
-        if (mode == 2 && a.G.g2 && G >= 8 && (G & 7) == 0) {
+        qc = nullptr;
+        if (mode == 3 && !(a.G.g2 && G >= 8 && (G & 7) == 0)) mode = 1;
+        if ((mode == 2 || mode == 3) && a.G.g2 && G >= 8 && (G & 7) == 0) {
             const uint32_t c = blockIdx.x & 7;
             g2 = a.G.g2;
             tb = a.lo / TILE;
@@ -208,6 +218,7 @@ struct TileWalk {
             t = blockIdx.x >> 3;
             end = nxa * kp;
             step = G >> 3;
+            if (mode == 3) qc = a.tq + c * TQ_STRIDE;
         } else if (mode == 0 && G >= 8 && (G & 7) == 0) {
             mode = 0;
             const uint32_t x = blockIdx.x & 7, k = blockIdx.x >> 3;
@@ -228,7 +239,7 @@ struct TileWalk {
     }
     // tile (relative to lo / TILE) of walk item t; false: empty item (block-uniform)
     __device__ __forceinline__ bool tile(uint32_t& rel) const {
-        if (mode != 2) {
+        if (mode != 2 && mode != 3) {
             rel = t;
             return true;
         }
@@ -323,9 +334,33 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
 #if GP_STAMPS
     uint64_t ph[7] = {0, 0, 0, 0, 0, 0, 0};
 #endif
-    for (TileWalk tw(a); tw.t < tw.end; tw.t += tw.step) {
+    TileWalk tw(a);
+    const bool dyn = tw.mode == 3;  // block-uniform
+    uint32_t it = 0;                // iteration: parity selects the LDS slot of the next claim
+    if (dyn) {
+        if (blockIdx.x == 0 && threadIdx.x < 8) a.tq_next[threadIdx.x * TQ_STRIDE] = 0u;  // next round's counters
+        if (threadIdx.x == 0) L.qn[0] = atomicAdd(tw.qc, 1u);
+        __syncthreads();
+        tw.t = L.qn[0];
+        ++it;
+    }
+    while (tw.t < tw.end) {
         uint32_t ti;
-        if (!tw.tile(ti)) continue;
+        // walk 3: thread 0 claims the next item now; it is published in LDS at the
+        // staging barrier (which waits for the atomic anyway)
+        uint32_t claim = 0;
+        if (dyn && threadIdx.x == 0) claim = atomicAdd(tw.qc, 1u);
+        if (!tw.tile(ti)) {  // an empty item (a plane has fewer tiles than kp)
+            if (dyn) {
+                if (threadIdx.x == 0) L.qn[it & 1] = claim;
+                __syncthreads();
+                tw.t = L.qn[it & 1];
+                ++it;
+            } else {
+                tw.t += tw.step;
+            }
+            continue;
+        }
         GP_STAMP(t0);
         // tiles sit on global multiples of TILE (4-aligned word I/O, 64-aligned
         // ballot words); the slab's first and last tile may be partial
@@ -346,7 +381,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
         const uint32_t cnt = e_hi - e_lo;
         const bool staged = cnt <= cap;
         bool pf_next = false;
-        if (TOPO == IMP3D) {
+        if (TOPO == IMP3D && !dyn) {
             TileWalk nw = tw;
             nw.t += nw.step;
             uint32_t nti;
@@ -458,8 +493,27 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
         int o_off = 0;  // L.off[jl + o_off] = in_off[T + jl]
         if (TOPO == IMP3D) o_off = (int)dma_stage_words(L.off, a.in_off, j0, j1 + 1) - (int)(j0 - T);
         GP_STAMP(t2);
+        if (dyn && threadIdx.x == 0) L.qn[it & 1] = claim;
         __syncthreads();  // staging copies, in-edge bitmap and gathered messages retired
         GP_STAMP(t3);
+        uint32_t t_next = tw.t + tw.step;
+        if (dyn) {
+            t_next = L.qn[it & 1];
+            ++it;
+            // the next tile's in-edge range (two uniform loads, consumed next tile)
+            if (TOPO == IMP3D) {
+                TileWalk nw = tw;
+                nw.t = t_next;
+                uint32_t nti;
+                pf_tile = 0xFFFFFFFFu;
+                if (nw.t < nw.end && nw.tile(nti)) {
+                    const uint32_t nT = (a.lo / TILE + nti) * TILE;
+                    pf_lo = a.in_off[max(a.lo, nT)];
+                    pf_hi = a.in_off[min(a.lo + a.nloc, nT + TILE)];
+                    pf_tile = nti;
+                }
+            }
+        }
 
         // per node, 16 bits (two nodes per word): bits 0-5 lattice mask, bit 6 draw a
         // next-round direction, bits 7-10 the node byte's flag bits 3-6
@@ -713,6 +767,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
         // no barrier here: the next tile's in-edge pass and staging copies write
         // bits / msg / rows / xm / xp / off, none of which this byte output reads,
         // and its node phase writes L.out only after its staging barrier
+        tw.t = t_next;
     }
 #if GP_STAMPS
     if (threadIdx.x == 0)
@@ -1020,7 +1075,22 @@ RoundArgs make_round_args(const DevState& S, uint32_t round) {
     a.wx = S.tile_wx;
     a.fuse = S.fuse_finalize;
     a.eb = S.eb;
+    a.tq = S.tq + (round & 1) * 8 * TQ_STRIDE;
+    a.tq_next = S.tq + ((round + 1) & 1) * 8 * TQ_STRIDE;
     return a;
+}
+
+// Resident 256-thread blocks of the push-sum tile kernel on this device (walk 3
+// runs exactly that grid); 0 if unknown.
+int ps_tile_resident_blocks(int topo, bool remote, int device) {
+    const void* f = topo == LINE     ? reinterpret_cast<const void*>(&k_ps_tile<LINE, false>)
+                    : topo == GRID3D ? reinterpret_cast<const void*>(&k_ps_tile<GRID3D, false>)
+                    : remote         ? reinterpret_cast<const void*>(&k_ps_tile<IMP3D, true>)
+                                     : reinterpret_cast<const void*>(&k_ps_tile<IMP3D, false>);
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, TPB, 0) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
+    return per_cu * cus;
 }
 
 hipError_t launch_round_tile(const DevState& S, uint32_t round, int grid, hipStream_t st) {
