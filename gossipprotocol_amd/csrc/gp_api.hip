@@ -907,6 +907,15 @@ int build_sim(gp_sim* s) {
         if (const char* e = std::getenv("GP_STAGE_CAP")) sl.S.tile_stage_cap = (uint32_t)std::max(0, std::atoi(e));
 #endif
         if ((rc = alloc_slab(s, sl, sl.rank))) return rc;
+        if (sl.S.tile_walk == 3) {  // the tile list of the per-XCD queues
+            std::vector<uint32_t> list;
+            if (!build_walk_list(sl.S, list, sl.S.woff)) {
+                set_err("internal: walk-3 tile list does not cover the slab");
+                return GP_EINVAL;
+            }
+            if ((rc = dev_alloc_t(s, &sl.S.wtiles, list.size() + 1))) return rc;
+            HIP_TRY(hipMemcpy(sl.S.wtiles, list.data(), sizeof(uint32_t) * list.size(), hipMemcpyHostToDevice));
+        }
     }
     if (s->cfg.topology == GP_IMP3D && (rc = build_imp3d(s))) return rc;
     if ((s->cfg.topology == GP_IMP3D || s->cfg.topology == GP_FULL) && s->world > 1 && (rc = setup_exchange(s)))

@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "gp_device.hpp"
 
 namespace gp {
@@ -172,6 +174,10 @@ struct DevState {
     // walk 3 (dynamic tile queue): per round parity, 8 per-XCD item counters,
     // TQ_STRIDE words apart (one 256-byte line each)
     uint32_t* tq;
+    // walk 3: the slab's tiles (relative to lo / TILE) in visiting order, XCD c's
+    // items at [woff[c], woff[c + 1])
+    uint32_t* wtiles;
+    uint32_t woff[9];
 };
 constexpr int TQ_STRIDE = 64;
 
@@ -199,6 +205,8 @@ struct RoundArgs {
     uint32_t stage_cap;  // k_ps_tile: tiles with more in-edges take the unstaged path (tests force it)
     uint32_t fuse;       // k_ps_tile: the last block closes the round (no k_finalize launch)
     const uint64_t* eb;  // Imp3D: this round's edge decisions (k_edge_decide), or null
+    const uint32_t* wt;  // walk 3: tile list (DevState::wtiles), XCD c's items at [wo[c], wo[c + 1])
+    uint32_t wo[9];
     uint32_t* tq;        // walk 3: this round's 8 per-XCD tile-item counters (TQ_STRIDE apart)
     uint32_t* tq_next;   // walk 3: the next round's counters, zeroed by block 0 this round
 };
@@ -244,6 +252,7 @@ hipError_t launch_col_rbits_init(const DevState& S, hipStream_t st);
 uint32_t rbits_words_for(uint32_t lo, uint32_t nloc);
 hipError_t launch_round_tile(const DevState& S, uint32_t round, int grid, hipStream_t st);
 int ps_tile_resident_blocks(int topo, bool remote, int device);
+bool build_walk_list(const DevState& S, std::vector<uint32_t>& list, uint32_t woff[9]);
 hipError_t launch_rbits_init(const DevState& S, int grid, hipStream_t st);
 hipError_t launch_pack_src_deg(const uint32_t* src, uint32_t* out, uint32_t n, const Geom& G, int grid,
                                hipStream_t st);

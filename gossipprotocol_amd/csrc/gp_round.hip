@@ -22,6 +22,7 @@
 // Built with -ffp-contract=off: the fold must round exactly like the oracle.
 #include <algorithm>
 #include <type_traits>
+#include <vector>
 
 #include "gp_internal.hpp"
 
@@ -187,23 +188,36 @@ __device__ unsigned long long gp_stamp_acc[8];
 //     in-plane position of ~wx consecutive planes (x+-1 neighbours) and of a few
 //     consecutive k (y+-1 rows), so lattice gathers and the x+-1 byte planes hit
 //     the XCD's L2 instead of HBM.
-//   walk 3 (k_ps_tile): walk 2's items, claimed in order from a per-XCD counter
-//     (one returning atomic per tile, issued a tile ahead) instead of the
-//     static stride, on a grid of exactly the resident blocks.  The tiles an XCD
-//     has in flight are then always ~160 consecutive items (20 in-plane
+//   walk 3 (k_ps_tile): walk 2's items without the empty ones, listed per XCD
+//     at create time (DevState::wtiles, build_walk_list in gp_api.hip) and
+//     claimed in order from a per-XCD counter (one returning atomic per tile,
+//     issued a tile ahead) on a grid of exactly the resident blocks.  The tiles
+//     an XCD has in flight are then always ~160 consecutive items (20 in-plane
 //     positions of 8 planes), and the tiles just finished are their y-1 / x+-1
-//     neighbours; the static stride keeps items 2048 apart in flight.
+//     neighbours; walk 2's static stride keeps items 2048 apart in flight, and
+//     its item -> tile arithmetic (64-bit divisions) costs ~100 scalar
+//     instructions per tile and wave.
 struct TileWalk {
     uint32_t t, end, step;
-    // walk 2 / 3
+    // walk 2
     uint32_t mode, tb, tend, g2, x0, xa, nxa, kp, nwin;
-    uint32_t* qc;  // walk 3: this XCD's item counter
+    // walk 3: this XCD's item counter and tile list
+    uint32_t* qc;
+    const uint32_t* wl;
     __device__ TileWalk(const RoundArgs& a) {
         const uint32_t G = gridDim.x;
         mode = a.walk;
         qc = nullptr;
-        if (mode == 3 && !(a.G.g2 && G >= 8 && (G & 7) == 0)) mode = 1;
-        if ((mode == 2 || mode == 3) && a.G.g2 && G >= 8 && (G & 7) == 0) {
+        wl = nullptr;
+        if (mode == 3 && (a.wt == nullptr || G < 8 || (G & 7) != 0)) mode = 1;
+        if (mode == 3) {
+            const uint32_t c = blockIdx.x & 7;
+            qc = a.tq + c * TQ_STRIDE;
+            wl = a.wt + a.wo[c];
+            t = 0;
+            end = a.wo[c + 1] - a.wo[c];
+            step = 1;
+        } else if (mode == 2 && a.G.g2 && G >= 8 && (G & 7) == 0) {
             const uint32_t c = blockIdx.x & 7;
             g2 = a.G.g2;
             tb = a.lo / TILE;
@@ -218,7 +232,6 @@ struct TileWalk {
             t = blockIdx.x >> 3;
             end = nxa * kp;
             step = G >> 3;
-            if (mode == 3) qc = a.tq + c * TQ_STRIDE;
         } else if (mode == 0 && G >= 8 && (G & 7) == 0) {
             mode = 0;
             const uint32_t x = blockIdx.x & 7, k = blockIdx.x >> 3;
@@ -239,7 +252,11 @@ struct TileWalk {
     }
     // tile (relative to lo / TILE) of walk item t; false: empty item (block-uniform)
     __device__ __forceinline__ bool tile(uint32_t& rel) const {
-        if (mode != 2 && mode != 3) {
+        if (mode == 3) {
+            rel = wl[t];
+            return true;
+        }
+        if (mode != 2) {
             rel = t;
             return true;
         }
@@ -1075,9 +1092,44 @@ RoundArgs make_round_args(const DevState& S, uint32_t round) {
     a.wx = S.tile_wx;
     a.fuse = S.fuse_finalize;
     a.eb = S.eb;
+    a.wt = S.wtiles;
+    for (int c = 0; c <= 8; ++c) a.wo[c] = S.woff[c];
     a.tq = S.tq + (round & 1) * 8 * TQ_STRIDE;
     a.tq_next = S.tq + ((round + 1) & 1) * 8 * TQ_STRIDE;
     return a;
+}
+
+// Walk 3's visiting order (host, at create): walk 2's items (TileWalk) for each
+// of the 8 XCDs, empty items dropped -- every tile of the slab exactly once.
+// list: tiles relative to lo / TILE; woff[c]..woff[c + 1]: XCD c's items.
+bool build_walk_list(const DevState& S, std::vector<uint32_t>& list, uint32_t woff[9]) {
+    const uint64_t g2 = S.G.g2;
+    if (!g2 || S.nloc % g2 || S.lo % g2) return false;
+    const uint32_t tb = S.lo / TILE;
+    const uint32_t tend = (uint32_t)(((uint64_t)S.lo + S.nloc + TILE - 1) / TILE);
+    const uint32_t x0 = (uint32_t)(S.lo / g2), nx = (uint32_t)(S.nloc / g2);
+    const uint32_t kp = (uint32_t)((g2 + TILE - 1) / TILE + 1);
+    auto first = [&](uint32_t x) -> uint32_t {
+        return x <= x0 ? tb : (uint32_t)std::min<uint64_t>((x * g2 + TILE - 1) / TILE, tend);
+    };
+    list.clear();
+    for (uint32_t c = 0; c < 8; ++c) {
+        woff[c] = (uint32_t)list.size();
+        const uint32_t xa = x0 + (uint32_t)((uint64_t)nx * c / 8);
+        const uint32_t nxa = x0 + (uint32_t)((uint64_t)nx * (c + 1) / 8) - xa;
+        uint32_t nwin = S.tile_wx ? (nxa + S.tile_wx - 1) / S.tile_wx : 1u;
+        if (nwin == 0) nwin = 1;
+        for (uint32_t v = 0; v < nwin; ++v) {
+            const uint32_t xs = (uint32_t)((uint64_t)nxa * v / nwin), xe = (uint32_t)((uint64_t)nxa * (v + 1) / nwin);
+            for (uint32_t k = 0; k < kp; ++k)
+                for (uint32_t x = xa + xs; x < xa + xe; ++x) {
+                    const uint32_t ti = first(x) + k;
+                    if (ti < first(x + 1)) list.push_back(ti - tb);
+                }
+        }
+    }
+    woff[8] = (uint32_t)list.size();
+    return list.size() == (size_t)(tend - tb);
 }
 
 // Resident 256-thread blocks of the push-sum tile kernel on this device (walk 3

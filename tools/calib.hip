@@ -120,6 +120,43 @@ __global__ __launch_bounds__(TPB) void k_gatdma_nt(const double2* __restrict__ a
     if (lds[threadIdx.x].x == 1.25) out[0] = 1;
 }
 
+// random 16-B gathers by LDS-DMA, one per distinct line, with cache-policy bits
+// AUX (bit 0 sc0, bit 1 nt, bit 4 sc1): which policy fetches less than a line
+template <int AUX>
+__global__ __launch_bounds__(TPB) void k_gatdma_aux(const double2* __restrict__ a, uint32_t m, uint32_t* out) {
+    __shared__ double2 lds[TPB];
+    const uint32_t wv = threadIdx.x >> 6;
+    for (uint32_t k0 = blockIdx.x * TPB; k0 < m; k0 += gridDim.x * TPB) {
+        const uint32_t k = k0 + threadIdx.x;
+        if (k < m) __builtin_amdgcn_global_load_lds((gvoid_t*)(a + gidx<true>(k, 0)), (lvoid_t*)(lds + wv * 64), 16, 0, AUX);
+        __syncthreads();
+    }
+    if (lds[threadIdx.x].x == 1.25) out[0] = 1;
+}
+
+// uncached memory (hipDeviceMallocUncached): random 16-B reads into registers
+// and sparse 16-B stores (one row in every 8th line, i.e. partial lines)
+// (m must be a power of two: row 8 * ((k * odd) mod m) of a buffer of 8 m rows)
+__global__ __launch_bounds__(TPB) void k_gat16_uc(const double2* __restrict__ a, uint32_t m, double* out) {
+    double s = 0;
+    for (uint32_t k = blockIdx.x * TPB + threadIdx.x; k < m; k += gridDim.x * TPB) {
+        const double2 v = a[(size_t)((k * 0x9E3779B1u) & (m - 1u)) * 8u];
+        s += v.x + v.y;
+    }
+    if (s == 1.25) out[0] = s;
+}
+
+__global__ __launch_bounds__(TPB) void k_sc16_uc(double2* __restrict__ a, uint32_t m) {
+    for (uint32_t k = blockIdx.x * TPB + threadIdx.x; k < m; k += gridDim.x * TPB)
+        a[(size_t)k * 8] = make_double2((double)k, 1.0);
+}
+
+// the same sparse 16-B stores into ordinary (cached) memory
+__global__ __launch_bounds__(TPB) void k_sc16(double2* __restrict__ a, uint32_t m) {
+    for (uint32_t k = blockIdx.x * TPB + threadIdx.x; k < m; k += gridDim.x * TPB)
+        a[(size_t)k * 8] = make_double2((double)k, 1.0);
+}
+
 __global__ __launch_bounds__(TPB) void k_st16_nt(double2* __restrict__ a, size_t n) {
     for (size_t i = blockIdx.x * (size_t)TPB + threadIdx.x; i < n; i += (size_t)gridDim.x * TPB) {
         __builtin_nontemporal_store((double)i, &a[i].x);
@@ -206,6 +243,32 @@ int main() {
              hipLaunchKernelGGL((k_gatdma_nt<false>), dim3(grid), dim3(TPB), 0, 0, a, (uint32_t)N16, M,
                                 reinterpret_cast<uint32_t*>(dout));
          }));
+#define AUXCASE(X)                                                                                       \
+    flush();                                                                                             \
+    line("gatdma_aux" #X, ML * 16.0, 0, timeit([&] {                                                     \
+             hipLaunchKernelGGL((k_gatdma_aux<X>), dim3(grid), dim3(TPB), 0, 0, a, ML,                   \
+                                reinterpret_cast<uint32_t*>(dout));                                      \
+         }));
+    AUXCASE(0)
+    AUXCASE(1)
+    AUXCASE(3)
+    AUXCASE(16)
+    AUXCASE(17)
+    AUXCASE(19)
+    {
+        double2* uc;
+        CK(hipExtMallocWithFlags(reinterpret_cast<void**>(&uc), (size_t)ML * 8 * 16, hipDeviceMallocUncached));
+        CK(hipMemset(uc, 0, (size_t)ML * 8 * 16));
+        flush();
+        line("gat16_uc", ML * 16.0, 0, timeit([&] {
+                 hipLaunchKernelGGL(k_gat16_uc, dim3(grid), dim3(TPB), 0, 0, uc, ML, dout);
+             }));
+        flush();
+        line("sc16_uc", 0, ML * 16.0, timeit([&] { hipLaunchKernelGGL(k_sc16_uc, dim3(grid), dim3(TPB), 0, 0, uc, ML); }));
+        flush();
+        line("sc16", 0, ML * 16.0, timeit([&] { hipLaunchKernelGGL(k_sc16, dim3(grid), dim3(TPB), 0, 0, b, ML); }));
+        CK(hipFree(uc));
+    }
     flush();
     line("st16_nt", 0, N16 * 16.0,
          timeit([&] { hipLaunchKernelGGL(k_st16_nt, dim3(grid), dim3(TPB), 0, 0, a, N16); }));

@@ -25,6 +25,9 @@ SHAPE_KERNEL = {  # shape (calib.log) -> kernel name in the PMC csv
     "gat16": "k_gat16<false>", "gatdma_nt": "k_gatdma_nt<false>",
     "st16_nt": "k_st16_nt(", "st4_nt": "k_st4_nt(",
 }
+SHAPE_KERNEL.update({"gat16_uc": "k_gat16_uc(", "sc16_uc": "k_sc16_uc(", "sc16": "k_sc16("})
+for _a in (0, 1, 3, 16, 17, 19):
+    SHAPE_KERNEL[f"gatdma_aux{_a}"] = f"k_gatdma_aux<{_a}>"
 
 
 def largest(rows, key):
@@ -46,6 +49,7 @@ def main():
             shape, rd, wr, ms = p[0], float(p[2]), float(p[4]), float(p[6])
             sub = SHAPE_KERNEL[shape]
             a, b, w = (per_dispatch(dirs[n], sub) for n in ("rdA", "rdB", "wr"))
+            u = per_dispatch(os.path.join(root, "rdU"), sub) if os.path.isdir(os.path.join(root, "rdU")) else []
             nall, n32 = largest(a, "TCC_EA0_RDREQ_sum"), largest(a, "TCC_EA0_RDREQ_32B_sum")
             n64, n128 = largest(b, "TCC_EA0_RDREQ_64B_sum"), largest(b, "TCC_EA0_RDREQ_128B_sum")
             wbytes = largest(w, "WRITE_SIZE") * 1024.0
@@ -59,6 +63,13 @@ def main():
                 rec["fetch_size_factor"] = fetch_eq / rd
             if wr:
                 rec["write_factor"] = wbytes / wr
+            q = per_dispatch(os.path.join(root, "wrq"), sub) if os.path.isdir(os.path.join(root, "wrq")) else []
+            if q:
+                rec["wrreq"] = largest(q, "TCC_EA0_WRREQ_sum")
+                rec["wrreq_64b"] = largest(q, "TCC_EA0_WRREQ_64B_sum")
+            if u:
+                rec["rd_uncached_32b"] = largest(u, "TCC_EA0_RD_UNCACHED_32B_sum")
+                rec["rdreq_dram"] = largest(u, "TCC_EA0_RDREQ_DRAM_sum")
             if shape.startswith("gat"):
                 g = rd / 16.0
                 rec["requests_per_gather"] = nall / g
