@@ -436,8 +436,32 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                         sent[m] = q < cnt && ((a.eb[e >> 6] >> (e & 63u)) & 1ull);
                     }
                 } else if (all_active && GP_BATCH_EDGE) {
+                    // the first NPT edges per thread cover a tile's mean in-degree (TILE);
+                    // the slots above are drawn only by waves that hold an edge there
+                    // (a wave-uniform test: most tiles have fewer than TILE + 64 in-edges)
+                    constexpr int F0 = FU < NPT ? FU : NPT;
                     uint32_t x[FU], y[FU];
-                    philox2_batch<FU>(isrc, r, S_PUSHSUM, a.k0, a.k1, x, y);
+                    {
+                        uint32_t n0[F0], x0[F0], y0[F0];
+#pragma unroll
+                        for (int m = 0; m < F0; ++m) n0[m] = isrc[m];
+                        philox2_batch<F0>(n0, r, S_PUSHSUM, a.k0, a.k1, x0, y0);
+#pragma unroll
+                        for (int m = 0; m < F0; ++m) {
+                            x[m] = x0[m];
+                            y[m] = y0[m];
+                        }
+                    }
+#pragma unroll
+                    for (int m = F0; m < FU; ++m) {
+                        x[m] = y[m] = 0u;
+                        if (cnt > (uint32_t)(m * TPB) + (__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u)) {
+                            uint32_t n1[1] = {isrc[m]}, x1[1], y1[1];
+                            philox2_batch<1>(n1, r, S_PUSHSUM, a.k0, a.k1, x1, y1);
+                            x[m] = x1[0];
+                            y[m] = y1[0];
+                        }
+                    }
 #pragma unroll
                     for (int m = 0; m < FU; ++m) {
                         const uint32_t q = threadIdx.x + m * TPB;
@@ -538,14 +562,18 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
 #pragma unroll
         for (int k = 0; k < (NPT + 1) / 2; ++k) pend[k] = 0u;
         {
-            // lattice coordinates of this thread's first node, advanced by TPB per node
-            uint32_t cx = 0, cy = 0, cz = 0;
+            // Lattice coordinates of the WAVE's first node of slot k (wave-uniform, so
+            // scalar), advanced by TPB per slot.  A wave whose 64 nodes are all
+            // interior (no lattice boundary; ~93 % of waves at g = 1000) takes mask =
+            // 63 without per-lane coordinates; the others compute each node's mask.
+            const uint32_t wbase = __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u);
+            uint32_t wcx = 0, wcy = 0, wcz = 0;
             if (TOPO != LINE) {
-                const uint32_t j = T + threadIdx.x;
-                cx = fastdiv(j, G.div_g2);
-                const uint32_t rem = j - cx * G.g2;
-                cy = fastdiv(rem, G.div_g);
-                cz = rem - cy * G.g;
+                const uint32_t jw = T + wbase;
+                wcx = fastdiv(jw, G.div_g2);
+                const uint32_t rem = jw - wcx * G.g2;
+                wcy = fastdiv(rem, G.div_g);
+                wcz = rem - wcy * G.g;
             }
             constexpr uint32_t ND = TOPO == LINE ? 2 : 6;
             constexpr int NG = GP_NGROUP;  // nodes whose lattice gathers are in flight together
@@ -562,21 +590,28 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                     const int k = k0 + h;
                     const uint32_t j = T + k * TPB + threadIdx.x;
                     if (TOPO != LINE && k > 0) {
-                        cz += TPB;
-                        if (cz >= G.g) {
-                            const uint32_t q = fastdiv(cz, G.div_g);
-                            cz -= q * G.g;
-                            cy += q;
-                            if (cy >= G.g) {
-                                const uint32_t q2 = fastdiv(cy, G.div_g);
-                                cy -= q2 * G.g;
-                                cx += q2;
+                        wcz += TPB;
+                        if (wcz >= G.g) {
+                            const uint32_t q = fastdiv(wcz, G.div_g);
+                            wcz -= q * G.g;
+                            wcy += q;
+                            if (wcy >= G.g) {
+                                const uint32_t q2 = fastdiv(wcy, G.div_g);
+                                wcy -= q2 * G.g;
+                                wcx += q2;
                             }
                         }
                     }
                     const uint32_t jr = j - b_rows;
                     gb[h] = lds_byte(L.rows, jr);
-                    const uint32_t mask = TOPO == LINE ? present_mask<TOPO>(j, G) : mask_xyz(cx, cy, cz, G.g - 1u);
+                    uint32_t mask;
+                    if (TOPO == LINE) {
+                        mask = present_mask<TOPO>(j, G);
+                    } else {
+                        const uint32_t gm = G.g - 1u;
+                        const bool interior = wcz >= 1u && wcz + 64u < gm && wcy >= 1u && wcy < gm && wcx >= 1u && wcx < gm;
+                        mask = interior ? 63u : present_mask<TOPO>(j, G);
+                    }
                     uint32_t from = 0;
                     if (TOPO == LINE) {
                         from |= ((mask & 1u) && (lds_byte(L.rows, (mask & 1u) ? jr - 1 : jr) & DIR_MASK) == 1u) ? 1u : 0u;
@@ -624,8 +659,9 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                         bool active = (b & B_ACTIVE) != 0;
                         const double2 sv = own[k];
                         const bool halve = active && deg > 0;
-                        double acc_s = halve ? sv.x * 0.5 : sv.x;
-                        double acc_w = halve ? sv.y * 0.5 : sv.y;
+                        const double hf = halve ? 0.5 : 1.0;  // exact either way
+                        double acc_s = sv.x * hf;
+                        double acc_w = sv.y * hf;
                         // fused: fma(m, 0.5, acc) rounds once, exactly like the specification's
                         // acc + m * 0.5 whenever m * 0.5 is exact, i.e. |m| >= 2^-1021; every
                         // node checks its own round-start (s, w) -- the values its messages
