@@ -23,3 +23,34 @@ def test_unavailable_without_dotnet(monkeypatch):
 def test_missing_reference_project(tmp_path):
     r = at.run_reference(10, "full", "push-sum", reference=str(tmp_path), dotnet="/bin/true")
     assert r["available"] is False and "not found" in r["reason"]
+
+
+def _fake_reference(tmp_path):
+    proj = tmp_path / "Project2"
+    proj.mkdir()
+    (proj / "Program.fs").write_text("// stand-in project directory (never compiled)\n")
+    return str(tmp_path)
+
+
+def _fake_dotnet(tmp_path, body):
+    exe = tmp_path / "dotnet"
+    exe.write_text("#!/bin/bash\n" + body)
+    exe.chmod(0o755)
+    return str(exe)
+
+
+def test_build_failure_reported_unavailable(tmp_path):
+    dn = _fake_dotnet(tmp_path, 'if [ "$1" = build ]; then echo "restore failed: no network"; exit 1; fi\n')
+    r = at.run_reference(10, "line", "gossip", reference=_fake_reference(tmp_path), dotnet=dn)
+    assert r["available"] is False and "build failed" in r["reason"] and "restore failed" in r["reason"]
+
+
+def test_timed_run_parses_and_kills_group_on_timeout(tmp_path):
+    dn = _fake_dotnet(tmp_path, 'if [ "$1" = build ]; then exit 0; fi\n'
+                      'if [ "$8" = slow ]; then sleep 30 & wait; fi\n'
+                      'echo "Convergence Time: 12.5 ms"\n')
+    ref = _fake_reference(tmp_path)
+    r = at.run_reference(10, "line", "gossip", reference=ref, dotnet=dn)
+    assert r["available"] and r["converged"] and r["convergence_ms"] == 12.5
+    r = at.run_reference(10, "line", "slow", reference=ref, dotnet=dn, timeout=1)
+    assert r["available"] and r["converged"] is False and "timeout" in r["reason"]

@@ -20,6 +20,7 @@ import json
 import os
 import re
 import shutil
+import signal
 import subprocess
 import tempfile
 import time
@@ -43,24 +44,43 @@ def run_reference(nodes, topology, algorithm, reference="/root/reference", timeo
     if not os.path.isdir(proj):
         return {"available": False, "reason": f"reference project not found at {proj}", **cfg}
     ncpu = os.cpu_count() or 1
-    used = min(cores, ncpu) if cores > 0 else ncpu
     with tempfile.TemporaryDirectory(prefix="akka_ref_") as tmp:
         work = os.path.join(tmp, "Project2")
         shutil.copytree(proj, work, ignore=shutil.ignore_patterns("bin", "obj"))
-        cmd = [dotnet, "run", "-c", "Release", "--", str(nodes), topology, algorithm]
+        # build first (restore + compile are not part of the timed run; with no
+        # package source the restore fails, reported as unavailable with the reason)
+        rc, out, err, _ = _run_group([dotnet, "build", "-c", "Release"], work, timeout)
+        if rc != 0:
+            why = "timeout" if rc is None else f"exit {rc}"
+            return {"available": False, "reason": f"dotnet build failed ({why}): {(out + err)[-300:]}", **cfg}
+        cmd = [dotnet, "run", "--no-build", "-c", "Release", "--", str(nodes), topology, algorithm]
+        used = ncpu  # cores the run may use: pinned only when taskset is really applied
         if cores > 0 and shutil.which("taskset"):
+            used = min(cores, ncpu)
             cmd = ["taskset", "-c", f"0-{used - 1}"] + cmd
         t0 = time.perf_counter()
-        try:
-            p = subprocess.run(cmd, cwd=work, stdin=subprocess.DEVNULL, capture_output=True, text=True,
-                               timeout=timeout)
-        except subprocess.TimeoutExpired:
-            return {"available": True, "converged": False, "reason": f"timeout after {timeout} s", "cores": used,
-                    **cfg}
+        rc, out, _, timed_out = _run_group(cmd, work, timeout)
         wall = time.perf_counter() - t0
-    ms = parse_convergence_ms(p.stdout)
+    if timed_out:
+        return {"available": True, "converged": False, "reason": f"timeout after {timeout} s", "cores": used, **cfg}
+    ms = parse_convergence_ms(out)
     return {"available": True, "converged": ms is not None, "convergence_ms": ms, "wall_s": wall,
-            "exit_code": p.returncode, "cores": used, **cfg}
+            "exit_code": rc, "cores": used, **cfg}
+
+
+def _run_group(cmd, cwd, timeout):
+    """Run cmd in its own session; on timeout kill the whole process group (the
+    app process `dotnet run` spawns would otherwise outlive it, live-locked on the
+    pinned cores).  Returns (returncode or None, stdout, stderr, timed_out)."""
+    p = subprocess.Popen(cmd, cwd=cwd, stdin=subprocess.DEVNULL, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                         text=True, start_new_session=True)
+    try:
+        out, err = p.communicate(timeout=timeout)
+        return p.returncode, out, err, False
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        out, err = p.communicate()
+        return None, out or "", err or "", True
 
 
 def main():
