@@ -392,6 +392,11 @@ int build_imp3d(gp_sim* s) {
             if ((rc = dev_alloc_t(s, &S.in_srcd, (size_t)ne + 4))) return rc;
             if (ne) HIP_TRY(launch_pack_src_deg(S.in_src, S.in_srcd, ne, S.G, s->grid, s->stream));
         }
+        S.ind4 = nullptr;
+        if (S.alg == PUSHSUM && S.kernel == KERNEL_TILE) {
+            if ((rc = dev_alloc_t(s, &S.ind4, ind4_bytes_for(S.lo, S.nloc)))) return rc;
+            HIP_TRY(launch_pack_ind4(S, s->grid, s->stream));
+        }
         S.nedges = ne;
         S.eb = nullptr;
         // separate dense edge-decision pass (k_edge_decide): measured slower than the

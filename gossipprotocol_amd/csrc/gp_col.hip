@@ -34,7 +34,12 @@ __device__ __forceinline__ uint32_t col_rb_word(const WaveArgs& a, uint32_t x, u
     return ((x - a.x_lo) * a.G.g + y) * a.zsegs + (z >> 6);
 }
 
-// Did sender i (on this rank) use its random edge in round r?
+// Did sender i (on this rank) use its random edge in round r?  Its direction
+// draw of round r (counter (i, r), SRS v1 B.2) must pick the random slot -- the
+// last one, deg - 1 -- and, unless every node is active, it must have been
+// active: the bitmap bit (= active and that draw).  Redrawing first reads the
+// bitmap (a random 8-byte load, one 128-byte line) only for the ~1/7 of in-edges
+// whose draw selects the random slot.
 __device__ __forceinline__ bool col_sent_random(const WaveArgs& a, uint32_t i, uint32_t r, bool all_active,
                                                 uint32_t stream) {
     const Geom& G = a.G;
@@ -42,14 +47,9 @@ __device__ __forceinline__ bool col_sent_random(const WaveArgs& a, uint32_t i, u
     const uint32_t rem = i - x * G.g2;
     const uint32_t y = fastdiv(rem, G.div_g);
     const uint32_t z = rem - y * G.g;
-    if (all_active) {
-        const uint32_t gm = G.g - 1;
-        const uint32_t mask = (x > 0 ? 1u : 0u) | (x < gm ? 2u : 0u) | (y < gm ? 4u : 0u) | (y > 0 ? 8u : 0u) |
-                              (z < gm ? 16u : 0u) | (z > 0 ? 32u : 0u);
-        const uint32_t di = popc6(mask) + 1u;
-        return uniform(a.k0, a.k1, stream, i, r, di) == di - 1u;
-    }
-    return (a.rbc[col_rb_word(a, x, y, z)] >> (z & 63)) & 1ull;
+    const uint32_t di = popc6(mask_xyz(x, y, z, G.g - 1)) + 1u;
+    if (uniform(a.k0, a.k1, stream, i, r, di) != di - 1u) return false;
+    return all_active || ((a.rbc[col_rb_word(a, x, y, z)] >> (z & 63)) & 1ull);
 }
 
 // XCD-contiguous deal of n work items over the grid's waves (speed only).
@@ -92,16 +92,41 @@ __device__ __forceinline__ void sweep_in_edges(const WaveArgs& a, WaveLds& L, co
             eidx[m] = eb + (q - pb);
             src[m] = q < nst ? a.in_src[eidx[m]] : lo;
         }
+        // decisions: every sender's direction draw of round r as one Philox batch
+        // (interleaved chains), the bitmap read only where the draw picks the
+        // random slot (col_sent_random)
+        {
+            const Geom& G = a.G;
+            uint32_t xs[EU], ys[EU], wrd[EU], di[EU];
 #pragma unroll
-        for (int m = 0; m < EU; ++m) {
-            const uint32_t q = q0 + m * 64 + lane;
-            bool s = false;
-            if (q < nst) {
+            for (int m = 0; m < EU; ++m) {
                 const uint32_t i = src[m];
-                if (i - lo >= nloc) s = a.rtag[eidx[m]] == r;  // sender on another rank
-                else s = col_sent_random(a, i, r, all_active, stream);
+                const uint32_t x = fastdiv(i, G.div_g2);
+                const uint32_t rem = i - x * G.g2;
+                const uint32_t y = fastdiv(rem, G.div_g);
+                const uint32_t z = rem - y * G.g;
+                di[m] = popc6(mask_xyz(x, y, z, G.g - 1)) + 1u;
+                wrd[m] = z;
+                xs[m] = x;
+                ys[m] = y;
             }
-            sent[m] = s;
+            uint32_t X[EU], Y[EU];
+            philox2_batch<EU>(src, r, stream, a.k0, a.k1, X, Y);
+#pragma unroll
+            for (int m = 0; m < EU; ++m) {
+                const uint32_t q = q0 + m * 64 + lane;
+                bool s = false;
+                if (q < nst) {
+                    const uint32_t i = src[m];
+                    if (i - lo >= nloc) {
+                        s = a.rtag[eidx[m]] == r;  // sender on another rank
+                    } else if (uniform_from(X[m], Y[m], di[m]) == di[m] - 1u) {
+                        const uint32_t z = wrd[m];
+                        s = all_active || ((a.rbc[col_rb_word(a, xs[m], ys[m], z)] >> (z & 63)) & 1ull);
+                    }
+                }
+                sent[m] = s;
+            }
         }
         if (PUSH) {
             double2 val[EU];

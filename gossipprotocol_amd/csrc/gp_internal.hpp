@@ -140,6 +140,8 @@ struct DevState {
     uint32_t* in_off;  // P+1
     uint32_t* in_src;  // P
     uint32_t* in_srcd; // push-sum tile kernel: in_src with deg - 4 in bits 30-31 (P <= 2^30), else null
+    uint8_t* ind4;     // push-sum tile kernel: in-degree of every node of the slab's tiles, a nibble each
+                       // (min(deg, 15); 0 outside the slab), byte (j - lo / TILE * TILE) / 2, low nibble first
     // gossip injector
     uint32_t* live_bits;   // ceil(T / INJ_CHUNK) * 2048 words, bit = id still listed
     uint32_t* chunk_live;  // live ids per chunk
@@ -192,6 +194,7 @@ struct RoundArgs {
     const uint32_t* in_off;  // indexed by global id
     const uint32_t* in_src;
     const uint32_t* in_srcd; // in_src with the sender's deg - 4 in bits 30-31, or null
+    const uint8_t* ind4;     // nibble in-degrees (DevState::ind4), offset so that ind4 + j / 2 is node j's byte
     const uint32_t* rtag;    // per local in-edge: round of the delivered remote message
     const double2* rmsg;
     int32_t* c;              // indexed by global id
@@ -254,6 +257,8 @@ hipError_t launch_round_tile(const DevState& S, uint32_t round, int grid, hipStr
 int ps_tile_resident_blocks(int topo, bool remote, int device);
 bool build_walk_list(const DevState& S, std::vector<uint32_t>& list, uint32_t woff[9]);
 hipError_t launch_rbits_init(const DevState& S, int grid, hipStream_t st);
+uint32_t ind4_bytes_for(uint32_t lo, uint32_t nloc);
+hipError_t launch_pack_ind4(const DevState& S, int grid, hipStream_t st);
 hipError_t launch_pack_src_deg(const uint32_t* src, uint32_t* out, uint32_t n, const Geom& G, int grid,
                                hipStream_t st);
 

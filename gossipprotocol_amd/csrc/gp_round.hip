@@ -65,6 +65,12 @@ namespace gp {
 #ifndef GP_STAMPS
 #define GP_STAMPS 0      // diagnostics (experiments build): per-phase cycle counts of the push-sum tile kernel
 #endif
+#ifndef GP_OWN_EARLY
+#define GP_OWN_EARLY 0   // own (s, w) loaded ahead of the staging copies (1) or with the lattice gathers (0)
+#endif
+#ifndef GP_ZDPP
+#define GP_ZDPP 1        // push-sum tile kernel: the j+-1 messages from the neighbour lane's registers (DPP)
+#endif
 #ifndef GP_MINB
 #define GP_MINB 5  // __launch_bounds__ minimum waves per SIMD (= resident 256-thread blocks per CU):
                    // the LDS tile allows 5, so keep VGPRs <= 96 to not lose the fifth
@@ -107,7 +113,7 @@ struct TileLdsP {
     uint32_t rows[W_ROWS + DMA_SLACK];
     uint32_t xm[W_PLANE + DMA_SLACK];
     uint32_t xp[W_PLANE + DMA_SLACK];
-    uint32_t off[TILE + 1 + DMA_SLACK];
+    uint32_t ind[TILE / 8 + DMA_SLACK];  // in-degrees of the tile's nodes, a nibble each (DevState::ind4)
     unsigned long long bits[SLOT_FU * (TPB / 64) + 1];  // bit q: in-edge q (tile order) was used by its sender; then 0
     double2 msg[SLOTS];               // edge q's message at slot q
     uint32_t out[TILE / 4];
@@ -115,6 +121,11 @@ struct TileLdsP {
     uint32_t qn[2];                   // walk 3: the block's next item, by iteration parity
 };
 
+
+// set bits of m below this lane
+__device__ __forceinline__ uint32_t mbcnt64(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
 
 __device__ __forceinline__ uint32_t lds_byte(const uint32_t* w, uint32_t idx) {
     return reinterpret_cast<const uint8_t*>(w)[idx];
@@ -285,6 +296,19 @@ struct TileWalk {
 };
 
 __device__ __forceinline__ double2 ld_sw(const double2* p) { return *p; }
+
+// v of another lane of the wave by DPP (CTRL 0x130 wave_shl:1 = lane + 1's,
+// 0x138 wave_shr:1 = lane - 1's; the lane at the wave's end gets 0)
+template <int CTRL>
+__device__ __forceinline__ double2 dpp_double2(double2 v) {
+    auto mv = [](double d) {
+        const uint64_t u = __builtin_bit_cast(uint64_t, d);
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xF, 0xF, false);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
+        return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+    };
+    return make_double2(mv(v.x), mv(v.y));
+}
 
 // Next-round state is written once and not read again this round: non-temporal
 // stores keep it from displacing the current round's (s, w) in the XCD's L2,
@@ -518,11 +542,13 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
         }
         GP_STAMP(t1);
         // own (s, w): consumed after staging
+        // (loaded here, ahead of the staging copies, or -- GP_OWN_EARLY 0 -- with
+        // the node's lattice gathers, which keeps 12 fewer VGPRs live)
         double2 own[NPT];
 #pragma unroll
         for (int k = 0; k < NPT; ++k) {
             const uint32_t j = T + k * TPB + threadIdx.x;
-            own[k] = (j >= j0 && j < j1) ? swc[j] : make_double2(0.0, 1.0);
+            if (GP_OWN_EARLY) own[k] = (j >= j0 && j < j1) ? swc[j] : make_double2(0.0, 1.0);
         }
         // every staging copy of the tile in flight at once (LDS-DMA)
         const uint32_t b_rows = dma_stage_bytes(L.rows, a.nbc, (int64_t)j0 - H, (int64_t)j1 + H, a.ext_lo, a.ext_hi);
@@ -531,12 +557,36 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
             b_xm = dma_stage_bytes(L.xm, a.nbc, (int64_t)j0 - G.g2, (int64_t)j1 - G.g2, a.ext_lo, a.ext_hi);
             b_xp = dma_stage_bytes(L.xp, a.nbc, (int64_t)j0 + G.g2, (int64_t)j1 + G.g2, a.ext_lo, a.ext_hi);
         }
-        int o_off = 0;  // L.off[jl + o_off] = in_off[T + jl]
-        if (TOPO == IMP3D) o_off = (int)dma_stage_words(L.off, a.in_off, j0, j1 + 1) - (int)(j0 - T);
+        // the tile's in-degrees, a nibble per node (512 bytes; the slab's arrays
+        // cover whole tiles, ids outside the slab are 0)
+        if (TOPO == IMP3D) dma_copy<DMA_ONCE>(L.ind, reinterpret_cast<const char*>(a.ind4 + T / 2), TILE / 2);
         GP_STAMP(t2);
         if (dyn && threadIdx.x == 0) L.qn[it & 1] = claim;
         __syncthreads();  // staging copies, in-edge bitmap and gathered messages retired
         GP_STAMP(t3);
+        // Imp3D: node jl's in-edges are [e_lo + pre(jl), + d(jl)), pre = exclusive
+        // prefix of the nibble in-degrees.  Every wave sums all 16 64-node chunks
+        // (lane L: nodes 16L..16L+15) and keeps the prefixes of its own chunks
+        // 4k + wave (scalars); the lane part comes from ballots in the node loop.
+        // A tile holding a node of in-degree >= 15 (nibble 15, ~1e-12 of nodes)
+        // reads in_off from HBM instead.
+        uint32_t cinc = 0;
+        bool wide = false;
+        if (TOPO == IMP3D) {
+            const uint2 w2 = reinterpret_cast<const uint2*>(L.ind)[lane];
+            auto nsum = [](uint32_t w) { return (((w & 0x0F0F0F0Fu) + ((w >> 4) & 0x0F0F0F0Fu)) * 0x01010101u) >> 24; };
+            auto has15 = [](uint32_t w) { return (w & (w >> 1) & (w >> 2) & (w >> 3) & 0x11111111u) != 0u; };
+            uint32_t incl = nsum(w2.x) + nsum(w2.y);
+            wide = __ballot(has15(w2.x) || has15(w2.y)) != 0ull;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t t = __shfl_up(incl, o, 64);
+                if (lane >= (uint32_t)o) incl += t;
+            }
+            // exclusive chunk prefix at lane 4c (read per slot in the node loop)
+            const uint32_t ex = __shfl_up(incl, 1, 64);
+            cinc = lane == 0 ? 0u : ex;
+        }
         uint32_t t_next = tw.t + tw.step;
         if (dyn) {
             t_next = L.qn[it & 1];
@@ -583,6 +633,22 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                 // phase A: node byte, present mask, lattice senders (from the staged
                 // direction bytes), one gather per direction -- a direction without a
                 // sender reads the zero sentinel swc[ext_hi] (adding +0.0 is exact)
+                // in-edge ranges of the group's nodes (all lanes take part in the ballots)
+                uint32_t epre[NG], edeg[NG];
+#pragma unroll
+                for (int h = 0; h < NG; ++h) {
+                    epre[h] = edeg[h] = 0u;
+                    if (TOPO == IMP3D) {
+                        const int k = k0 + h;
+                        const uint32_t jl = k * TPB + threadIdx.x;
+                        const uint32_t d = (lds_byte(L.ind, jl >> 1) >> ((jl & 1u) * 4u)) & 15u;
+                        uint32_t ex = mbcnt64(__ballot(d & 1u)) + 2u * mbcnt64(__ballot(d & 2u));
+                        if (__ballot(d >= 4u)) ex += 4u * mbcnt64(__ballot(d & 4u)) + 8u * mbcnt64(__ballot(d & 8u));
+                        const int wvu = __builtin_amdgcn_readfirstlane((int)wv);
+                        epre[h] = (uint32_t)__builtin_amdgcn_readlane((int)cinc, 16 * k + 4 * wvu) + ex;
+                        edeg[h] = d;
+                    }
+                }
                 uint32_t gb[NG], gmask[NG], gfrom[NG];
                 double2 m[NG][ND];
 #pragma unroll
@@ -632,10 +698,25 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                     if (!(j >= j0 && j < j1)) from = 0u;
                     gmask[h] = mask;
                     gfrom[h] = from;
+                    if (!GP_OWN_EARLY) own[k] = (j >= j0 && j < j1) ? swc[j] : make_double2(0.0, 1.0);
+                    // j + 1 and j - 1 are the neighbour lanes' nodes: their (s, w) -- own[k]
+                    // of those lanes -- move across by DPP in phase B; a gather here only
+                    // where that lane's node is outside the wave or the tile's valid range
+                    constexpr uint32_t dP = TOPO == LINE ? 1u : 4u, dM = TOPO == LINE ? 0u : 5u;
+                    double2 vP = make_double2(0.0, 0.0), vM = make_double2(0.0, 0.0);
+                    if (GP_ZDPP) {
+                        const bool lane_p = lane < 63u && j + 1u < j1, lane_m = lane > 0u && j > j0;
+                        if (((from >> dP) & 1u) && !lane_p) vP = ld_sw(swc + j + 1);
+                        if (((from >> dM) & 1u) && !lane_m) vM = ld_sw(swc + j - 1);
+                    }
 #pragma unroll
                     for (uint32_t d = 0; d < ND; ++d)
                         if ((GP_ABL_DIRS >> d) & 1) {  // ablation (timing only): no gathers in slot d
                             m[h][d] = make_double2(0.0, 0.0);
+                        } else if (GP_ZDPP && d == dP) {
+                            m[h][d] = vP;
+                        } else if (GP_ZDPP && d == dM) {
+                            m[h][d] = vM;
                         } else if (GP_LMASK) {  // only lanes with a sender load (exec-masked gather)
                             m[h][d] = make_double2(0.0, 0.0);
                             if ((from >> d) & 1u) m[h][d] = ld_sw(swc + nbr<TOPO>(j, d, G));
@@ -653,11 +734,21 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                     const uint32_t j = T + jl;
                     const bool valid = j >= j0 && j < j1;
                     uint32_t dir = DIR_NONE;
+                    if (GP_ZDPP) {  // all lanes active here: DPP reads the neighbour lanes
+                        constexpr uint32_t dP = TOPO == LINE ? 1u : 4u, dM = TOPO == LINE ? 0u : 5u;
+                        const uint32_t from = gfrom[h];
+                        const bool lane_p = lane < 63u && j + 1u < j1, lane_m = lane > 0u && j > j0;
+                        const double2 zup = dpp_double2<0x130>(own[k]);  // wave_shl:1 -- lane + 1's (s, w)
+                        const double2 zdn = dpp_double2<0x138>(own[k]);  // wave_shr:1 -- lane - 1's (s, w)
+                        if (((from >> dP) & 1u) && lane_p) m[h][dP] = zup;
+                        if (((from >> dM) & 1u) && lane_m) m[h][dM] = zdn;
+                    }
                     if (valid) {
                         const uint32_t b = gb[h], mask = gmask[h], from = gfrom[h];
                         const uint32_t deg = popc6(mask) + (TOPO == IMP3D ? 1u : 0u);
                         bool active = (b & B_ACTIVE) != 0;
                         const double2 sv = own[k];
+
                         const bool halve = active && deg > 0;
                         const double hf = halve ? 0.5 : 1.0;  // exact either way
                         double acc_s = sv.x * hf;
@@ -680,7 +771,11 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
 #pragma unroll
                         for (uint32_t d = 0; d < ND; ++d) fold(m[h][d]);
                         if (TOPO == IMP3D) {
-                            const uint32_t e_b = L.off[jl + o_off], e_e = L.off[jl + 1 + o_off];
+                            uint32_t e_b = e_lo + epre[h], e_e = e_b + edeg[h];
+                            if (wide) {
+                                e_b = a.in_off[j];
+                                e_e = a.in_off[j + 1];
+                            }
                             if (staged) {
                                 // the node's used in-edges: its window of the tile bitmap, 32 bits
                                 // at a time (funnel shift of two LDS words), walked set bit by set
@@ -978,13 +1073,21 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_gossip_tile(RoundArgs a, uint3
                     const uint32_t q = threadIdx.x + m * TPB;
                     isrc[m] = q < cnt ? a.in_src[e_lo + q] : 0u;
                 }
+                // the senders' direction draws of round r as one Philox batch; the
+                // bitmap (bit = active and the draw picks the random slot) is read
+                // only where the draw picks it, ~1/7 of the in-edges, instead of a
+                // random 128-byte line per in-edge
+                uint32_t X[FU], Y[FU];
+                philox2_batch<FU>(isrc, r, S_GOSSIP, a.k0, a.k1, X, Y);
                 unsigned long long wv[FU];
 #pragma unroll
                 for (int m = 0; m < FU; ++m) {
                     const uint32_t q = threadIdx.x + m * TPB;
                     const uint32_t li = isrc[m] - a.lo;
+                    const uint32_t di = popc6(present_mask<IMP3D>(isrc[m], G)) + 1u;
+                    const bool pick = uniform_from(X[m], Y[m], di) == di - 1u;
                     wv[m] = q >= cnt ? 0ull
-                            : (!REMOTE || li < a.nloc) ? a.rbc[(isrc[m] >> 6) - (a.lo >> 6)]
+                            : (!REMOTE || li < a.nloc) ? (pick ? a.rbc[(isrc[m] >> 6) - (a.lo >> 6)] : 0ull)
                                           : (a.rtag[e_lo + q] == r ? ~0ull : 0ull);
                 }
 #pragma unroll
@@ -1110,6 +1213,7 @@ RoundArgs make_round_args(const DevState& S, uint32_t round) {
     a.in_off = S.in_off ? S.in_off - S.lo : nullptr;
     a.in_src = S.in_src;
     a.in_srcd = S.in_srcd;
+    a.ind4 = S.ind4 ? S.ind4 - (S.lo / TILE) * (TILE / 2) : nullptr;
     a.rtag = S.rtag;
     a.rmsg = S.rmsg;
     a.c = S.c ? S.c - S.lo : nullptr;
@@ -1195,6 +1299,7 @@ hipError_t launch_round_tile(const DevState& S, uint32_t round, int grid, hipStr
             hipLaunchKernelGGL((k_edge_decide<false>), ge, dim3(256), 0, st, src, S.nedges, S.eb, S.G, S.k0, S.k1,
                                S.ctl, round);
     }
+    if (S.alg == PUSHSUM && S.topo == IMP3D && !S.ind4) return hipErrorInvalidValue;
     if (S.alg == PUSHSUM) {
         switch (S.topo) {
             case LINE: hipLaunchKernelGGL((k_ps_tile<LINE, false>), g, b, 0, st, a, round); break;
@@ -1232,6 +1337,29 @@ __global__ __launch_bounds__(TPB) void k_pack_src_deg(const uint32_t* src, uint3
 hipError_t launch_pack_src_deg(const uint32_t* src, uint32_t* out, uint32_t n, const Geom& G, int grid,
                                hipStream_t st) {
     hipLaunchKernelGGL(k_pack_src_deg, dim3(grid), dim3(TPB), 0, st, src, out, n, G);
+    return hipGetLastError();
+}
+
+// Nibble in-degrees of the slab's tiles (DevState::ind4) from in_off.
+__global__ __launch_bounds__(TPB) void k_pack_ind4(const uint32_t* __restrict__ in_off, uint32_t lo, uint32_t nloc,
+                                                   uint32_t j00, uint8_t* __restrict__ out, uint32_t nbytes) {
+    for (uint32_t b = blockIdx.x * TPB + threadIdx.x; b < nbytes; b += gridDim.x * TPB) {
+        uint32_t v = 0;
+#pragma unroll
+        for (uint32_t h = 0; h < 2; ++h) {
+            const uint32_t j = j00 + 2 * b + h;
+            if (j - lo < nloc) v |= min(in_off[j + 1] - in_off[j], 15u) << (4 * h);
+        }
+        out[b] = (uint8_t)v;
+    }
+}
+
+uint32_t ind4_bytes_for(uint32_t lo, uint32_t nloc) { return tiles_for(lo, nloc) * (TILE / 2) + 16u; }
+
+hipError_t launch_pack_ind4(const DevState& S, int grid, hipStream_t st) {
+    const uint32_t nbytes = tiles_for(S.lo, S.nloc) * (TILE / 2);
+    hipLaunchKernelGGL(k_pack_ind4, dim3(grid), dim3(TPB), 0, st, S.in_off - S.lo, S.lo, S.nloc, (S.lo / TILE) * TILE,
+                       S.ind4, nbytes);
     return hipGetLastError();
 }
 

@@ -39,6 +39,9 @@ VARIANTS = {  # name -> extra -D flags for gp_round.hip
     "npt2": ["-DGP_NPT=2"],
     "plainld": ["-DGP_NT_LOADS=0"],
     "plainst": ["-DGP_NT_STORES=0"],
+    "ownearly": ["-DGP_OWN_EARLY=1"],
+    "nozdpp": ["-DGP_ZDPP=0"],
+    "nozdpp_oe": ["-DGP_ZDPP=0", "-DGP_OWN_EARLY=1"],
 }
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-DGP_EXPERIMENTS"]
 
