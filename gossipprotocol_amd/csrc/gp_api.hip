@@ -313,6 +313,9 @@ int alloc_slab(gp_sim* s, Slab& sl, int r) {
             (rc = dev_alloc_t(s, &S.fb_hdr2, m2)) || (rc = dev_alloc_t(s, &S.fb_pay2, m2)))
             return rc;
     }
+    if (S.topo == IMP3D && S.alg == GOSSIP && S.kernel == KERNEL_COL &&
+        (rc = dev_alloc_t(s, &S.rcnt, (size_t)S.nloc + 64)))
+        return rc;
     if (S.topo == IMP3D) {
         S.rbits_words = S.kernel == KERNEL_COL ? col_rbits_words(S.nloc / S.G.g2, S.G.g)
                                                : rbits_words_for(S.lo, S.nloc);
@@ -798,12 +801,14 @@ int launch_round(gp_sim* s, uint32_t r, hipEvent_t e0, hipEvent_t e1) {
 double alg_bytes(const gp_sim* s) {
     const DevState& S = s->slab[0].S;
     if (S.alg == PUSHSUM) {
-        // sw r+w 32, node byte r+w 2 (+ Imp3D in-list: offset 4 + sender 4)
-        if (S.topo == IMP3D) return 42.0;
+        // sw r+w 32, node byte r+w 2 (+ Imp3D: in-degree nibble 0.5 + sender 4 of the
+        // in-list, and the random-edge message payload, 16 B for the ~1/7 of senders
+        // that use the random edge -- a random gather, moved as a 128-B line)
+        if (S.topo == IMP3D) return 38.5 + 16.0 / 7.0;
         if (S.topo != FULL) return 34.0;
-        // send: byte 1 + own (s, w) 16 + message write 24; split: message r+w 48; fold: header
-        // 8 twice + payload 16 + own (s, w) r+w 32 + byte r+w 2 (gp_fullbin.hip)
-        return 1.0 + 16.0 + 24.0 + 48.0 + 16.0 + 16.0 + 32.0 + 2.0;
+        // send: byte 1 + own (s, w) 16 + message write 20; split: message r+w 40; fold:
+        // message 20 + own (s, w) r+w 32 + byte r+w 2 (gp_fullbin.hip)
+        return 1.0 + 16.0 + 20.0 + 40.0 + 20.0 + 32.0 + 2.0;
     }
     // gossip: counter r+w 8, direction byte r+w 2 (+ Imp3D in-list 8)
     if (S.topo == IMP3D) return 18.0;

@@ -157,7 +157,7 @@ __device__ __forceinline__ void sweep_in_edges(const WaveArgs& a, WaveLds& L, co
 }
 
 // Row k's CSR bounds of the patch-step: per-lane offset and the row's end.
-__device__ __forceinline__ void row_offsets(const WaveArgs& a, uint32_t rs, uint32_t nz, bool row_ok, uint32_t& off,
+[[maybe_unused]] __device__ __forceinline__ void row_offsets(const WaveArgs& a, uint32_t rs, uint32_t nz, bool row_ok, uint32_t& off,
                                             uint32_t& rend) {
     const int lane = threadIdx.x & 63;
     if (row_ok) {
@@ -380,14 +380,12 @@ __global__ __launch_bounds__(BULK_THREADS) void k_ps_col(WaveArgs a, uint32_t r)
 // + the injector; all dropped if j was converged at round start (Program.fs:87).
 template <int TOPO>
 __global__ __launch_bounds__(BULK_THREADS) void k_gossip_col(WaveArgs a, uint32_t r) {
-    __shared__ WaveLds Lw[WPB];
     Ctl* ctl = a.ctl;
     if (ld_agent(&ctl->done)) return;
     const long long inj = ld_agent(&ctl->inj_target);
     const int lane = threadIdx.x & 63;
-    WaveLds& L = Lw[threadIdx.x >> 6];
     const uint8_t* __restrict__ nbc = a.nbc;
-    const uint32_t g = a.G.g, g2 = a.G.g2, base = a.base, lo = a.lo, nloc = a.nloc;
+    const uint32_t g = a.G.g, g2 = a.G.g2, base = a.base, lo = a.lo;
     uint32_t alerts = 0;
 
     uint32_t it, it_end, it_step;
@@ -399,7 +397,6 @@ __global__ __launch_bounds__(BULK_THREADS) void k_gossip_col(WaveArgs a, uint32_
         const uint32_t xa = a.x_lo + (t / a.yblocks) * a.xs_len;
         const uint32_t xb = min(a.x_hi, xa + a.xs_len);
         const uint32_t z = zs * 64 + (uint32_t)lane;
-        const uint32_t nz = min(64u, g - zs * 64);
         const uint32_t y0 = yb * NR;
         const bool zv = z < g;
         bool rv[NR];
@@ -438,18 +435,11 @@ __global__ __launch_bounds__(BULK_THREADS) void k_gossip_col(WaveArgs a, uint32_
                 zbm |= ((rv[k] && z > 0) ? (uint32_t)nbc[jl - 1] : (uint32_t)DIR_NONE) << (8 * k);
                 zbp |= ((rv[k] && z + 1 < g) ? (uint32_t)nbc[jl + 1] : (uint32_t)DIR_NONE) << (8 * k);
             }
-            uint32_t off[NR], rend[NR], e0[NR], P[NR + 1];
-            if (TOPO == IMP3D) {
+            // Imp3D: the random-edge deliveries of the patch rows, counted per
+            // receiver by k_gossip_redges before this kernel
+            uint32_t rcv[NR];
 #pragma unroll
-                for (int k = 0; k < NR; ++k) row_offsets(a, px + (y0 + k) * g + zs * 64, nz, y0 + k < g, off[k], rend[k]);
-                P[0] = 0;
-#pragma unroll
-                for (int k = 0; k < NR; ++k) {
-                    e0[k] = __builtin_amdgcn_readlane(off[k], 0);
-                    P[k + 1] = P[k] + (rend[k] - e0[k]);
-                }
-                sweep_in_edges<false>(a, L, e0, P, r, false, S_GOSSIP);
-            }
+            for (int k = 0; k < NR; ++k) rcv[k] = (TOPO == IMP3D && rv[k]) ? (uint32_t)a.rcnt[px + yo[k] - lo] : 0u;
 #pragma unroll
             for (int k = 0; k < NR; ++k) {
                 const uint32_t j = px + yo[k];
@@ -461,21 +451,7 @@ __global__ __launch_bounds__(BULK_THREADS) void k_gossip_col(WaveArgs a, uint32_
                 n += ((mask & 8u) && ((k > 0 ? byte_of(cb, k - 1) : hym) & DIR_MASK) == 2u) ? 1u : 0u;
                 n += ((mask & 16u) && (byte_of(zbp, k) & DIR_MASK) == 5u) ? 1u : 0u;
                 n += ((mask & 32u) && (byte_of(zbm, k) & DIR_MASK) == 4u) ? 1u : 0u;
-                if (TOPO == IMP3D) {
-                    const uint32_t ebk = off[k];
-                    uint32_t ee = __shfl_down(ebk, 1, 64);
-                    if (lane == 63) ee = rend[k];
-                    for (uint32_t e = ebk; e < ee; ++e) {
-                        const uint32_t q = P[k] + (e - e0[k]);
-                        if (q < ECAP) {
-                            n += L.code[q];
-                        } else {
-                            const uint32_t i = a.in_src[e];
-                            n += (i - lo >= nloc) ? (a.rtag[e] == r ? 1u : 0u)
-                                                  : (col_sent_random(a, i, r, false, S_GOSSIP) ? 1u : 0u);
-                        }
-                    }
-                }
+                n += rcv[k];
                 int32_t c1v = cv[k];
                 if (rv[k] && c1v < (int32_t)GOSSIP_DONE && n) {
                     c1v += (int32_t)n;
@@ -494,13 +470,33 @@ __global__ __launch_bounds__(BULK_THREADS) void k_gossip_col(WaveArgs a, uint32_
                     if (lane == 0 && y0 + k < g) a.rbn[col_rb_word(a, x, y0 + k, zs * 64)] = bits;
                 }
             }
-            if (TOPO == IMP3D) wave_lds_sync();
             pb = cb;
             cb = nb;
             nb = nnb;
         }
     }
     block_add2(alerts, 0u, &ctl->round_alerts, nullptr);
+}
+
+// Imp3D gossip, before the column kernel: per local receiver, how many of its
+// in-edge senders sent it a rumour on their random edge this round
+// (col_sent_random; remote senders by the exchange tag).  Thread per receiver,
+// every receiver independent, so the in_off -> in_src -> bitmap chains of all
+// receivers overlap -- inside the x-march they were three dependent memory
+// round trips per patch step.
+__global__ __launch_bounds__(BULK_THREADS) void k_gossip_redges(WaveArgs a, uint32_t r) {
+    if (ld_agent(&a.ctl->done)) return;
+    const uint32_t lo = a.lo, nloc = a.nloc;
+    for (uint32_t lj = blockIdx.x * BULK_THREADS + threadIdx.x; lj < nloc; lj += gridDim.x * BULK_THREADS) {
+        const uint32_t eb = a.in_off[lj], ee = a.in_off[lj + 1];
+        uint32_t n = 0;
+        for (uint32_t e = eb; e < ee; ++e) {
+            const uint32_t i = a.in_src[e];
+            if (i - lo >= nloc) n += a.rtag[e] == r ? 1u : 0u;  // sender on another rank
+            else n += col_sent_random(a, i, r, false, S_GOSSIP) ? 1u : 0u;
+        }
+        a.rcnt[lj] = (uint16_t)n;
+    }
 }
 
 // Random-edge bits of round 0 in the column layout (only the seed can be sending).
@@ -548,8 +544,14 @@ hipError_t launch_round_col(const WaveArgs& a, int topo, int alg, uint32_t round
         return hipErrorInvalidValue;
 #endif
     } else {
-        if (topo == GRID3D) hipLaunchKernelGGL(k_gossip_col<GRID3D>, g, b, 0, st, a, round);
-        else hipLaunchKernelGGL(k_gossip_col<IMP3D>, g, b, 0, st, a, round);
+        if (topo == GRID3D) {
+            hipLaunchKernelGGL(k_gossip_col<GRID3D>, g, b, 0, st, a, round);
+        } else {
+            if (!a.rcnt) return hipErrorInvalidValue;
+            const uint32_t ge = std::min<uint32_t>((a.nloc + BULK_THREADS - 1) / BULK_THREADS, 256u * 64u);
+            hipLaunchKernelGGL(k_gossip_redges, dim3(std::max(1u, ge)), b, 0, st, a, round);
+            hipLaunchKernelGGL(k_gossip_col<IMP3D>, g, b, 0, st, a, round);
+        }
     }
     return hipGetLastError();
 }

@@ -11,16 +11,19 @@
 // Per round, three kernels:
 //   A  k_fb_send   senders in chunks of FB_CHUNK: target t = U(P-1) mapped past i
 //                  (Philox), LDS counting by coarse bin (t >> s1), one global
-//                  reservation per (chunk, bin), each message {t, i | s/2, w/2}
+//                  reservation per (chunk, bin), each message {i | s/2, w/2}
 //                  written into its coarse bin's run;
-//   B  k_fb_split  each coarse bin's messages in chunks: LDS counting by fine
-//                  tile (t >> FB_TB, FB_TILE receivers), reservation, copy;
+//   B  k_fb_split  each coarse bin's messages in chunks: the target recomputed
+//                  from the sender's Philox draw, LDS counting by fine tile
+//                  (t >> FB_TB, FB_TILE receivers), reservation, copy;
 //   C  k_fb_fold   one fine tile per block: LDS counting sort of the tile's
-//                  messages by receiver, each receiver's (few) messages put in
-//                  ascending sender order, folded, ratio test, next state.
+//                  messages by receiver (target recomputed once more), each
+//                  receiver's (few) messages put in ascending sender order,
+//                  folded, ratio test, next state.
 // Order inside a bin is whatever the LDS atomics produce; the fold restores the
 // canonical order by sender id, so results do not depend on it.  Every message
-// is moved as 24 bytes (header 8 + payload 16), each pass coalesced -- no
+// is moved as 20 bytes (sender id 4 + payload 16; recomputing the target costs
+// a Philox draw per pass instead of 4 bytes per move), each pass coalesced -- no
 // random 16-byte gather of a sender's (s, w) anywhere.  Bin capacities are the
 // expected load + 12 sigma + slack; an overflow is flagged (Ctl::overflow) and
 // fails the batch in gp_step.
@@ -32,22 +35,34 @@
 namespace gp {
 namespace {
 
-constexpr int FB_THREADS = 256;
+// Passes A and B: 1024-thread blocks over chunks of FB_CHUNK senders / messages
+// (16 per thread), so a chunk writes runs of ~86 (A) and ~32 (B) consecutive
+// messages per bin and reserves each run with one global atomic.
+constexpr int FB_THREADS = 256;                    // C
+constexpr int FBX_THREADS = 1024;                  // A, B
 #ifndef GP_FB_PER
 #define GP_FB_PER 16
 #endif
 constexpr int FB_PER = GP_FB_PER;                  // senders / messages per thread per chunk
-constexpr int FB_CHUNK = FB_THREADS * FB_PER;      // 4096
+constexpr int FB_CHUNK = FBX_THREADS * FB_PER;     // 16384
 constexpr int FB_MAXBINS = 4096;                   // LDS counters of A and B
+constexpr uint32_t FB_NONE = 0xFFFFu;
+#ifndef GP_FB_BATCH
+#define GP_FB_BATCH 8
+#endif
+constexpr int FB_BATCH = GP_FB_BATCH;              // loads issued together before their stores
 
 template <typename T>
 __device__ __forceinline__ T ld_agent(const T* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Exclusive scan of cnt[0..n) in LDS (n <= FB_MAXBINS), one block; returns the total.
+
+// Exclusive scan of cnt[0..n) in LDS (n <= FB_MAXBINS), one block of NT threads;
+// returns the total.
+template <int NT>
 __device__ uint32_t lds_excl_scan(uint32_t* cnt, uint32_t n, uint32_t* tmp) {
-    constexpr int PER = FB_MAXBINS / FB_THREADS;  // 16 counters per thread
+    constexpr int PER = (FB_MAXBINS + NT - 1) / NT;
     uint32_t v[PER], s = 0;
     const uint32_t b = threadIdx.x * PER;
 #pragma unroll
@@ -55,7 +70,6 @@ __device__ uint32_t lds_excl_scan(uint32_t* cnt, uint32_t n, uint32_t* tmp) {
         v[k] = b + k < n ? cnt[b + k] : 0u;
         s += v[k];
     }
-    // block scan of the per-thread sums
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     uint32_t incl = s;
 #pragma unroll
@@ -66,7 +80,7 @@ __device__ uint32_t lds_excl_scan(uint32_t* cnt, uint32_t n, uint32_t* tmp) {
     if (lane == 63) tmp[wid] = incl;
     __syncthreads();
     uint32_t wbase = 0, total = 0;
-    for (int w = 0; w < FB_THREADS / 64; ++w) {
+    for (int w = 0; w < NT / 64; ++w) {
         if (w < wid) wbase += tmp[w];
         total += tmp[w];
     }
@@ -83,54 +97,69 @@ __device__ uint32_t lds_excl_scan(uint32_t* cnt, uint32_t n, uint32_t* tmp) {
 }  // namespace
 
 // ---------------------------------------------------------------- A: send + coarse bins
-__global__ __launch_bounds__(FB_THREADS) void k_fb_send(FullBinArgs a, uint32_t r) {
+__global__ __launch_bounds__(FBX_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_fb_send(FullBinArgs a, uint32_t r) {
     __shared__ uint32_t cnt[FB_MAXBINS];       // per bin: count, then the chunk's global base
-    __shared__ uint32_t tgt[FB_CHUNK];         // target per sender of the chunk (~0: inactive)
+    __shared__ uint16_t bin[FB_CHUNK];         // coarse bin per sender of the chunk (FB_NONE: inactive)
     __shared__ uint16_t rank[FB_CHUNK];        // its position in the chunk's run of its bin
     if (ld_agent(&a.ctl->done)) return;
     const uint32_t P = a.P;
     for (uint64_t c0 = (uint64_t)blockIdx.x * FB_CHUNK; c0 < P; c0 += (uint64_t)gridDim.x * FB_CHUNK) {
-        for (uint32_t b = threadIdx.x; b < a.nb1; b += FB_THREADS) cnt[b] = 0u;
+        for (uint32_t b = threadIdx.x; b < a.nb1; b += FBX_THREADS) cnt[b] = 0u;
         __syncthreads();
         constexpr int PB = 8;  // Philox chains interleaved per batch
 #pragma unroll
         for (int k0 = 0; k0 < FB_PER; k0 += PB) {
             uint32_t node[PB], x[PB], y[PB];
 #pragma unroll
-            for (int k = 0; k < PB; ++k) node[k] = (uint32_t)(c0 + (k0 + k) * FB_THREADS + threadIdx.x);
+            for (int k = 0; k < PB; ++k) node[k] = (uint32_t)(c0 + (k0 + k) * FBX_THREADS + threadIdx.x);
             philox2_batch<PB>(node, r, S_PUSHSUM, a.k0, a.k1, x, y);
 #pragma unroll
             for (int k = 0; k < PB; ++k) {
-                const uint32_t i = node[k], q = (k0 + k) * FB_THREADS + threadIdx.x;
-                uint32_t t = 0xFFFFFFFFu;
+                const uint32_t i = node[k], q = (k0 + k) * FBX_THREADS + threadIdx.x;
+                uint32_t bb = FB_NONE;
                 if (i < P && (a.nb[i] & B_ACTIVE) && P > 1) {
-                    t = full_target(i, uniform_from(x[k], y[k], P - 1));  // Program.fs:213-215
-                    rank[q] = (uint16_t)atomicAdd(&cnt[t >> a.s1], 1u);
+                    bb = full_target(i, uniform_from(x[k], y[k], P - 1)) >> a.s1;  // Program.fs:213-215
+                    rank[q] = (uint16_t)atomicAdd(&cnt[bb], 1u);
                 }
-                tgt[q] = t;
+                bin[q] = (uint16_t)bb;
             }
         }
         __syncthreads();
         // reserve the chunk's run in every coarse bin it touches
-        for (uint32_t b = threadIdx.x; b < a.nb1; b += FB_THREADS) {
+        for (uint32_t b = threadIdx.x; b < a.nb1; b += FBX_THREADS) {
             const uint32_t n = cnt[b];
             cnt[b] = n ? atomicAdd(&a.cnt1[b], n) : 0u;
         }
         __syncthreads();
-#pragma unroll 4
-        for (int k = 0; k < FB_PER; ++k) {
-            const uint32_t q = k * FB_THREADS + threadIdx.x, t = tgt[q];
-            if (t == 0xFFFFFFFFu) continue;
-            const uint32_t i = (uint32_t)(c0 + q), b = t >> a.s1;
-            const uint32_t pos = cnt[b] + rank[q];
-            if (pos >= a.cap1) {
-                atomicOr(a.overflow, 1u);
-                continue;
+        // FB_BATCH senders' (s, w) loads in flight before their stores (the
+        // stores could alias the loads, so the compiler would not hoist them)
+#pragma unroll
+        for (int k0 = 0; k0 < FB_PER; k0 += FB_BATCH) {
+            double2 sv[FB_BATCH];
+            uint32_t o32[FB_BATCH];
+#pragma unroll
+            for (int k = 0; k < FB_BATCH; ++k) {
+                const uint32_t q = (k0 + k) * FBX_THREADS + threadIdx.x, b = bin[q];
+                o32[k] = 0xFFFFFFFFu;
+                sv[k] = make_double2(0.0, 0.0);
+                if (b != FB_NONE) {
+                    const uint32_t pos = cnt[b] + rank[q];
+                    if (pos < a.cap1) {
+                        o32[k] = b;  // bin; the position is recomputed below
+                        sv[k] = a.swc[(uint32_t)(c0 + q)];
+                    } else {
+                        atomicOr(a.overflow, 1u);
+                    }
+                }
             }
-            const double2 sv = a.swc[i];
-            const size_t o = (size_t)b * a.cap1 + pos;
-            a.hdr1[o] = make_uint2(t, i);
-            a.pay1[o] = make_double2(sv.x * 0.5, sv.y * 0.5);
+#pragma unroll
+            for (int k = 0; k < FB_BATCH; ++k) {
+                if (o32[k] == 0xFFFFFFFFu) continue;
+                const uint32_t q = (k0 + k) * FBX_THREADS + threadIdx.x;
+                const size_t o = (size_t)o32[k] * a.cap1 + cnt[o32[k]] + rank[q];
+                a.hdr1[o] = (uint32_t)(c0 + q);
+                a.pay1[o] = make_double2(sv[k].x * 0.5, sv[k].y * 0.5);
+            }
         }
         __syncthreads();
     }
@@ -138,7 +167,7 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_send(FullBinArgs a, uint32_t 
 
 // ---------------------------------------------------------------- B: coarse -> fine bins
 // Work item w = (coarse bin, chunk of FB_CHUNK of its messages).
-__global__ __launch_bounds__(FB_THREADS) void k_fb_split(FullBinArgs a) {
+__global__ __launch_bounds__(FBX_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_fb_split(FullBinArgs a, uint32_t r) {
     __shared__ uint32_t cnt[FB_MAXBINS];
     __shared__ uint16_t rank[FB_CHUNK];
     __shared__ uint16_t fine[FB_CHUNK];
@@ -151,30 +180,64 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_split(FullBinArgs a) {
         const uint32_t q0 = c * FB_CHUNK;
         if (q0 >= n_bin) continue;  // block-uniform
         const uint32_t n = min((uint32_t)FB_CHUNK, n_bin - q0);
-        for (uint32_t f = threadIdx.x; f < nfine; f += FB_THREADS) cnt[f] = 0u;
+        for (uint32_t f = threadIdx.x; f < nfine; f += FBX_THREADS) cnt[f] = 0u;
         __syncthreads();
         const size_t base = (size_t)b * a.cap1 + q0;
-        for (uint32_t q = threadIdx.x; q < n; q += FB_THREADS) {
-            const uint32_t f = (a.hdr1[base + q].x >> FB_TB) & (nfine - 1u);
-            fine[q] = (uint16_t)f;
-            rank[q] = (uint16_t)atomicAdd(&cnt[f], 1u);
+        constexpr int PB = 4;
+#pragma unroll 1
+        for (int k0 = 0; k0 < FB_PER; k0 += PB) {
+            uint32_t node[PB], x[PB], y[PB];
+#pragma unroll
+            for (int k = 0; k < PB; ++k) {
+                const uint32_t q = (k0 + k) * FBX_THREADS + threadIdx.x;
+                node[k] = q < n ? a.hdr1[base + q] : 0u;
+            }
+            philox2_batch<PB>(node, r, S_PUSHSUM, a.k0, a.k1, x, y);
+#pragma unroll
+            for (int k = 0; k < PB; ++k) {
+                const uint32_t q = (k0 + k) * FBX_THREADS + threadIdx.x;
+                if (q < n) {
+                    const uint32_t t = full_target(node[k], uniform_from(x[k], y[k], a.P - 1));
+                    const uint32_t f = (t >> FB_TB) & (nfine - 1u);
+                    fine[q] = (uint16_t)f;
+                    rank[q] = (uint16_t)atomicAdd(&cnt[f], 1u);
+                }
+            }
         }
         __syncthreads();
         const uint32_t f0 = b << (a.s1 - FB_TB);  // first fine tile of the coarse bin
-        for (uint32_t f = threadIdx.x; f < nfine; f += FB_THREADS) {
+        for (uint32_t f = threadIdx.x; f < nfine; f += FBX_THREADS) {
             const uint32_t m = cnt[f];
             cnt[f] = m && f0 + f < a.nb2 ? atomicAdd(&a.cnt2[f0 + f], m) : 0u;
         }
         __syncthreads();
-        for (uint32_t q = threadIdx.x; q < n; q += FB_THREADS) {
-            const uint32_t f = fine[q], pos = cnt[f] + rank[q];
-            if (f0 + f >= a.nb2 || pos >= a.cap2) {
-                atomicOr(a.overflow, 1u);
-                continue;
+#pragma unroll 1
+        for (int k0 = 0; k0 < FB_PER; k0 += FB_BATCH) {
+            uint32_t h[FB_BATCH];
+            double2 pv[FB_BATCH];
+#pragma unroll
+            for (int k = 0; k < FB_BATCH; ++k) {
+                const uint32_t q = (k0 + k) * FBX_THREADS + threadIdx.x;
+                h[k] = 0u;
+                pv[k] = make_double2(0.0, 0.0);
+                if (q < n) {
+                    h[k] = a.hdr1[base + q];
+                    pv[k] = a.pay1[base + q];
+                }
             }
-            const size_t o = (size_t)(f0 + f) * a.cap2 + pos;
-            a.hdr2[o] = a.hdr1[base + q];
-            a.pay2[o] = a.pay1[base + q];
+#pragma unroll
+            for (int k = 0; k < FB_BATCH; ++k) {
+                const uint32_t q = (k0 + k) * FBX_THREADS + threadIdx.x;
+                if (q >= n) continue;
+                const uint32_t f = fine[q], pos = cnt[f] + rank[q];
+                if (f0 + f >= a.nb2 || pos >= a.cap2) {
+                    atomicOr(a.overflow, 1u);
+                    continue;
+                }
+                const size_t o = (size_t)(f0 + f) * a.cap2 + pos;
+                a.hdr2[o] = h[k];
+                a.pay2[o] = pv[k];
+            }
         }
         __syncthreads();
     }
@@ -188,29 +251,65 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_fold(FullBinArgs a, uint32_t 
     __shared__ uint32_t src[FB_CAP2];             // message sender ids in receiver order
     __shared__ uint16_t idx[FB_CAP2];             // message index in the fine bin, receiver order
     __shared__ uint16_t rnk[FB_CAP2];
+    __shared__ uint16_t loc[FB_CAP2];             // message's receiver within the tile
     __shared__ uint32_t tmp[FB_THREADS / 64];
     __shared__ uint32_t red[2][FB_THREADS / 64];
     Ctl* ctl = a.ctl;
     if (ld_agent(&ctl->done)) return;
     const uint32_t P = a.P;
+    const double2* __restrict__ swc = a.swc;
+    const double2* __restrict__ pay2 = a.pay2;
+    double2* __restrict__ swn = a.swn;
+    uint8_t* __restrict__ nbp = a.nb;
     uint32_t alerts = 0, newly = 0;
     for (uint32_t f = blockIdx.x; f < a.nb2; f += gridDim.x) {
         const uint32_t n = min(ld_agent(&a.cnt2[f]), (uint32_t)a.cap2);
         const size_t base = (size_t)f * a.cap2;
         for (uint32_t v = threadIdx.x; v < TILE; v += FB_THREADS) cnt[v] = 0u;
         __syncthreads();
-        for (uint32_t q = threadIdx.x; q < n; q += FB_THREADS)
-            rnk[q] = (uint16_t)atomicAdd(&cnt[a.hdr2[base + q].x & (TILE - 1)], 1u);
+        {
+            // the tile's messages, FQ per thread: senders loaded together, targets
+            // recomputed as one Philox batch
+            constexpr int FQ = (FB_CAP2 + FB_THREADS - 1) / FB_THREADS;
+            uint32_t snd[FQ], x[FQ], y[FQ];
+#pragma unroll
+            for (int k = 0; k < FQ; ++k) {
+                const uint32_t q = k * FB_THREADS + threadIdx.x;
+                snd[k] = q < n ? a.hdr2[base + q] : 0u;
+            }
+            philox2_batch<FQ>(snd, r, S_PUSHSUM, a.k0, a.k1, x, y);
+#pragma unroll
+            for (int k = 0; k < FQ; ++k) {
+                const uint32_t q = k * FB_THREADS + threadIdx.x;
+                if (q < n) {
+                    const uint32_t v = full_target(snd[k], uniform_from(x[k], y[k], P - 1)) & (TILE - 1);
+                    loc[q] = (uint16_t)v;
+                    rnk[q] = (uint16_t)atomicAdd(&cnt[v], 1u);
+                }
+            }
+        }
         __syncthreads();
-        lds_excl_scan(cnt, TILE, tmp);
+        lds_excl_scan<FB_THREADS>(cnt, TILE, tmp);
         if (threadIdx.x == 0) cnt[TILE] = n;
         for (uint32_t q = threadIdx.x; q < n; q += FB_THREADS) {
-            const uint2 h = a.hdr2[base + q];
-            const uint32_t p = cnt[h.x & (TILE - 1)] + rnk[q];
-            src[p] = h.y;
+            const uint32_t p = cnt[loc[q]] + rnk[q];
+            src[p] = a.hdr2[base + q];
             idx[p] = (uint16_t)q;
         }
         __syncthreads();
+        // every node's byte and (s, w) in flight before any store of the tile
+        uint8_t bk[NPT];
+        double2 svk[NPT];
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            const uint32_t j = f * TILE + k * FB_THREADS + threadIdx.x;
+            bk[k] = 0;
+            svk[k] = make_double2(0.0, 1.0);
+            if (j < P) {
+                bk[k] = nbp[j];
+                svk[k] = swc[j];
+            }
+        }
 #pragma unroll
         for (int k = 0; k < NPT; ++k) {
             const uint32_t v = k * FB_THREADS + threadIdx.x;
@@ -231,13 +330,13 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_fold(FullBinArgs a, uint32_t 
                 src[q] = s;
                 idx[q] = x;
             }
-            const uint8_t b = a.nb[j];
-            const double2 sv = a.swc[j];
+            const uint8_t b = bk[k];
+            const double2 sv = svk[k];
             const bool active = (b & B_ACTIVE) != 0;
             double acc_s = active && P > 1 ? sv.x * 0.5 : sv.x;
             double acc_w = active && P > 1 ? sv.y * 0.5 : sv.y;
             for (uint32_t p = p0; p < p1; ++p) {
-                const double2 m = a.pay2[base + idx[p]];  // already halved by the sender
+                const double2 m = pay2[base + idx[p]];  // already halved by the sender
                 acc_s = acc_s + m.x;
                 acc_w = acc_w + m.y;
             }
@@ -258,9 +357,9 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_fold(FullBinArgs a, uint32_t 
                     ++newly;
                     flags |= B_ACTIVE;
                 }
-                a.nb[j] = (uint8_t)flags;
+                nbp[j] = (uint8_t)flags;
             }
-            a.swn[j] = make_double2(acc_s, acc_w);
+            swn[j] = make_double2(acc_s, acc_w);
         }
         __syncthreads();
     }
@@ -311,10 +410,10 @@ hipError_t launch_full_bin_round(const FullBinArgs& a, uint32_t round, int grid,
     if ((e = hipMemsetAsync(a.cnt1, 0, sizeof(uint32_t) * a.nb1, st)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(a.cnt2, 0, sizeof(uint32_t) * a.nb2, st)) != hipSuccess) return e;
     const uint32_t chunks = (a.P + FB_CHUNK - 1) / FB_CHUNK;
-    hipLaunchKernelGGL(k_fb_send, dim3(std::min<uint32_t>(chunks, (uint32_t)grid)), dim3(FB_THREADS), 0, st, a,
-                       round);
+    const uint32_t gx = (uint32_t)std::max(1, grid / 4);  // 1024-thread blocks
+    hipLaunchKernelGGL(k_fb_send, dim3(std::min<uint32_t>(chunks, gx)), dim3(FBX_THREADS), 0, st, a, round);
     const uint32_t items = a.nb1 * ((a.cap1 + FB_CHUNK - 1) / FB_CHUNK);
-    hipLaunchKernelGGL(k_fb_split, dim3(std::min<uint32_t>(items, (uint32_t)grid)), dim3(FB_THREADS), 0, st, a);
+    hipLaunchKernelGGL(k_fb_split, dim3(std::min<uint32_t>(items, gx)), dim3(FBX_THREADS), 0, st, a, round);
     hipLaunchKernelGGL(k_fb_fold, dim3(std::min<uint32_t>(a.nb2, (uint32_t)grid)), dim3(FB_THREADS), 0, st, a,
                        round);
     return hipGetLastError();

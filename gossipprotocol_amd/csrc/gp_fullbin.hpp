@@ -27,9 +27,9 @@ struct FullBinArgs {
     uint32_t s1, nb1, nb2, cap1, cap2;
     uint32_t* cnt1;      // [nb1] messages per coarse bin (zeroed every round)
     uint32_t* cnt2;      // [nb2] messages per fine tile
-    uint2* hdr1;         // [nb1 * cap1] {target, sender}
+    uint32_t* hdr1;      // [nb1 * cap1] sender id (the target is recomputed from its Philox draw)
     double2* pay1;       // [nb1 * cap1] {s / 2, w / 2}
-    uint2* hdr2;         // [nb2 * cap2]
+    uint32_t* hdr2;      // [nb2 * cap2] sender id
     double2* pay2;
 };
 

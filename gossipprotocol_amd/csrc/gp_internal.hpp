@@ -131,6 +131,9 @@ struct DevState {
     uint8_t* nb[2];
     // gossip: rumour counters (in place), direction byte double buffered (nb)
     int32_t* c;
+    // gossip, Imp3D, column kernel: random-edge rumours each local node receives
+    // this round (k_gossip_redges, before the round kernel), indexed from lo
+    uint16_t* rcnt;
     // Imp3D: bit i of rbits[b] = node i sends on its random edge in the round
     // of buffer b (ballot-packed by the round kernel)
     uint64_t* rbits[2];
@@ -151,7 +154,7 @@ struct DevState {
     // push-sum, one rank: two-level LDS binning of the round's messages (gp_fullbin.hip)
     uint32_t fb_s1, fb_nb1, fb_nb2, fb_cap1, fb_cap2;
     uint32_t *fb_cnt1, *fb_cnt2;
-    uint2 *fb_hdr1, *fb_hdr2;
+    uint32_t *fb_hdr1, *fb_hdr2;  // sender ids
     double2 *fb_pay1, *fb_pay2;
     // slab of this rank (single GPU: lo = 0, nloc = P, base = 0): node ids
     // [lo, lo + nloc) are owned; per-node arrays (sw, nb) start at id `base`
@@ -229,6 +232,7 @@ struct WaveArgs {
     const uint32_t* rtag;
     const double2* rmsg;
     int32_t* c;
+    uint16_t* rcnt;          // gossip Imp3D (column kernel): random-edge deliveries per local node
     Ctl* ctl;
     Geom G;
     uint32_t k0, k1, seed_node;

@@ -413,6 +413,7 @@ WaveArgs make_wave_args(const DevState& S, uint32_t round) {
     a.rtag = S.rtag;
     a.rmsg = S.rmsg;
     a.c = S.c;
+    a.rcnt = S.rcnt;
     a.ctl = S.ctl;
     a.G = S.G;
     a.k0 = S.k0;

@@ -225,7 +225,9 @@ or_sim* or_create(int64_t num_nodes, int topology, int algorithm, uint64_t seed,
     s->n = num_nodes; s->P = P; s->T = T; s->g = g;
     s->max_rounds = max_rounds;
 #ifdef _OPENMP
-    s->threads = threads > 0 ? threads : omp_get_max_threads();
+    /* default: all cores, except for small populations, whose rounds are too short
+     * for a fork-join per loop to pay (and oversubscribe when tests run in parallel) */
+    s->threads = threads > 0 ? threads : (P < 262144 ? 1 : omp_get_max_threads());
 #else
     (void)threads;
     s->threads = 1;

@@ -42,6 +42,8 @@ VARIANTS = {  # name -> extra -D flags for gp_round.hip
     "ownearly": ["-DGP_OWN_EARLY=1"],
     "nozdpp": ["-DGP_ZDPP=0"],
     "nozdpp_oe": ["-DGP_ZDPP=0", "-DGP_OWN_EARLY=1"],
+    "t512m6": ["-DGP_TPB=512", "-DGP_NPT=2", "-DGP_MINB=6"],
+    "t1024m8": ["-DGP_TPB=1024", "-DGP_NPT=1", "-DGP_MINB=8"],
 }
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-DGP_EXPERIMENTS"]
 
