@@ -810,8 +810,10 @@ double alg_bytes(const gp_sim* s) {
         // message 20 + own (s, w) r+w 32 + byte r+w 2 (gp_fullbin.hip)
         return 1.0 + 16.0 + 20.0 + 40.0 + 20.0 + 32.0 + 2.0;
     }
-    // gossip: counter r+w 8, direction byte r+w 2 (+ Imp3D in-list 8)
-    if (S.topo == IMP3D) return 18.0;
+    // gossip: counter r+w 8, direction byte r+w 2 (+ Imp3D in-list 8, and with the
+    // separate random-edge delivery pass of the column kernel its per-node count
+    // written and read, 2 + 2)
+    if (S.topo == IMP3D) return S.rcnt ? 22.0 : 18.0;
     if (S.topo != FULL) return 10.0;
     return 4.0 + 8.0 + 8.0 + 8.0;  // send: c + atomic RMW; recv: inc r+w, c r+w
 }

@@ -479,23 +479,89 @@ __global__ __launch_bounds__(BULK_THREADS) void k_gossip_col(WaveArgs a, uint32_
 }
 
 // Imp3D gossip, before the column kernel: per local receiver, how many of its
-// in-edge senders sent it a rumour on their random edge this round
-// (col_sent_random; remote senders by the exchange tag).  Thread per receiver,
-// every receiver independent, so the in_off -> in_src -> bitmap chains of all
-// receivers overlap -- inside the x-march they were three dependent memory
-// round trips per patch step.
+// in-edge senders sent it a rumour on their random edge this round.  Tiles of
+// RE_TILE receivers: the tile's in-edges (receiver-sorted, contiguous) are
+// decided RE_FU per thread -- senders loaded together, their direction draws as
+// one Philox batch, the bitmap read only for the ~1/7 that pick the random slot
+// (col_sent_random), remote senders by the exchange tag -- into a byte per edge
+// in LDS, then every receiver sums its edge range.  Inside the x-march these
+// were three dependent memory round trips per patch step.
+constexpr uint32_t RE_TILE = 1024;
+constexpr int RE_FU = 6;  // staged in-edges per thread: 1536 per tile (mean 1024, 16 sigma)
+
 __global__ __launch_bounds__(BULK_THREADS) void k_gossip_redges(WaveArgs a, uint32_t r) {
+    __shared__ uint8_t sent[BULK_THREADS * RE_FU];
     if (ld_agent(&a.ctl->done)) return;
     const uint32_t lo = a.lo, nloc = a.nloc;
-    for (uint32_t lj = blockIdx.x * BULK_THREADS + threadIdx.x; lj < nloc; lj += gridDim.x * BULK_THREADS) {
-        const uint32_t eb = a.in_off[lj], ee = a.in_off[lj + 1];
-        uint32_t n = 0;
-        for (uint32_t e = eb; e < ee; ++e) {
-            const uint32_t i = a.in_src[e];
-            if (i - lo >= nloc) n += a.rtag[e] == r ? 1u : 0u;  // sender on another rank
-            else n += col_sent_random(a, i, r, false, S_GOSSIP) ? 1u : 0u;
+    const Geom& G = a.G;
+    constexpr int NPT = RE_TILE / BULK_THREADS;
+    const uint32_t ntl = (nloc + RE_TILE - 1) / RE_TILE;
+    for (uint32_t t = blockIdx.x; t < ntl; t += gridDim.x) {
+        const uint32_t j0 = t * RE_TILE, j1 = min(nloc, j0 + RE_TILE);  // local receiver ids
+        const uint32_t e_lo = a.in_off[j0], e_hi = a.in_off[j1];
+        const uint32_t cnt = e_hi - e_lo;
+        const bool staged = cnt <= (uint32_t)(BULK_THREADS * RE_FU);
+        uint32_t eb[NPT], ee[NPT];
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            const uint32_t jl = j0 + k * BULK_THREADS + threadIdx.x;
+            eb[k] = ee[k] = 0u;
+            if (jl < j1) {
+                eb[k] = a.in_off[jl];
+                ee[k] = a.in_off[jl + 1];
+            }
         }
-        a.rcnt[lj] = (uint16_t)n;
+        if (staged) {
+            uint32_t src[RE_FU], di[RE_FU], wrd[RE_FU], zb[RE_FU], X[RE_FU], Y[RE_FU];
+#pragma unroll
+            for (int m = 0; m < RE_FU; ++m) {
+                const uint32_t q = threadIdx.x + m * BULK_THREADS;
+                src[m] = q < cnt ? a.in_src[e_lo + q] : lo;
+            }
+#pragma unroll
+            for (int m = 0; m < RE_FU; ++m) {
+                const uint32_t i = src[m];
+                const uint32_t x = fastdiv(i, G.div_g2);
+                const uint32_t rem = i - x * G.g2;
+                const uint32_t y = fastdiv(rem, G.div_g);
+                const uint32_t z = rem - y * G.g;
+                di[m] = popc6(mask_xyz(x, y, z, G.g - 1)) + 1u;
+                wrd[m] = i - lo < nloc ? col_rb_word(a, x, y, z) : 0u;
+                zb[m] = z & 63u;
+            }
+            philox2_batch<RE_FU>(src, r, S_GOSSIP, a.k0, a.k1, X, Y);
+            unsigned long long w[RE_FU];
+#pragma unroll
+            for (int m = 0; m < RE_FU; ++m) {
+                const uint32_t q = threadIdx.x + m * BULK_THREADS;
+                const uint32_t i = src[m];
+                w[m] = 0ull;
+                if (q < cnt) {
+                    if (i - lo >= nloc) w[m] = a.rtag[e_lo + q] == r ? ~0ull : 0ull;  // sender on another rank
+                    else if (uniform_from(X[m], Y[m], di[m]) == di[m] - 1u) w[m] = a.rbc[wrd[m]];
+                }
+            }
+#pragma unroll
+            for (int m = 0; m < RE_FU; ++m) sent[threadIdx.x + m * BULK_THREADS] = (uint8_t)((w[m] >> zb[m]) & 1ull);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            const uint32_t jl = j0 + k * BULK_THREADS + threadIdx.x;
+            if (jl >= j1) continue;
+            uint32_t n = 0;
+            if (staged) {
+                for (uint32_t e = eb[k]; e < ee[k]; ++e) n += sent[e - e_lo];
+            } else {  // rare: tile in-degree above the staging capacity
+                for (uint32_t e = eb[k]; e < ee[k]; ++e) {
+                    const uint32_t i = a.in_src[e];
+                    if (i - lo >= nloc) n += a.rtag[e] == r ? 1u : 0u;
+                    else n += col_sent_random(a, i, r, false, S_GOSSIP) ? 1u : 0u;
+                }
+            }
+            a.rcnt[jl] = (uint16_t)n;
+        }
+        __syncthreads();
     }
 }
 
@@ -548,7 +614,7 @@ hipError_t launch_round_col(const WaveArgs& a, int topo, int alg, uint32_t round
             hipLaunchKernelGGL(k_gossip_col<GRID3D>, g, b, 0, st, a, round);
         } else {
             if (!a.rcnt) return hipErrorInvalidValue;
-            const uint32_t ge = std::min<uint32_t>((a.nloc + BULK_THREADS - 1) / BULK_THREADS, 256u * 64u);
+            const uint32_t ge = std::min<uint32_t>((a.nloc + RE_TILE - 1) / RE_TILE, 256u * 16u);
             hipLaunchKernelGGL(k_gossip_redges, dim3(std::max(1u, ge)), b, 0, st, a, round);
             hipLaunchKernelGGL(k_gossip_col<IMP3D>, g, b, 0, st, a, round);
         }
