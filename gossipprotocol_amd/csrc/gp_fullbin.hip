@@ -9,7 +9,7 @@
 // (Program.fs:114-123).
 //
 // Per round, three kernels:
-//   A  k_fb_send   senders in chunks of FB_CHUNK: target t = U(P-1) mapped past i
+//   A  k_fb_send   senders in chunks of FBO_CHUNK: target t = U(P-1) mapped past i
 //                  (Philox), LDS counting by coarse bin (t >> s1), one global
 //                  reservation per (chunk, bin), each message {i | s/2, w/2}
 //                  written into its coarse bin's run;
@@ -35,22 +35,18 @@
 namespace gp {
 namespace {
 
-// Passes A and B: 1024-thread blocks over chunks of FB_CHUNK senders / messages
-// (16 per thread), so a chunk writes runs of ~86 (A) and ~32 (B) consecutive
+// Passes A and B: 1024-thread blocks over chunks of FBO_CHUNK senders / messages
+// (8 per thread), so a chunk writes runs of ~43 (A) and ~16 (B) consecutive
 // messages per bin and reserves each run with one global atomic.
 constexpr int FB_THREADS = 256;                    // C
 constexpr int FBX_THREADS = 1024;                  // A, B
-#ifndef GP_FB_PER
-#define GP_FB_PER 16
-#endif
-constexpr int FB_PER = GP_FB_PER;                  // senders / messages per thread per chunk
-constexpr int FB_CHUNK = FBX_THREADS * FB_PER;     // 16384
 constexpr int FB_MAXBINS = 4096;                   // LDS counters of A and B
 constexpr uint32_t FB_NONE = 0xFFFFu;
 #ifndef GP_FB_BATCH
 #define GP_FB_BATCH 8
 #endif
 constexpr int FB_BATCH = GP_FB_BATCH;              // loads issued together before their stores
+
 
 template <typename T>
 __device__ __forceinline__ T ld_agent(const T* p) {
@@ -96,68 +92,76 @@ __device__ uint32_t lds_excl_scan(uint32_t* cnt, uint32_t n, uint32_t* tmp) {
 
 }  // namespace
 
-// ---------------------------------------------------------------- A: send + coarse bins
-__global__ __launch_bounds__(FBX_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_fb_send(FullBinArgs a, uint32_t r) {
-    __shared__ uint32_t cnt[FB_MAXBINS];       // per bin: count, then the chunk's global base
-    __shared__ uint16_t bin[FB_CHUNK];         // coarse bin per sender of the chunk (FB_NONE: inactive)
-    __shared__ uint16_t rank[FB_CHUNK];        // its position in the chunk's run of its bin
+// ---------------------------------------------------------------- A, B: binning passes
+// A chunk's messages are put in bin order in LDS (perm) first, so consecutive
+// threads write consecutive slots of one bin's run (whole lines) instead of 64
+// different runs per store instruction (measured: send 2.06 -> 1.37 ms, split
+// 2.31 -> 2.00 ms at P = 1e8); the payload loads become gathers inside the
+// chunk's input instead.
+constexpr int FBO_PER = 8;
+constexpr int FBO_CHUNK = FBX_THREADS * FBO_PER;  // 8192
+
+__global__ __launch_bounds__(FBX_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_fb_send(FullBinArgs a,
+                                                                                                      uint32_t r) {
+    __shared__ uint32_t loff[FB_MAXBINS];      // per bin: count, then the bin's first position in perm
+    __shared__ uint32_t gb[FB_MAXBINS];        // per bin: the chunk's reserved base in the global bin
+    __shared__ uint16_t bin[FBO_CHUNK];
+    __shared__ uint16_t rank[FBO_CHUNK];
+    __shared__ uint16_t perm[FBO_CHUNK];       // chunk positions in bin order
+    uint32_t* tmp = reinterpret_cast<uint32_t*>(perm);  // scan scratch, used before perm is written
     if (ld_agent(&a.ctl->done)) return;
     const uint32_t P = a.P;
-    for (uint64_t c0 = (uint64_t)blockIdx.x * FB_CHUNK; c0 < P; c0 += (uint64_t)gridDim.x * FB_CHUNK) {
-        for (uint32_t b = threadIdx.x; b < a.nb1; b += FBX_THREADS) cnt[b] = 0u;
+    for (uint64_t c0 = (uint64_t)blockIdx.x * FBO_CHUNK; c0 < P; c0 += (uint64_t)gridDim.x * FBO_CHUNK) {
+        for (uint32_t b = threadIdx.x; b < a.nb1; b += FBX_THREADS) loff[b] = 0u;
         __syncthreads();
-        constexpr int PB = 8;  // Philox chains interleaved per batch
+        {
+            uint32_t node[FBO_PER], x[FBO_PER], y[FBO_PER];
 #pragma unroll
-        for (int k0 = 0; k0 < FB_PER; k0 += PB) {
-            uint32_t node[PB], x[PB], y[PB];
+            for (int k = 0; k < FBO_PER; ++k) node[k] = (uint32_t)(c0 + k * FBX_THREADS + threadIdx.x);
+            philox2_batch<FBO_PER>(node, r, S_PUSHSUM, a.k0, a.k1, x, y);
 #pragma unroll
-            for (int k = 0; k < PB; ++k) node[k] = (uint32_t)(c0 + (k0 + k) * FBX_THREADS + threadIdx.x);
-            philox2_batch<PB>(node, r, S_PUSHSUM, a.k0, a.k1, x, y);
-#pragma unroll
-            for (int k = 0; k < PB; ++k) {
-                const uint32_t i = node[k], q = (k0 + k) * FBX_THREADS + threadIdx.x;
+            for (int k = 0; k < FBO_PER; ++k) {
+                const uint32_t i = node[k], q = k * FBX_THREADS + threadIdx.x;
                 uint32_t bb = FB_NONE;
                 if (i < P && (a.nb[i] & B_ACTIVE) && P > 1) {
                     bb = full_target(i, uniform_from(x[k], y[k], P - 1)) >> a.s1;  // Program.fs:213-215
-                    rank[q] = (uint16_t)atomicAdd(&cnt[bb], 1u);
+                    rank[q] = (uint16_t)atomicAdd(&loff[bb], 1u);
                 }
                 bin[q] = (uint16_t)bb;
             }
         }
         __syncthreads();
-        // reserve the chunk's run in every coarse bin it touches
         for (uint32_t b = threadIdx.x; b < a.nb1; b += FBX_THREADS) {
-            const uint32_t n = cnt[b];
-            cnt[b] = n ? atomicAdd(&a.cnt1[b], n) : 0u;
+            const uint32_t n = loff[b];
+            gb[b] = n ? atomicAdd(&a.cnt1[b], n) : 0u;
+        }
+        const uint32_t total = lds_excl_scan<FBX_THREADS>(loff, a.nb1, tmp);
+#pragma unroll
+        for (int k = 0; k < FBO_PER; ++k) {
+            const uint32_t q = k * FBX_THREADS + threadIdx.x, b = bin[q];
+            if (b != FB_NONE) perm[loff[b] + rank[q]] = (uint16_t)q;
         }
         __syncthreads();
-        // FB_BATCH senders' (s, w) loads in flight before their stores (the
-        // stores could alias the loads, so the compiler would not hoist them)
-#pragma unroll
-        for (int k0 = 0; k0 < FB_PER; k0 += FB_BATCH) {
+        for (uint32_t p0 = 0; p0 < total; p0 += FBX_THREADS * FB_BATCH) {
+            uint32_t qq[FB_BATCH];
             double2 sv[FB_BATCH];
-            uint32_t o32[FB_BATCH];
 #pragma unroll
             for (int k = 0; k < FB_BATCH; ++k) {
-                const uint32_t q = (k0 + k) * FBX_THREADS + threadIdx.x, b = bin[q];
-                o32[k] = 0xFFFFFFFFu;
-                sv[k] = make_double2(0.0, 0.0);
-                if (b != FB_NONE) {
-                    const uint32_t pos = cnt[b] + rank[q];
-                    if (pos < a.cap1) {
-                        o32[k] = b;  // bin; the position is recomputed below
-                        sv[k] = a.swc[(uint32_t)(c0 + q)];
-                    } else {
-                        atomicOr(a.overflow, 1u);
-                    }
-                }
+                const uint32_t p = p0 + k * FBX_THREADS + threadIdx.x;
+                qq[k] = p < total ? perm[p] : 0xFFFFu;
+                sv[k] = qq[k] != 0xFFFFu ? a.swc[(uint32_t)(c0 + qq[k])] : make_double2(0.0, 0.0);
             }
 #pragma unroll
             for (int k = 0; k < FB_BATCH; ++k) {
-                if (o32[k] == 0xFFFFFFFFu) continue;
-                const uint32_t q = (k0 + k) * FBX_THREADS + threadIdx.x;
-                const size_t o = (size_t)o32[k] * a.cap1 + cnt[o32[k]] + rank[q];
-                a.hdr1[o] = (uint32_t)(c0 + q);
+                const uint32_t p = p0 + k * FBX_THREADS + threadIdx.x;
+                if (p >= total) continue;
+                const uint32_t b = bin[qq[k]], pos = gb[b] + (p - loff[b]);
+                if (pos >= a.cap1) {
+                    atomicOr(a.overflow, 1u);
+                    continue;
+                }
+                const size_t o = (size_t)b * a.cap1 + pos;
+                a.hdr1[o] = (uint32_t)(c0 + qq[k]);
                 a.pay1[o] = make_double2(sv[k].x * 0.5, sv[k].y * 0.5);
             }
         }
@@ -165,27 +169,29 @@ __global__ __launch_bounds__(FBX_THREADS) __attribute__((amdgpu_waves_per_eu(8, 
     }
 }
 
-// ---------------------------------------------------------------- B: coarse -> fine bins
-// Work item w = (coarse bin, chunk of FB_CHUNK of its messages).
-__global__ __launch_bounds__(FBX_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_fb_split(FullBinArgs a, uint32_t r) {
-    __shared__ uint32_t cnt[FB_MAXBINS];
-    __shared__ uint16_t rank[FB_CHUNK];
-    __shared__ uint16_t fine[FB_CHUNK];
+__global__ __launch_bounds__(FBX_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_fb_split(FullBinArgs a,
+                                                                                                       uint32_t r) {
+    __shared__ uint32_t loff[FB_MAXBINS];
+    __shared__ uint32_t gb[FB_MAXBINS];
+    __shared__ uint16_t fine[FBO_CHUNK];
+    __shared__ uint16_t rank[FBO_CHUNK];
+    __shared__ uint16_t perm[FBO_CHUNK];
+    uint32_t* tmp = reinterpret_cast<uint32_t*>(perm);  // scan scratch, used before perm is written
     if (ld_agent(&a.ctl->done)) return;
-    const uint32_t per_bin = (a.cap1 + FB_CHUNK - 1) / FB_CHUNK;  // chunk slots per coarse bin
-    const uint32_t nfine = 1u << (a.s1 - FB_TB);                 // fine tiles per coarse bin
+    const uint32_t per_bin = (a.cap1 + FBO_CHUNK - 1) / FBO_CHUNK;
+    const uint32_t nfine = 1u << (a.s1 - FB_TB);
     for (uint32_t w = blockIdx.x; w < a.nb1 * per_bin; w += gridDim.x) {
         const uint32_t b = w / per_bin, c = w % per_bin;
         const uint32_t n_bin = min(ld_agent(&a.cnt1[b]), a.cap1);
-        const uint32_t q0 = c * FB_CHUNK;
+        const uint32_t q0 = c * FBO_CHUNK;
         if (q0 >= n_bin) continue;  // block-uniform
-        const uint32_t n = min((uint32_t)FB_CHUNK, n_bin - q0);
-        for (uint32_t f = threadIdx.x; f < nfine; f += FBX_THREADS) cnt[f] = 0u;
+        const uint32_t n = min((uint32_t)FBO_CHUNK, n_bin - q0);
+        for (uint32_t f = threadIdx.x; f < nfine; f += FBX_THREADS) loff[f] = 0u;
         __syncthreads();
         const size_t base = (size_t)b * a.cap1 + q0;
         constexpr int PB = 4;
 #pragma unroll 1
-        for (int k0 = 0; k0 < FB_PER; k0 += PB) {
+        for (int k0 = 0; k0 < FBO_PER; k0 += PB) {
             uint32_t node[PB], x[PB], y[PB];
 #pragma unroll
             for (int k = 0; k < PB; ++k) {
@@ -200,36 +206,39 @@ __global__ __launch_bounds__(FBX_THREADS) __attribute__((amdgpu_waves_per_eu(8, 
                     const uint32_t t = full_target(node[k], uniform_from(x[k], y[k], a.P - 1));
                     const uint32_t f = (t >> FB_TB) & (nfine - 1u);
                     fine[q] = (uint16_t)f;
-                    rank[q] = (uint16_t)atomicAdd(&cnt[f], 1u);
+                    rank[q] = (uint16_t)atomicAdd(&loff[f], 1u);
                 }
             }
         }
         __syncthreads();
-        const uint32_t f0 = b << (a.s1 - FB_TB);  // first fine tile of the coarse bin
+        const uint32_t f0 = b << (a.s1 - FB_TB);
         for (uint32_t f = threadIdx.x; f < nfine; f += FBX_THREADS) {
-            const uint32_t m = cnt[f];
-            cnt[f] = m && f0 + f < a.nb2 ? atomicAdd(&a.cnt2[f0 + f], m) : 0u;
+            const uint32_t m = loff[f];
+            gb[f] = m && f0 + f < a.nb2 ? atomicAdd(&a.cnt2[f0 + f], m) : 0u;
         }
+        lds_excl_scan<FBX_THREADS>(loff, nfine, tmp);
+        for (uint32_t q = threadIdx.x; q < n; q += FBX_THREADS) perm[loff[fine[q]] + rank[q]] = (uint16_t)q;
         __syncthreads();
 #pragma unroll 1
-        for (int k0 = 0; k0 < FB_PER; k0 += FB_BATCH) {
-            uint32_t h[FB_BATCH];
+        for (uint32_t p0 = 0; p0 < n; p0 += FBX_THREADS * FB_BATCH) {
+            uint32_t qq[FB_BATCH], h[FB_BATCH];
             double2 pv[FB_BATCH];
 #pragma unroll
             for (int k = 0; k < FB_BATCH; ++k) {
-                const uint32_t q = (k0 + k) * FBX_THREADS + threadIdx.x;
+                const uint32_t p = p0 + k * FBX_THREADS + threadIdx.x;
+                qq[k] = p < n ? perm[p] : 0xFFFFu;
                 h[k] = 0u;
                 pv[k] = make_double2(0.0, 0.0);
-                if (q < n) {
-                    h[k] = a.hdr1[base + q];
-                    pv[k] = a.pay1[base + q];
+                if (qq[k] != 0xFFFFu) {
+                    h[k] = a.hdr1[base + qq[k]];
+                    pv[k] = a.pay1[base + qq[k]];
                 }
             }
 #pragma unroll
             for (int k = 0; k < FB_BATCH; ++k) {
-                const uint32_t q = (k0 + k) * FBX_THREADS + threadIdx.x;
-                if (q >= n) continue;
-                const uint32_t f = fine[q], pos = cnt[f] + rank[q];
+                const uint32_t p = p0 + k * FBX_THREADS + threadIdx.x;
+                if (p >= n) continue;
+                const uint32_t f = fine[qq[k]], pos = gb[f] + (p - loff[f]);
                 if (f0 + f >= a.nb2 || pos >= a.cap2) {
                     atomicOr(a.overflow, 1u);
                     continue;
@@ -242,7 +251,6 @@ __global__ __launch_bounds__(FBX_THREADS) __attribute__((amdgpu_waves_per_eu(8, 
         __syncthreads();
     }
 }
-
 // ---------------------------------------------------------------- C: fold per fine tile
 __global__ __launch_bounds__(FB_THREADS) void k_fb_fold(FullBinArgs a, uint32_t r) {
     constexpr int TILE = 1 << FB_TB;
@@ -409,10 +417,10 @@ hipError_t launch_full_bin_round(const FullBinArgs& a, uint32_t round, int grid,
     hipError_t e;
     if ((e = hipMemsetAsync(a.cnt1, 0, sizeof(uint32_t) * a.nb1, st)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(a.cnt2, 0, sizeof(uint32_t) * a.nb2, st)) != hipSuccess) return e;
-    const uint32_t chunks = (a.P + FB_CHUNK - 1) / FB_CHUNK;
     const uint32_t gx = (uint32_t)std::max(1, grid / 4);  // 1024-thread blocks
+    const uint32_t chunks = (a.P + FBO_CHUNK - 1) / FBO_CHUNK;
     hipLaunchKernelGGL(k_fb_send, dim3(std::min<uint32_t>(chunks, gx)), dim3(FBX_THREADS), 0, st, a, round);
-    const uint32_t items = a.nb1 * ((a.cap1 + FB_CHUNK - 1) / FB_CHUNK);
+    const uint32_t items = a.nb1 * ((a.cap1 + FBO_CHUNK - 1) / FBO_CHUNK);
     hipLaunchKernelGGL(k_fb_split, dim3(std::min<uint32_t>(items, gx)), dim3(FBX_THREADS), 0, st, a, round);
     hipLaunchKernelGGL(k_fb_fold, dim3(std::min<uint32_t>(a.nb2, (uint32_t)grid)), dim3(FB_THREADS), 0, st, a,
                        round);

@@ -68,6 +68,9 @@ namespace gp {
 #ifndef GP_OWN_EARLY
 #define GP_OWN_EARLY 0   // own (s, w) loaded ahead of the staging copies (1) or with the lattice gathers (0)
 #endif
+#ifndef GP_EDGE_BATCH
+#define GP_EDGE_BATCH GP_NPT  // in-edge redraws per thread in the first Philox batch (the rest one at a time)
+#endif
 #ifndef GP_ZDPP
 #define GP_ZDPP 1        // push-sum tile kernel: the j+-1 messages from the neighbour lane's registers (DPP)
 #endif
@@ -119,6 +122,7 @@ struct TileLdsP {
     uint32_t out[TILE / 4];
     uint32_t red[2][TPB / 64];
     uint32_t qn[2];                   // walk 3: the block's next item, by iteration parity
+    double2 zb[TPB / 64][NPT][2];     // GP_ZDPP: (s, w) across each wave's ends, slot k: [0] node - 1, [1] node + 64
 };
 
 
@@ -463,7 +467,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                     // the first NPT edges per thread cover a tile's mean in-degree (TILE);
                     // the slots above are drawn only by waves that hold an edge there
                     // (a wave-uniform test: most tiles have fewer than TILE + 64 in-edges)
-                    constexpr int F0 = FU < NPT ? FU : NPT;
+                    constexpr int F0 = FU < GP_EDGE_BATCH ? FU : GP_EDGE_BATCH;
                     uint32_t x[FU], y[FU];
                     {
                         uint32_t n0[F0], x0[F0], y0[F0];
@@ -557,6 +561,14 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
             b_xm = dma_stage_bytes(L.xm, a.nbc, (int64_t)j0 - G.g2, (int64_t)j1 - G.g2, a.ext_lo, a.ext_hi);
             b_xp = dma_stage_bytes(L.xp, a.nbc, (int64_t)j0 + G.g2, (int64_t)j1 + G.g2, a.ext_lo, a.ext_hi);
         }
+        // (s, w) across every wave's ends, slot k: node T + k*TPB + 64 wave - 1 and + 64
+        // (clamped into the node arrays; used only where that neighbour sent)
+        if (GP_ZDPP && lane < 2u * NPT) {
+            int64_t jn = (int64_t)T + (int64_t)((lane >> 1) * TPB + wv * 64u) + ((lane & 1u) ? 64 : -1);
+            if (jn < (int64_t)a.ext_lo) jn = a.ext_lo;
+            if (jn > (int64_t)a.ext_hi) jn = a.ext_hi;
+            __builtin_amdgcn_global_load_lds((gvoid_t*)(swc + jn), (lvoid_t*)&L.zb[wv][0][0], 16, 0, 0);
+        }
         // the tile's in-degrees, a nibble per node (512 bytes; the slab's arrays
         // cover whole tiles, ids outside the slab are 0)
         if (TOPO == IMP3D) dma_copy<DMA_ONCE>(L.ind, reinterpret_cast<const char*>(a.ind4 + T / 2), TILE / 2);
@@ -626,6 +638,9 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                 wcz = rem - wcy * G.g;
             }
             constexpr uint32_t ND = TOPO == LINE ? 2 : 6;
+            // lattice directions gathered from HBM / L2; with GP_ZDPP the j +- 1 ones
+            // (z +- 1, or both line neighbours) are the neighbour lanes' own (s, w)
+            constexpr uint32_t NDG = GP_ZDPP ? (TOPO == LINE ? 0u : 4u) : ND;
             constexpr int NG = GP_NGROUP;  // nodes whose lattice gathers are in flight together
             static_assert(NPT % NG == 0, "node groups");
 #pragma unroll
@@ -650,7 +665,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                     }
                 }
                 uint32_t gb[NG], gmask[NG], gfrom[NG];
-                double2 m[NG][ND];
+                double2 m[NG][NDG > 0 ? NDG : 1];
 #pragma unroll
                 for (int h = 0; h < NG; ++h) {
                     const int k = k0 + h;
@@ -699,24 +714,10 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                     gmask[h] = mask;
                     gfrom[h] = from;
                     if (!GP_OWN_EARLY) own[k] = (j >= j0 && j < j1) ? swc[j] : make_double2(0.0, 1.0);
-                    // j + 1 and j - 1 are the neighbour lanes' nodes: their (s, w) -- own[k]
-                    // of those lanes -- move across by DPP in phase B; a gather here only
-                    // where that lane's node is outside the wave or the tile's valid range
-                    constexpr uint32_t dP = TOPO == LINE ? 1u : 4u, dM = TOPO == LINE ? 0u : 5u;
-                    double2 vP = make_double2(0.0, 0.0), vM = make_double2(0.0, 0.0);
-                    if (GP_ZDPP) {
-                        const bool lane_p = lane < 63u && j + 1u < j1, lane_m = lane > 0u && j > j0;
-                        if (((from >> dP) & 1u) && !lane_p) vP = ld_sw(swc + j + 1);
-                        if (((from >> dM) & 1u) && !lane_m) vM = ld_sw(swc + j - 1);
-                    }
 #pragma unroll
-                    for (uint32_t d = 0; d < ND; ++d)
+                    for (uint32_t d = 0; d < NDG; ++d)
                         if ((GP_ABL_DIRS >> d) & 1) {  // ablation (timing only): no gathers in slot d
                             m[h][d] = make_double2(0.0, 0.0);
-                        } else if (GP_ZDPP && d == dP) {
-                            m[h][d] = vP;
-                        } else if (GP_ZDPP && d == dM) {
-                            m[h][d] = vM;
                         } else if (GP_LMASK) {  // only lanes with a sender load (exec-masked gather)
                             m[h][d] = make_double2(0.0, 0.0);
                             if ((from >> d) & 1u) m[h][d] = ld_sw(swc + nbr<TOPO>(j, d, G));
@@ -734,14 +735,22 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                     const uint32_t j = T + jl;
                     const bool valid = j >= j0 && j < j1;
                     uint32_t dir = DIR_NONE;
-                    if (GP_ZDPP) {  // all lanes active here: DPP reads the neighbour lanes
+                    // j + 1 / j - 1: the neighbour lane's own (s, w) by DPP (all lanes active
+                    // here), across the wave's ends from the values staged in L.zb; a load
+                    // only where that lane's node is outside the tile's valid range
+                    // (partial tiles at slab ends)
+                    double2 zP = make_double2(0.0, 0.0), zM = zP;
+                    if (GP_ZDPP) {
                         constexpr uint32_t dP = TOPO == LINE ? 1u : 4u, dM = TOPO == LINE ? 0u : 5u;
                         const uint32_t from = gfrom[h];
-                        const bool lane_p = lane < 63u && j + 1u < j1, lane_m = lane > 0u && j > j0;
-                        const double2 zup = dpp_double2<0x130>(own[k]);  // wave_shl:1 -- lane + 1's (s, w)
-                        const double2 zdn = dpp_double2<0x138>(own[k]);  // wave_shr:1 -- lane - 1's (s, w)
-                        if (((from >> dP) & 1u) && lane_p) m[h][dP] = zup;
-                        if (((from >> dM) & 1u) && lane_m) m[h][dM] = zdn;
+                        zP = dpp_double2<0x130>(own[k]);  // wave_shl:1 -- lane + 1's (s, w)
+                        zM = dpp_double2<0x138>(own[k]);  // wave_shr:1 -- lane - 1's (s, w)
+                        if (lane == 63u) zP = L.zb[wv][k][1];
+                        if (lane == 0u) zM = L.zb[wv][k][0];
+                        if (!((from >> dP) & 1u)) zP = make_double2(0.0, 0.0);
+                        else if (lane != 63u && j + 1u >= j1) zP = ld_sw(swc + j + 1);
+                        if (!((from >> dM) & 1u)) zM = make_double2(0.0, 0.0);
+                        else if (lane != 0u && j <= j0) zM = ld_sw(swc + j - 1);
                     }
                     if (valid) {
                         const uint32_t b = gb[h], mask = gmask[h], from = gfrom[h];
@@ -768,8 +777,18 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                         };
                         tiny |= (sv.y < 0x1p-1020) | (sv.x != 0.0 && sv.x < 0x1p-1020);
                         bool recv = from != 0;
+                        // lattice slots in slot order: line j-1, j+1; 3D x-1, x+1, y+1, y-1, z+1, z-1
+                        if (GP_ZDPP && TOPO == LINE) {
+                            fold(zM);
+                            fold(zP);
+                        } else {
 #pragma unroll
-                        for (uint32_t d = 0; d < ND; ++d) fold(m[h][d]);
+                            for (uint32_t d = 0; d < NDG; ++d) fold(m[h][d]);
+                            if (GP_ZDPP) {
+                                fold(zP);
+                                fold(zM);
+                            }
+                        }
                         if (TOPO == IMP3D) {
                             uint32_t e_b = e_lo + epre[h], e_e = e_b + edeg[h];
                             if (wide) {
