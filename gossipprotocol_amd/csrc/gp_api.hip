@@ -398,7 +398,11 @@ int build_imp3d(gp_sim* s) {
         S.ind4 = nullptr;
         if (S.alg == PUSHSUM && S.kernel == KERNEL_TILE) {
             if ((rc = dev_alloc_t(s, &S.ind4, ind4_bytes_for(S.lo, S.nloc)))) return rc;
-            HIP_TRY(launch_pack_ind4(S, s->grid, s->stream));
+            uint32_t wide_at = 15;  // in-degree >= 15: the tile reads in_off (gp_round.hip)
+#ifdef GP_EXPERIMENTS
+            if (const char* e = std::getenv("GP_IND4_WIDE")) wide_at = (uint32_t)std::max(1, std::atoi(e));
+#endif
+            HIP_TRY(launch_pack_ind4(S, wide_at, s->grid, s->stream));
         }
         S.nedges = ne;
         S.eb = nullptr;

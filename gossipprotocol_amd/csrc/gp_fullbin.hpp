@@ -6,8 +6,12 @@
 
 namespace gp {
 
-constexpr int FB_TB = 10;        // fine tile = 2^FB_TB receivers (one fold block)
-constexpr int FB_CAP2 = 1536;    // messages per fine tile: 1024 expected + 12 sigma (384) + 128
+#ifndef GP_FB_TB
+#define GP_FB_TB 10
+#endif
+constexpr int FB_TB = GP_FB_TB;  // fine tile = 2^FB_TB receivers (one fold block)
+// messages per fine tile: expected 2^FB_TB + 12 sigma + 128 (1536 at 1024 receivers)
+constexpr int FB_CAP2 = ((1 << FB_TB) + 12 * (1 << (FB_TB / 2)) * (FB_TB % 2 ? 1414 : 1000) / 1000 + 128 + 63) / 64 * 64;
 
 struct FullBinPlan {
     uint32_t s1;    // coarse bin = target >> s1

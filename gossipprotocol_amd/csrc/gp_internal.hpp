@@ -262,7 +262,7 @@ int ps_tile_resident_blocks(int topo, bool remote, int device);
 bool build_walk_list(const DevState& S, std::vector<uint32_t>& list, uint32_t woff[9]);
 hipError_t launch_rbits_init(const DevState& S, int grid, hipStream_t st);
 uint32_t ind4_bytes_for(uint32_t lo, uint32_t nloc);
-hipError_t launch_pack_ind4(const DevState& S, int grid, hipStream_t st);
+hipError_t launch_pack_ind4(const DevState& S, uint32_t wide_at, int grid, hipStream_t st);
 hipError_t launch_pack_src_deg(const uint32_t* src, uint32_t* out, uint32_t n, const Geom& G, int grid,
                                hipStream_t st);
 

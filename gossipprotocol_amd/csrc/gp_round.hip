@@ -664,7 +664,8 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                         edeg[h] = d;
                     }
                 }
-                uint32_t gb[NG], gmask[NG], gfrom[NG];
+                // per node: byte | mask << 8 | from << 14 | in-degree << 20 (one register)
+                uint32_t gst[NG];
                 double2 m[NG][NDG > 0 ? NDG : 1];
 #pragma unroll
                 for (int h = 0; h < NG; ++h) {
@@ -684,7 +685,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                         }
                     }
                     const uint32_t jr = j - b_rows;
-                    gb[h] = lds_byte(L.rows, jr);
+                    const uint32_t gbv = lds_byte(L.rows, jr);
                     uint32_t mask;
                     if (TOPO == LINE) {
                         mask = present_mask<TOPO>(j, G);
@@ -711,8 +712,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                         from &= mask;
                     }
                     if (!(j >= j0 && j < j1)) from = 0u;
-                    gmask[h] = mask;
-                    gfrom[h] = from;
+                    gst[h] = gbv | (mask << 8) | (from << 14) | (edeg[h] << 20);
                     if (!GP_OWN_EARLY) own[k] = (j >= j0 && j < j1) ? swc[j] : make_double2(0.0, 1.0);
 #pragma unroll
                     for (uint32_t d = 0; d < NDG; ++d)
@@ -742,7 +742,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                     double2 zP = make_double2(0.0, 0.0), zM = zP;
                     if (GP_ZDPP) {
                         constexpr uint32_t dP = TOPO == LINE ? 1u : 4u, dM = TOPO == LINE ? 0u : 5u;
-                        const uint32_t from = gfrom[h];
+                        const uint32_t from = (gst[h] >> 14) & 63u;
                         zP = dpp_double2<0x130>(own[k]);  // wave_shl:1 -- lane + 1's (s, w)
                         zM = dpp_double2<0x138>(own[k]);  // wave_shr:1 -- lane - 1's (s, w)
                         if (lane == 63u) zP = L.zb[wv][k][1];
@@ -753,7 +753,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                         else if (lane != 0u && j <= j0) zM = ld_sw(swc + j - 1);
                     }
                     if (valid) {
-                        const uint32_t b = gb[h], mask = gmask[h], from = gfrom[h];
+                        const uint32_t b = gst[h] & 0xFFu, mask = (gst[h] >> 8) & 63u, from = (gst[h] >> 14) & 63u;
                         const uint32_t deg = popc6(mask) + (TOPO == IMP3D ? 1u : 0u);
                         bool active = (b & B_ACTIVE) != 0;
                         const double2 sv = own[k];
@@ -790,7 +790,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                             }
                         }
                         if (TOPO == IMP3D) {
-                            uint32_t e_b = e_lo + epre[h], e_e = e_b + edeg[h];
+                            uint32_t e_b = e_lo + epre[h], e_e = e_b + (gst[h] >> 20);
                             if (wide) {
                                 e_b = a.in_off[j];
                                 e_e = a.in_off[j + 1];
@@ -1360,14 +1360,20 @@ hipError_t launch_pack_src_deg(const uint32_t* src, uint32_t* out, uint32_t n, c
 }
 
 // Nibble in-degrees of the slab's tiles (DevState::ind4) from in_off.
+// wide_at: in-degrees from this value on are stored as 15, the "read in_off"
+// mark (15 in the product; tests lower it to exercise that path).
 __global__ __launch_bounds__(TPB) void k_pack_ind4(const uint32_t* __restrict__ in_off, uint32_t lo, uint32_t nloc,
-                                                   uint32_t j00, uint8_t* __restrict__ out, uint32_t nbytes) {
+                                                   uint32_t j00, uint8_t* __restrict__ out, uint32_t nbytes,
+                                                   uint32_t wide_at) {
     for (uint32_t b = blockIdx.x * TPB + threadIdx.x; b < nbytes; b += gridDim.x * TPB) {
         uint32_t v = 0;
 #pragma unroll
         for (uint32_t h = 0; h < 2; ++h) {
             const uint32_t j = j00 + 2 * b + h;
-            if (j - lo < nloc) v |= min(in_off[j + 1] - in_off[j], 15u) << (4 * h);
+            if (j - lo < nloc) {
+                const uint32_t d = in_off[j + 1] - in_off[j];
+                v |= (d >= wide_at ? 15u : d) << (4 * h);
+            }
         }
         out[b] = (uint8_t)v;
     }
@@ -1375,10 +1381,10 @@ __global__ __launch_bounds__(TPB) void k_pack_ind4(const uint32_t* __restrict__ 
 
 uint32_t ind4_bytes_for(uint32_t lo, uint32_t nloc) { return tiles_for(lo, nloc) * (TILE / 2) + 16u; }
 
-hipError_t launch_pack_ind4(const DevState& S, int grid, hipStream_t st) {
+hipError_t launch_pack_ind4(const DevState& S, uint32_t wide_at, int grid, hipStream_t st) {
     const uint32_t nbytes = tiles_for(S.lo, S.nloc) * (TILE / 2);
     hipLaunchKernelGGL(k_pack_ind4, dim3(grid), dim3(TPB), 0, st, S.in_off - S.lo, S.lo, S.nloc, (S.lo / TILE) * TILE,
-                       S.ind4, nbytes);
+                       S.ind4, nbytes, std::min(wide_at, 15u));
     return hipGetLastError();
 }
 

@@ -225,6 +225,24 @@ def test_tile_walk_and_sender_packing_parity(n, topo, seed, rounds, chk, walk, p
     sim.close()
 
 
+@pytest.mark.parametrize("wide_at", ["2", "4"])
+def test_nibble_wide_tile_fallback_parity(wide_at, monkeypatch):
+    """Push-sum tile kernel: a tile holding a node whose in-degree does not fit the
+    nibble array (>= 15, ~1e-12 of nodes, so never met by chance) reads in_off from
+    HBM for all its nodes.  GP_IND4_WIDE (experiments build) lowers that mark so
+    most (2) or some (4) tiles take the path; bit-exact vs the oracle through
+    activation into steady state."""
+    monkeypatch.setenv("GP_IND4_WIDE", wide_at)
+    n, topo = 512000, "Imp3D"
+    sim, orc = Sim(n, topo, "push-sum", seed=7, experimental=True), Oracle(n, topo, "push-sum", 7)
+    for _ in range(2):
+        ga, oa = sim.step(45), orc.step(45)
+        assert ga == oa
+        assert_same_state("push-sum", sim.state(), orc.state())
+    assert sim.info().active == sim.population
+    sim.close()
+
+
 @pytest.mark.parametrize("kernel", ["col", "tile", "wave"])
 def test_seed_random_edge_round0(kernel, monkeypatch):
     """Many seeds, so that several seed nodes send their round-0 rumour on the random
