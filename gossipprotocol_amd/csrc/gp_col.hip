@@ -24,6 +24,10 @@
 // Built with -ffp-contract=off: the fold must round exactly like the oracle.
 #include "gp_wavecommon.hpp"
 
+#ifndef GP_COL_MINW
+#define GP_COL_MINW 7  // gossip column kernel: waves per SIMD (measured 5..8, profiles/r02/s5_colw.txt)
+#endif
+
 namespace gp {
 namespace {
 
@@ -379,7 +383,7 @@ __global__ __launch_bounds__(BULK_THREADS) void k_ps_col(WaveArgs a, uint32_t r)
 // Deliveries to j = lattice senders pointing here + Imp3D random-edge senders
 // + the injector; all dropped if j was converged at round start (Program.fs:87).
 template <int TOPO>
-__global__ __launch_bounds__(BULK_THREADS) void k_gossip_col(WaveArgs a, uint32_t r) {
+__global__ __launch_bounds__(BULK_THREADS, GP_COL_MINW) void k_gossip_col(WaveArgs a, uint32_t r) {
     Ctl* ctl = a.ctl;
     if (ld_agent(&ctl->done)) return;
     const long long inj = ld_agent(&ctl->inj_target);
