@@ -9,24 +9,29 @@
 // (Program.fs:114-123).
 //
 // Per round, three kernels:
-//   A  k_fb_send   senders in chunks of FBO_CHUNK: target t = U(P-1) mapped past i
-//                  (Philox), LDS counting by coarse bin (t >> s1), one global
-//                  reservation per (chunk, bin), each message {i | s/2, w/2}
-//                  written into its coarse bin's run;
-//   B  k_fb_split  each coarse bin's messages in chunks: the target recomputed
-//                  from the sender's Philox draw, LDS counting by fine tile
-//                  (t >> FB_TB, FB_TILE receivers), reservation, copy;
-//   C  k_fb_fold   one fine tile per block: LDS counting sort of the tile's
-//                  messages by receiver (target recomputed once more), each
-//                  receiver's (few) messages put in ascending sender order,
-//                  folded, ratio test, next state.
+//   A  k_fb_send   ranges of senders (GP_FB_RANGE chunks of FBR_CHUNK, one
+//                  1024-thread block each): target t = U(P-1) mapped past i
+//                  (Philox); sweep 1 counts the range's messages per coarse bin
+//                  (t >> s1) in LDS and reserves one run per (range, bin); sweep
+//                  2 puts each chunk in bin order in LDS and writes {i | s/2,
+//                  w/2} into the runs, coalesced, the next chunk's loads in
+//                  flight meanwhile;
+//   B  k_fb_split  ranges of each coarse bin's messages, the same two sweeps by
+//                  fine tile (t >> FB_TB), the target recomputed from the
+//                  sender's Philox draw;
+//   C  k_fb_fold   one fine tile per block: the tile's messages loaded in bin
+//                  order (coalesced), LDS counting sort by receiver (target
+//                  recomputed once more) with the payloads, each receiver's (few)
+//                  messages put in ascending sender order, folded from LDS, ratio
+//                  test, next state.
 // Order inside a bin is whatever the LDS atomics produce; the fold restores the
 // canonical order by sender id, so results do not depend on it.  Every message
 // is moved as 20 bytes (sender id 4 + payload 16; recomputing the target costs
-// a Philox draw per pass instead of 4 bytes per move), each pass coalesced -- no
-// random 16-byte gather of a sender's (s, w) anywhere.  Bin capacities are the
+// a Philox draw per pass instead of 4 bytes per move), every global access is
+// coalesced -- no random 16-byte gather anywhere.  Bin capacities are the
 // expected load + 12 sigma + slack; an overflow is flagged (Ctl::overflow) and
-// fails the batch in gp_step.
+// fails the batch in gp_step.  GP_FB_V2=0 builds the round-2 version (per-chunk
+// reservations, payloads gathered in bin order) for A/B measurements.
 #include <algorithm>
 #include <cmath>
 
@@ -35,17 +40,12 @@
 namespace gp {
 namespace {
 
-// Passes A and B: 1024-thread blocks over chunks of FBO_CHUNK senders / messages
-// (8 per thread), so a chunk writes runs of ~43 (A) and ~16 (B) consecutive
-// messages per bin and reserves each run with one global atomic.
-constexpr int FB_THREADS = 256;                    // C
-constexpr int FBX_THREADS = 1024;                  // A, B
+constexpr int FB_THREADS = 256;                    // C (GP_FB_V2=0)
 constexpr int FB_MAXBINS = 4096;                   // LDS counters of A and B
 constexpr uint32_t FB_NONE = 0xFFFFu;
-#ifndef GP_FB_BATCH
-#define GP_FB_BATCH 8
+#ifndef GP_FB_V2
+#define GP_FB_V2 1  // range binning (1) or per-chunk binning with payload gathers (0, round-2 version)
 #endif
-constexpr int FB_BATCH = GP_FB_BATCH;              // loads issued together before their stores
 
 
 template <typename T>
@@ -54,9 +54,22 @@ __device__ __forceinline__ T ld_agent(const T* p) {
 }
 
 
+// Workgroup barrier for LDS traffic only: waits for this wave's LDS operations,
+// not for its global loads (__syncthreads waits vmcnt(0) too), so loads issued
+// ahead -- the next chunk's input -- stay in flight across it.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <bool LDS_ONLY>
+__device__ __forceinline__ void block_barrier() {
+    if (LDS_ONLY)
+        lds_barrier();
+    else
+        __syncthreads();
+}
+
 // Exclusive scan of cnt[0..n) in LDS (n <= FB_MAXBINS), one block of NT threads;
 // returns the total.
-template <int NT>
+template <int NT, bool LDS_ONLY = false>
 __device__ uint32_t lds_excl_scan(uint32_t* cnt, uint32_t n, uint32_t* tmp) {
     constexpr int PER = (FB_MAXBINS + NT - 1) / NT;
     uint32_t v[PER], s = 0;
@@ -74,7 +87,7 @@ __device__ uint32_t lds_excl_scan(uint32_t* cnt, uint32_t n, uint32_t* tmp) {
         if (lane >= o) incl += t;
     }
     if (lane == 63) tmp[wid] = incl;
-    __syncthreads();
+    block_barrier<LDS_ONLY>();
     uint32_t wbase = 0, total = 0;
     for (int w = 0; w < NT / 64; ++w) {
         if (w < wid) wbase += tmp[w];
@@ -86,13 +99,255 @@ __device__ uint32_t lds_excl_scan(uint32_t* cnt, uint32_t n, uint32_t* tmp) {
         if (b + k < n) cnt[b + k] = run;
         run += v[k];
     }
-    __syncthreads();
+    block_barrier<LDS_ONLY>();
     return total;
 }
 
 }  // namespace
 
 // ---------------------------------------------------------------- A, B: binning passes
+#if GP_FB_V2
+// Range binning (default).  A work item is a range of FBR_RANGE chunks of
+// FBR_CHUNK messages (A: senders; B: one coarse bin's messages), one 1024-thread
+// block per item:
+//   sweep 1  keys of every message of the range (Philox), LDS counts per bin;
+//            one global reservation per (range, bin) -- the range's messages of
+//            a bin then occupy one contiguous run of that bin;
+//   sweep 2  per chunk: loads in input order (coalesced), keys again, LDS rank
+//            per bin, the chunk put in bin order in LDS (payload, header, slot),
+//            written out in that order: consecutive threads write consecutive
+//            slots of one bin, and consecutive chunks continue the same runs.
+// No gather anywhere (the previous version gathered payloads in bin order from
+// an input window larger than the XCD's L2), and reservations drop from one per
+// (chunk, bin) to one per (range, bin).
+#ifndef GP_FBR_THREADS
+#define GP_FBR_THREADS 1024
+#endif
+constexpr int FBR_THREADS = GP_FBR_THREADS;
+constexpr int FBR_PER = 4;
+constexpr int FBR_CHUNK = FBR_THREADS * FBR_PER;
+#ifndef GP_FB_RANGE
+#define GP_FB_RANGE 4
+#endif
+constexpr uint32_t FBR_ITEM = (uint32_t)GP_FB_RANGE * FBR_CHUNK;  // messages per work item
+
+struct FbRangeLds {
+    double2 pay[FBR_CHUNK];     // the chunk's payloads in bin order
+    uint32_t hdr[FBR_CHUNK];    // sender ids in bin order
+    uint32_t pos[FBR_CHUNK];    // slot in the bin
+    uint16_t key[FBR_CHUNK];    // bin
+    uint32_t tmp[FBR_THREADS / 64];
+};
+// Dynamic LDS, 2 x nbins words (launch_full_bin_round): cnt = the chunk's count
+// per bin, then its first LDS position; base = the range's count per bin, then
+// the bin's next slot.
+extern __shared__ uint32_t fbr_dyn[];
+
+// Sweep 2's tail for one chunk whose keys / ranks are in registers: LDS bin
+// order, running slots, coalesced write-out.  LDS-only barriers, so the next
+// chunk's loads (issued before this call) stay in flight.
+__device__ __forceinline__ void fbr_emit(FbRangeLds& L, uint32_t* cnt, uint32_t* base, uint32_t nbins, const uint32_t (&key)[FBR_PER],
+                                         const uint32_t (&rank)[FBR_PER], const uint32_t (&hdr)[FBR_PER],
+                                         const double2 (&pay)[FBR_PER], uint32_t* __restrict__ ohdr,
+                                         double2* __restrict__ opay, uint32_t cap, uint32_t obin0, uint32_t nbins_out,
+                                         unsigned int* overflow) {
+    const uint32_t total = lds_excl_scan<FBR_THREADS, true>(cnt, nbins, L.tmp);
+#pragma unroll
+    for (int k = 0; k < FBR_PER; ++k) {
+        if (key[k] == FB_NONE) continue;
+        const uint32_t p = cnt[key[k]] + rank[k];
+        L.pay[p] = pay[k];
+        L.hdr[p] = hdr[k];
+        L.key[p] = (uint16_t)key[k];
+        L.pos[p] = base[key[k]] + rank[k];
+    }
+    lds_barrier();
+    for (uint32_t b = threadIdx.x; b < nbins; b += FBR_THREADS)
+        base[b] += (b + 1 < nbins ? cnt[b + 1] : total) - cnt[b];
+    // fixed trip count: a loop of unknown length would make the compiler wait for
+    // every outstanding load (the next chunk's) before entering it
+#pragma unroll
+    for (int k = 0; k < FBR_PER; ++k) {
+        const uint32_t p = k * FBR_THREADS + threadIdx.x;
+        if (p >= total) break;
+        const uint32_t b = obin0 + L.key[p], pos = L.pos[p];
+        if (pos >= cap || b >= nbins_out) {
+            atomicOr(overflow, 1u);
+            continue;
+        }
+        const size_t o = (size_t)b * cap + pos;
+        ohdr[o] = L.hdr[p];
+        opay[o] = L.pay[p];
+    }
+    lds_barrier();
+}
+
+// one global reservation per bin with messages in this range (base: count -> first slot)
+__device__ __forceinline__ void fbr_reserve(uint32_t* base, uint32_t nbins, uint32_t* gcnt, uint32_t gbin0,
+                                            uint32_t nbins_out) {
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nbins; b += FBR_THREADS) {
+        const uint32_t n = base[b];
+        base[b] = n && gbin0 + b < nbins_out ? atomicAdd(&gcnt[gbin0 + b], n) : 0u;
+    }
+}
+
+// A's input of one chunk: node bytes and (s, w) of its senders.  Loads are
+// unconditional (indices clamped into the range, validity tested at use), so
+// no branch or phi makes the compiler wait for them -- or for the previous
+// chunk's stores, which vmcnt also counts -- before they are consumed.
+struct SendIn {
+    uint8_t nbv[FBR_PER];
+    double2 sv[FBR_PER];
+    __device__ __forceinline__ void load(const FullBinArgs& a, uint64_t c0, uint64_t i1) {
+#pragma unroll
+        for (int k = 0; k < FBR_PER; ++k) {
+            const uint64_t g = std::min<uint64_t>(c0 + k * FBR_THREADS + threadIdx.x, i1 - 1);
+            nbv[k] = a.nb[g];
+            sv[k] = a.swc[g];
+        }
+    }
+};
+
+__global__ __launch_bounds__(FBR_THREADS) void k_fb_send(FullBinArgs a, uint32_t r) {
+    __shared__ FbRangeLds L;
+    if (ld_agent(&a.ctl->done)) return;
+    const uint32_t P = a.P;
+    const uint64_t i0 = (uint64_t)blockIdx.x * FBR_ITEM;
+    if (i0 >= P || P < 2) return;
+    const uint64_t i1 = std::min<uint64_t>(P, i0 + FBR_ITEM);
+    uint32_t* const cnt = fbr_dyn;
+    uint32_t* const base = fbr_dyn + a.nb1;
+    for (uint32_t b = threadIdx.x; b < a.nb1; b += FBR_THREADS) base[b] = 0u;
+    __syncthreads();
+    // sweep 1: coarse bin (target >> s1) of every active sender, counted; two
+    // chunks per iteration (one Philox batch of 2 FBR_PER)
+    constexpr int P2 = 2 * FBR_PER;
+    for (uint64_t c0 = i0; c0 < i1; c0 += 2 * FBR_CHUNK) {
+        uint32_t node[P2], x[P2], y[P2];
+        uint8_t nbv[P2];
+#pragma unroll
+        for (int k = 0; k < P2; ++k) {
+            const uint64_t g = c0 + k * FBR_THREADS + threadIdx.x;
+            node[k] = (uint32_t)g;
+            nbv[k] = a.nb[std::min<uint64_t>(g, i1 - 1)];
+        }
+        philox2_batch<P2>(node, r, S_PUSHSUM, a.k0, a.k1, x, y);
+#pragma unroll
+        for (int k = 0; k < P2; ++k)
+            if ((nbv[k] & B_ACTIVE) && c0 + k * FBR_THREADS + threadIdx.x < i1)  // Program.fs:213-215
+                atomicAdd(&base[full_target(node[k], uniform_from(x[k], y[k], P - 1)) >> a.s1], 1u);
+    }
+    fbr_reserve(base, a.nb1, a.cnt1, 0, a.nb1);
+    // sweep 2: {sender id | s/2, w/2} into the runs; the next chunk's input is
+    // loaded while this one is put in order and written
+    SendIn cur;
+    cur.load(a, i0, i1);
+    for (uint64_t c0 = i0; c0 < i1; c0 += FBR_CHUNK) {
+        for (uint32_t b = threadIdx.x; b < a.nb1; b += FBR_THREADS) cnt[b] = 0u;
+        uint32_t node[FBR_PER], x[FBR_PER], y[FBR_PER], key[FBR_PER], rank[FBR_PER];
+        double2 pay[FBR_PER];
+#pragma unroll
+        for (int k = 0; k < FBR_PER; ++k) node[k] = (uint32_t)(c0 + k * FBR_THREADS + threadIdx.x);
+        philox2_batch<FBR_PER>(node, r, S_PUSHSUM, a.k0, a.k1, x, y);
+        lds_barrier();  // counters zeroed
+#pragma unroll
+        for (int k = 0; k < FBR_PER; ++k) {
+            key[k] = FB_NONE;
+            rank[k] = 0;
+            if ((cur.nbv[k] & B_ACTIVE) && c0 + k * FBR_THREADS + threadIdx.x < i1) {
+                key[k] = full_target(node[k], uniform_from(x[k], y[k], P - 1)) >> a.s1;
+                rank[k] = atomicAdd(&cnt[key[k]], 1u);
+            }
+            pay[k] = make_double2(cur.sv[k].x * 0.5, cur.sv[k].y * 0.5);
+        }
+        cur.load(a, c0 + FBR_CHUNK < i1 ? c0 + FBR_CHUNK : c0, i1);  // (the last chunk reloads itself)
+        lds_barrier();  // ranks counted
+        fbr_emit(L, cnt, base, a.nb1, key, rank, node, pay, a.hdr1, a.pay1, a.cap1, 0, a.nb1, a.overflow);
+    }
+}
+
+// B's input of one chunk: sender ids and payloads of a coarse bin's messages
+// (unconditional loads, as SendIn)
+struct SplitIn {
+    uint32_t node[FBR_PER];
+    double2 pv[FBR_PER];
+    __device__ __forceinline__ void load(const FullBinArgs& a, size_t base, uint32_t c0, uint32_t q1) {
+#pragma unroll
+        for (int k = 0; k < FBR_PER; ++k) {
+            const uint32_t q = min(c0 + k * FBR_THREADS + threadIdx.x, q1 - 1);
+            node[k] = a.hdr1[base + q];
+            pv[k] = a.pay1[base + q];
+        }
+    }
+};
+
+__global__ __launch_bounds__(FBR_THREADS) void k_fb_split(FullBinArgs a, uint32_t r) {
+    __shared__ FbRangeLds L;
+    if (ld_agent(&a.ctl->done)) return;
+    const uint32_t per_bin = (a.cap1 + FBR_ITEM - 1) / FBR_ITEM;
+    const uint32_t b = blockIdx.x / per_bin, c = blockIdx.x % per_bin;
+    const uint32_t n_bin = min(ld_agent(&a.cnt1[b]), a.cap1);
+    const uint32_t q0 = c * FBR_ITEM;
+    if (q0 >= n_bin) return;
+    const uint32_t q1 = min(n_bin, q0 + FBR_ITEM);
+    const uint32_t nfine = 1u << (a.s1 - FB_TB), f0 = b << (a.s1 - FB_TB);
+    const size_t ibase = (size_t)b * a.cap1;
+    uint32_t* const cnt = fbr_dyn;
+    uint32_t* const base = fbr_dyn + nfine;
+    for (uint32_t f = threadIdx.x; f < nfine; f += FBR_THREADS) base[f] = 0u;
+    __syncthreads();
+    // sweep 1: fine tile of every message (target recomputed from the sender's
+    // draw), two chunks per iteration
+    constexpr int P2 = 2 * FBR_PER;
+    for (uint32_t c0 = q0; c0 < q1; c0 += 2 * FBR_CHUNK) {
+        uint32_t node[P2], x[P2], y[P2];
+#pragma unroll
+        for (int k = 0; k < P2; ++k) {
+            node[k] = a.hdr1[ibase + min(c0 + k * FBR_THREADS + threadIdx.x, q1 - 1)];
+        }
+        philox2_batch<P2>(node, r, S_PUSHSUM, a.k0, a.k1, x, y);
+#pragma unroll
+        for (int k = 0; k < P2; ++k)
+            if (c0 + k * FBR_THREADS + threadIdx.x < q1)
+                atomicAdd(&base[(full_target(node[k], uniform_from(x[k], y[k], a.P - 1)) >> FB_TB) & (nfine - 1u)],
+                          1u);
+    }
+    fbr_reserve(base, nfine, a.cnt2, f0, a.nb2);
+    // sweep 2: into the fine tiles' runs, the next chunk loaded meanwhile
+    SplitIn cur;
+    cur.load(a, ibase, q0, q1);
+    for (uint32_t c0 = q0; c0 < q1; c0 += FBR_CHUNK) {
+        for (uint32_t f = threadIdx.x; f < nfine; f += FBR_THREADS) cnt[f] = 0u;
+        uint32_t node[FBR_PER], x[FBR_PER], y[FBR_PER], key[FBR_PER], rank[FBR_PER];
+        double2 pay[FBR_PER];
+#pragma unroll
+        for (int k = 0; k < FBR_PER; ++k) {
+            node[k] = cur.node[k];
+            pay[k] = cur.pv[k];
+        }
+        philox2_batch<FBR_PER>(node, r, S_PUSHSUM, a.k0, a.k1, x, y);
+        lds_barrier();  // counters zeroed
+#pragma unroll
+        for (int k = 0; k < FBR_PER; ++k) {
+            key[k] = FB_NONE;
+            rank[k] = 0;
+            if (c0 + k * FBR_THREADS + threadIdx.x < q1) {
+                key[k] = (full_target(node[k], uniform_from(x[k], y[k], a.P - 1)) >> FB_TB) & (nfine - 1u);
+                rank[k] = atomicAdd(&cnt[key[k]], 1u);
+            }
+        }
+        cur.load(a, ibase, c0 + FBR_CHUNK < q1 ? c0 + FBR_CHUNK : c0, q1);
+        lds_barrier();  // ranks counted
+        fbr_emit(L, cnt, base, nfine, key, rank, node, pay, a.hdr2, a.pay2, a.cap2, f0, a.nb2, a.overflow);
+    }
+}
+#else
+constexpr int FBX_THREADS = 1024;                  // A, B
+#ifndef GP_FB_BATCH
+#define GP_FB_BATCH 8
+#endif
+constexpr int FB_BATCH = GP_FB_BATCH;              // loads issued together before their stores
 // A chunk's messages are put in bin order in LDS (perm) first, so consecutive
 // threads write consecutive slots of one bin's run (whole lines) instead of 64
 // different runs per store instruction (measured: send 2.06 -> 1.37 ms, split
@@ -251,7 +506,156 @@ __global__ __launch_bounds__(FBX_THREADS) __attribute__((amdgpu_waves_per_eu(8, 
         __syncthreads();
     }
 }
+#endif  // GP_FB_V2
 // ---------------------------------------------------------------- C: fold per fine tile
+#if GP_FB_V2
+// One fine tile per block.  The tile's messages (sender id + payload) are loaded
+// in bin order, coalesced, together with the receivers' own bytes and (s, w);
+// targets recomputed as one Philox batch; LDS counting sort by receiver puts
+// sender ids and payloads in receiver order; each receiver's (few) messages are
+// put in ascending sender order (insertion sort of (sender, LDS position)) and
+// folded from LDS -- no gather of the bin's payloads from global memory.
+#ifndef GP_FBF_THREADS
+#define GP_FBF_THREADS 512
+#endif
+constexpr int FBF_THREADS = GP_FBF_THREADS;
+
+__global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t r) {
+    constexpr int TILE = 1 << FB_TB;
+    constexpr int NPT = TILE / FBF_THREADS;
+    constexpr int FQ = (FB_CAP2 + FBF_THREADS - 1) / FBF_THREADS;
+    __shared__ uint32_t cnt[TILE + 1];            // per receiver: count, then start
+    __shared__ double2 msg[FB_CAP2];              // payloads in receiver order
+    __shared__ uint32_t src[FB_CAP2];             // sender ids in receiver order, sorted per receiver
+    __shared__ uint16_t idx[FB_CAP2];             // the message's slot in msg, permuted with src
+    __shared__ uint32_t tmp[FBF_THREADS / 64];
+    __shared__ uint32_t red[2][FBF_THREADS / 64];
+    Ctl* ctl = a.ctl;
+    if (ld_agent(&ctl->done)) return;
+    const uint32_t P = a.P;
+    const double2* __restrict__ swc = a.swc;
+    double2* __restrict__ swn = a.swn;
+    uint8_t* __restrict__ nbp = a.nb;
+    uint32_t alerts = 0, newly = 0;
+    for (uint32_t v = threadIdx.x; v < TILE; v += FBF_THREADS) cnt[v] = 0u;
+    __syncthreads();
+    for (uint32_t f = blockIdx.x; f < a.nb2; f += gridDim.x) {
+        const uint32_t n = min(ld_agent(&a.cnt2[f]), (uint32_t)a.cap2);
+        const size_t base = (size_t)f * a.cap2;
+        // every load of the tile in flight at once (indices clamped, validity at use)
+        uint32_t snd[FQ], x[FQ], y[FQ], vr[FQ], rk[FQ];
+        double ps[FQ], pw[FQ];  // (two scalar arrays: a double2 array here went to scratch)
+        uint8_t bk[NPT];
+        double2 svk[NPT];
+#pragma unroll
+        for (int k = 0; k < FQ; ++k) {
+            const uint32_t q = min((uint32_t)(k * FBF_THREADS + threadIdx.x), n > 0 ? n - 1 : 0u);
+            snd[k] = a.hdr2[base + q];
+            const double2 m = a.pay2[base + q];
+            ps[k] = m.x;
+            pw[k] = m.y;
+        }
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            const uint32_t j = min(f * TILE + k * FBF_THREADS + threadIdx.x, P - 1);
+            bk[k] = nbp[j];
+            svk[k] = swc[j];
+        }
+        philox2_batch<FQ>(snd, r, S_PUSHSUM, a.k0, a.k1, x, y);
+#pragma unroll
+        for (int k = 0; k < FQ; ++k) {
+            const uint32_t q = k * FBF_THREADS + threadIdx.x;
+            vr[k] = full_target(snd[k], uniform_from(x[k], y[k], P - 1)) & (TILE - 1);
+            rk[k] = q < n ? atomicAdd(&cnt[vr[k]], 1u) : 0u;
+        }
+        __syncthreads();
+        lds_excl_scan<FBF_THREADS>(cnt, TILE, tmp);
+        if (threadIdx.x == 0) cnt[TILE] = n;
+#pragma unroll
+        for (int k = 0; k < FQ; ++k) {
+            if (k * FBF_THREADS + threadIdx.x < n) {
+                const uint32_t p = cnt[vr[k]] + rk[k];
+                src[p] = snd[k];
+                msg[p] = make_double2(ps[k], pw[k]);
+                idx[p] = (uint16_t)p;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            const uint32_t v = k * FBF_THREADS + threadIdx.x;
+            const uint32_t j = f * TILE + v;
+            const uint32_t p0 = cnt[v], p1 = j < P ? cnt[v + 1] : p0;
+            // this receiver's messages in ascending sender id (canonical order)
+            for (uint32_t p = p0 + 1; p < p1; ++p) {
+                const uint32_t s = src[p];
+                const uint16_t xi = idx[p];
+                uint32_t q = p;
+                while (q > p0 && src[q - 1] > s) {
+                    src[q] = src[q - 1];
+                    idx[q] = idx[q - 1];
+                    --q;
+                }
+                src[q] = s;
+                idx[q] = xi;
+            }
+            const uint8_t b = bk[k];
+            const double2 sv = svk[k];
+            const bool active = (b & B_ACTIVE) != 0;
+            double acc_s = active && P > 1 ? sv.x * 0.5 : sv.x;
+            double acc_w = active && P > 1 ? sv.y * 0.5 : sv.y;
+            for (uint32_t p = p0; p < p1; ++p) {
+                const double2 m = msg[idx[p]];  // already halved by the sender
+                acc_s = acc_s + m.x;
+                acc_w = acc_w + m.y;
+            }
+            if (p1 > p0) {
+                uint32_t flags = b;
+                if (!(b & B_CONV)) {
+                    const double r_old = sv.x / sv.y;
+                    const double r_new = acc_s / acc_w;
+                    uint32_t c = (b >> CNT_SHIFT) & 3u;
+                    c = fabs(r_new - r_old) > 1e-10 ? 0u : c + 1u;
+                    flags = (flags & ~(3u << CNT_SHIFT)) | (c << CNT_SHIFT);
+                    if (c == 3) {
+                        flags |= B_CONV;
+                        ++alerts;
+                    }
+                }
+                if (!active) {
+                    ++newly;
+                    flags |= B_ACTIVE;
+                }
+                nbp[j] = (uint8_t)flags;
+            }
+            if (j < P) swn[j] = make_double2(acc_s, acc_w);
+        }
+        __syncthreads();
+        for (uint32_t v = threadIdx.x; v < TILE; v += FBF_THREADS) cnt[v] = 0u;
+        __syncthreads();
+    }
+    uint32_t x = alerts, y = newly;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        x += __shfl_xor(x, o, 64);
+        y += __shfl_xor(y, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = x;
+        red[1][threadIdx.x >> 6] = y;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        x = y = 0;
+        for (int w = 0; w < FBF_THREADS / 64; ++w) {
+            x += red[0][w];
+            y += red[1][w];
+        }
+        if (x) atomicAdd(&ctl->round_alerts, (unsigned long long)x);
+        if (y) atomicAdd(&ctl->round_active, (unsigned long long)y);
+    }
+}
+#else
 __global__ __launch_bounds__(FB_THREADS) void k_fb_fold(FullBinArgs a, uint32_t r) {
     constexpr int TILE = 1 << FB_TB;
     constexpr int NPT = TILE / FB_THREADS;
@@ -393,6 +797,8 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_fold(FullBinArgs a, uint32_t 
     }
 }
 
+#endif  // GP_FB_V2
+
 // ---------------------------------------------------------------- host side
 FullBinPlan full_bin_plan(uint32_t P) {
     FullBinPlan p{};
@@ -417,13 +823,26 @@ hipError_t launch_full_bin_round(const FullBinArgs& a, uint32_t round, int grid,
     hipError_t e;
     if ((e = hipMemsetAsync(a.cnt1, 0, sizeof(uint32_t) * a.nb1, st)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(a.cnt2, 0, sizeof(uint32_t) * a.nb2, st)) != hipSuccess) return e;
+#if GP_FB_V2
+    const uint32_t items_a = (uint32_t)(((uint64_t)a.P + FBR_ITEM - 1) / FBR_ITEM);
+    hipLaunchKernelGGL(k_fb_send, dim3(items_a), dim3(FBR_THREADS), 2 * sizeof(uint32_t) * a.nb1, st, a, round);
+    const uint32_t items_b = a.nb1 * ((a.cap1 + FBR_ITEM - 1) / FBR_ITEM);
+    hipLaunchKernelGGL(k_fb_split, dim3(items_b), dim3(FBR_THREADS), 2 * sizeof(uint32_t) * (1u << (a.s1 - FB_TB)), st,
+                       a, round);
+#else
     const uint32_t gx = (uint32_t)std::max(1, grid / 4);  // 1024-thread blocks
     const uint32_t chunks = (a.P + FBO_CHUNK - 1) / FBO_CHUNK;
     hipLaunchKernelGGL(k_fb_send, dim3(std::min<uint32_t>(chunks, gx)), dim3(FBX_THREADS), 0, st, a, round);
     const uint32_t items = a.nb1 * ((a.cap1 + FBO_CHUNK - 1) / FBO_CHUNK);
     hipLaunchKernelGGL(k_fb_split, dim3(std::min<uint32_t>(items, gx)), dim3(FBX_THREADS), 0, st, a, round);
+#endif
+#if GP_FB_V2
+    hipLaunchKernelGGL(k_fb_fold, dim3(std::min<uint32_t>(a.nb2, (uint32_t)grid * 256 / FBF_THREADS)),
+                       dim3(FBF_THREADS), 0, st, a, round);
+#else
     hipLaunchKernelGGL(k_fb_fold, dim3(std::min<uint32_t>(a.nb2, (uint32_t)grid)), dim3(FB_THREADS), 0, st, a,
                        round);
+#endif
     return hipGetLastError();
 }
 
