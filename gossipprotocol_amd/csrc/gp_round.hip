@@ -74,9 +74,19 @@ namespace gp {
 #ifndef GP_ZDPP
 #define GP_ZDPP 1        // push-sum tile kernel: the j+-1 messages from the neighbour lane's registers (DPP)
 #endif
+#ifndef GP_DEFER_ST
+#define GP_DEFER_ST 0    // a node slot's (s, w) store issued after the next slot's loads (measured: no gain)
+#endif
+#ifndef GP_OWN_LDS
+#define GP_OWN_LDS 0     // the tile's own (s, w) staged in LDS by DMA with the other staging copies
+#endif
 #ifndef GP_MINB
+#if GP_OWN_LDS
+#define GP_MINB 3  // 16 KB more LDS per tile: 3 resident workgroups per CU
+#else
 #define GP_MINB 5  // __launch_bounds__ minimum waves per SIMD (= resident 256-thread blocks per CU):
                    // the LDS tile allows 5, so keep VGPRs <= 96 to not lose the fifth
+#endif
 #endif
 
 namespace {
@@ -84,7 +94,10 @@ namespace {
 constexpr int TPB = GP_TPB;                // 256 (experiments: 128)
 constexpr int NPT = GP_NPT;                // nodes per thread per tile
 constexpr int TILE = TPB * NPT;            // 1024
-constexpr int HMAX = 1625;                 // largest lattice edge with g^3 < 2^32
+#ifndef GP_HMAX
+#define GP_HMAX 1625
+#endif
+constexpr int HMAX = GP_HMAX;              // largest lattice edge with g^3 < 2^32 (experiments: smaller)
 constexpr int W_ROWS = (TILE + 2 * HMAX) / 4 + 4;
 constexpr int W_PLANE = TILE / 4 + 4;
 constexpr int SRC_CAP = TILE * 3 / 2;       // gossip: staged in-list entries per tile (mean TILE)
@@ -123,6 +136,9 @@ struct TileLdsP {
     uint32_t red[2][TPB / 64];
     uint32_t qn[2];                   // walk 3: the block's next item, by iteration parity
     double2 zb[TPB / 64][NPT][2];     // GP_ZDPP: (s, w) across each wave's ends, slot k: [0] node - 1, [1] node + 64
+#if GP_OWN_LDS
+    double2 own[TILE];                // the tile's (s, w) at round start
+#endif
 };
 
 
@@ -572,6 +588,10 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
         // the tile's in-degrees, a nibble per node (512 bytes; the slab's arrays
         // cover whole tiles, ids outside the slab are 0)
         if (TOPO == IMP3D) dma_copy<DMA_ONCE>(L.ind, reinterpret_cast<const char*>(a.ind4 + T / 2), TILE / 2);
+#if GP_OWN_LDS
+        // own (s, w) of the tile (default cache policy: neighbouring tiles gather from these lines)
+        dma_copy(L.own + (j0 - T), reinterpret_cast<const char*>(swc + j0), (j1 - j0) * 16u);
+#endif
         GP_STAMP(t2);
         if (dyn && threadIdx.x == 0) L.qn[it & 1] = claim;
         __syncthreads();  // staging copies, in-edge bitmap and gathered messages retired
@@ -643,6 +663,13 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
             constexpr uint32_t NDG = GP_ZDPP ? (TOPO == LINE ? 0u : 4u) : ND;
             constexpr int NG = GP_NGROUP;  // nodes whose lattice gathers are in flight together
             static_assert(NPT % NG == 0, "node groups");
+            // GP_DEFER_ST: slot k's next-round (s, w) is stored after slot k + 1's loads
+            // are issued.  Stored before them, it sat in the in-order vmcnt queue ahead of
+            // those loads, and the compiler's conservative vmcnt(0) before the next slot
+            // (merged loop paths) then waited for the store's completion too.
+            double2 st_v = make_double2(0.0, 0.0);
+            uint32_t st_j = 0;
+            bool st_ok = false;
 #pragma unroll
             for (int k0 = 0; k0 < NPT; k0 += NG) {
                 // phase A: node byte, present mask, lattice senders (from the staged
@@ -713,7 +740,14 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                     }
                     if (!(j >= j0 && j < j1)) from = 0u;
                     gst[h] = gbv | (mask << 8) | (from << 14) | (edeg[h] << 20);
-                    if (!GP_OWN_EARLY) own[k] = (j >= j0 && j < j1) ? swc[j] : make_double2(0.0, 1.0);
+                    // unconditional (index clamped into the tile's valid range; invalid lanes'
+                    // values are never used): a load under a branch made the compiler wait
+                    // for it before issuing the lattice gathers
+#if GP_OWN_LDS
+                    own[k] = L.own[k * TPB + threadIdx.x];  // (invalid lanes: never used)
+#else
+                    if (!GP_OWN_EARLY) own[k] = swc[min(max(j, j0), j1 - 1u)];
+#endif
 #pragma unroll
                     for (uint32_t d = 0; d < NDG; ++d)
                         if ((GP_ABL_DIRS >> d) & 1) {  // ablation (timing only): no gathers in slot d
@@ -724,6 +758,11 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                         } else {
                             m[h][d] = ld_sw(swc + ((from >> d) & 1u ? nbr<TOPO>(j, d, G) : a.ext_hi));
                         }
+                }
+                if (GP_DEFER_ST) {  // the previous slot's store, behind this slot's loads
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (st_ok) st_stream(swn + st_j, st_v);
+                    st_ok = false;
                 }
                 // phase B: canonical fold (own half, lattice slots in slot order, random
                 // edges by ascending sender; every message contributes the sender's half),
@@ -863,7 +902,13 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                             if (active && deg > 0) dir = slot_to_dir_fast(mask, uniform(a.k0, a.k1, S_PUSHSUM, j, r + 1, deg));
                             reinterpret_cast<uint8_t*>(L.out)[jl] = (uint8_t)(flags | dir);
                         }
-                        st_stream(swn + j, make_double2(acc_s, acc_w));
+                        if (GP_DEFER_ST) {
+                            st_v = make_double2(acc_s, acc_w);
+                            st_j = j;
+                            st_ok = true;
+                        } else {
+                            st_stream(swn + j, make_double2(acc_s, acc_w));
+                        }
                     }
                     if (TOPO == IMP3D && !GP_BATCH_DIR) {
                         const unsigned long long bits = __ballot(valid && dir == DIR_RANDOM);
@@ -874,6 +919,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                     }
                 }
             }
+            if (GP_DEFER_ST && st_ok) st_stream(swn + st_j, st_v);
         }
         GP_STAMP(t4);
         // next-round directions of this thread's nodes: one Philox batch
