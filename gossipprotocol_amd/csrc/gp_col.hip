@@ -493,6 +493,23 @@ __global__ __launch_bounds__(BULK_THREADS, GP_COL_MINW) void k_gossip_col(WaveAr
 constexpr uint32_t RE_TILE = 1024;
 constexpr int RE_FU = 6;  // staged in-edges per thread: 1536 per tile (mean 1024, 16 sigma)
 
+// Tiles are software-pipelined one step deep: tile t's edge range and senders
+// were loaded during the previous tile of this block, so a tile costs one
+// exposed memory round trip (the bitmap reads of its picks) instead of three
+// (range -> senders -> bitmap).  Loads are unconditional where possible
+// (clamped indices) and the barriers wait for LDS only, so the next tile's
+// loads stay in flight across them.
+__device__ __forceinline__ void redges_src(const WaveArgs& a, uint32_t e_lo, uint32_t e_hi, uint32_t (&src)[RE_FU]) {
+    const uint32_t cnt = e_hi - e_lo;
+#pragma unroll
+    for (int m = 0; m < RE_FU; ++m) {
+        const uint32_t q = threadIdx.x + m * BULK_THREADS;
+        src[m] = a.in_src[cnt ? e_lo + min(q, cnt - 1u) : 0u];  // lanes with q >= cnt: never used
+    }
+}
+
+__device__ __forceinline__ void lds_barrier_only() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 __global__ __launch_bounds__(BULK_THREADS) void k_gossip_redges(WaveArgs a, uint32_t r) {
     __shared__ uint8_t sent[BULK_THREADS * RE_FU];
     if (ld_agent(&a.ctl->done)) return;
@@ -500,28 +517,31 @@ __global__ __launch_bounds__(BULK_THREADS) void k_gossip_redges(WaveArgs a, uint
     const Geom& G = a.G;
     constexpr int NPT = RE_TILE / BULK_THREADS;
     const uint32_t ntl = (nloc + RE_TILE - 1) / RE_TILE;
-    for (uint32_t t = blockIdx.x; t < ntl; t += gridDim.x) {
+    uint32_t t = blockIdx.x;
+    if (t >= ntl) return;
+    uint32_t e_lo = a.in_off[t * RE_TILE], e_hi = a.in_off[min(nloc, t * RE_TILE + RE_TILE)];
+    uint32_t src[RE_FU];
+    redges_src(a, e_lo, e_hi, src);
+    for (;;) {
         const uint32_t j0 = t * RE_TILE, j1 = min(nloc, j0 + RE_TILE);  // local receiver ids
-        const uint32_t e_lo = a.in_off[j0], e_hi = a.in_off[j1];
+        const uint32_t tn = t + gridDim.x;
+        const bool more = tn < ntl;  // block-uniform
         const uint32_t cnt = e_hi - e_lo;
         const bool staged = cnt <= (uint32_t)(BULK_THREADS * RE_FU);
         uint32_t eb[NPT], ee[NPT];
 #pragma unroll
         for (int k = 0; k < NPT; ++k) {
-            const uint32_t jl = j0 + k * BULK_THREADS + threadIdx.x;
-            eb[k] = ee[k] = 0u;
-            if (jl < j1) {
-                eb[k] = a.in_off[jl];
-                ee[k] = a.in_off[jl + 1];
-            }
+            const uint32_t jl = min(j0 + k * BULK_THREADS + threadIdx.x, j1 - 1u);
+            eb[k] = a.in_off[jl];
+            ee[k] = a.in_off[jl + 1];
+        }
+        uint32_t n_lo = 0, n_hi = 0;
+        if (more) {
+            n_lo = a.in_off[tn * RE_TILE];
+            n_hi = a.in_off[min(nloc, tn * RE_TILE + RE_TILE)];
         }
         if (staged) {
-            uint32_t src[RE_FU], di[RE_FU], wrd[RE_FU], zb[RE_FU], X[RE_FU], Y[RE_FU];
-#pragma unroll
-            for (int m = 0; m < RE_FU; ++m) {
-                const uint32_t q = threadIdx.x + m * BULK_THREADS;
-                src[m] = q < cnt ? a.in_src[e_lo + q] : lo;
-            }
+            uint32_t di[RE_FU], wrd[RE_FU], zb[RE_FU], X[RE_FU], Y[RE_FU];
 #pragma unroll
             for (int m = 0; m < RE_FU; ++m) {
                 const uint32_t i = src[m];
@@ -545,10 +565,15 @@ __global__ __launch_bounds__(BULK_THREADS) void k_gossip_redges(WaveArgs a, uint
                     else if (uniform_from(X[m], Y[m], di[m]) == di[m] - 1u) w[m] = a.rbc[wrd[m]];
                 }
             }
+            // the next tile's senders, behind this tile's bitmap reads (issued on every
+            // path -- the last tile reloads its own -- so the wait below counts them)
+            redges_src(a, more ? n_lo : e_lo, more ? n_hi : e_hi, src);
 #pragma unroll
             for (int m = 0; m < RE_FU; ++m) sent[threadIdx.x + m * BULK_THREADS] = (uint8_t)((w[m] >> zb[m]) & 1ull);
+        } else {
+            redges_src(a, more ? n_lo : e_lo, more ? n_hi : e_hi, src);
         }
-        __syncthreads();
+        lds_barrier_only();
 #pragma unroll
         for (int k = 0; k < NPT; ++k) {
             const uint32_t jl = j0 + k * BULK_THREADS + threadIdx.x;
@@ -565,7 +590,11 @@ __global__ __launch_bounds__(BULK_THREADS) void k_gossip_redges(WaveArgs a, uint
             }
             a.rcnt[jl] = (uint16_t)n;
         }
-        __syncthreads();
+        if (!more) break;
+        lds_barrier_only();
+        t = tn;
+        e_lo = n_lo;
+        e_hi = n_hi;
     }
 }
 
