@@ -810,9 +810,10 @@ double alg_bytes(const gp_sim* s) {
         // that use the random edge -- a random gather, moved as a 128-B line)
         if (S.topo == IMP3D) return 38.5 + 16.0 / 7.0;
         if (S.topo != FULL) return 34.0;
-        // send: byte 1 + own (s, w) 16 + message write 20; split: message r+w 40; fold:
-        // message 20 + own (s, w) r+w 32 + byte r+w 2 (gp_fullbin.hip)
-        return 1.0 + 16.0 + 20.0 + 40.0 + 20.0 + 32.0 + 2.0;
+        // send: byte 1 (sweep 1) + byte 1 + own (s, w) 16 + message write 20; split: sender
+        // id 4 (sweep 1) + message r+w 40; fold: message 20 + own (s, w) r+w 32 + byte r+w 2
+        // (gp_fullbin.hip, range binning)
+        return 1.0 + 1.0 + 16.0 + 20.0 + 4.0 + 40.0 + 20.0 + 32.0 + 2.0;
     }
     // gossip: counter r+w 8, direction byte r+w 2 (+ Imp3D in-list 8, and with the
     // separate random-edge delivery pass of the column kernel its per-node count
