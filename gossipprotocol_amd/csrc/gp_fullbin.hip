@@ -40,7 +40,7 @@
 namespace gp {
 namespace {
 
-constexpr int FB_THREADS = 256;                    // C (GP_FB_V2=0)
+[[maybe_unused]] constexpr int FB_THREADS = 256;  // C (GP_FB_V2=0)
 constexpr int FB_MAXBINS = 4096;                   // LDS counters of A and B
 constexpr uint32_t FB_NONE = 0xFFFFu;
 #ifndef GP_FB_V2
@@ -219,6 +219,9 @@ __global__ __launch_bounds__(FBR_THREADS) void k_fb_send(FullBinArgs a, uint32_t
     uint32_t* const cnt = fbr_dyn;
     uint32_t* const base = fbr_dyn + a.nb1;
     for (uint32_t b = threadIdx.x; b < a.nb1; b += FBR_THREADS) base[b] = 0u;
+    // sweep 2's first chunk is loaded now, in flight through sweep 1 and the reservations
+    SendIn cur;
+    cur.load(a, i0, i1);
     __syncthreads();
     // sweep 1: coarse bin (target >> s1) of every active sender, counted; two
     // chunks per iteration (one Philox batch of 2 FBR_PER)
@@ -241,8 +244,6 @@ __global__ __launch_bounds__(FBR_THREADS) void k_fb_send(FullBinArgs a, uint32_t
     fbr_reserve(base, a.nb1, a.cnt1, 0, a.nb1);
     // sweep 2: {sender id | s/2, w/2} into the runs; the next chunk's input is
     // loaded while this one is put in order and written
-    SendIn cur;
-    cur.load(a, i0, i1);
     for (uint64_t c0 = i0; c0 < i1; c0 += FBR_CHUNK) {
         for (uint32_t b = threadIdx.x; b < a.nb1; b += FBR_THREADS) cnt[b] = 0u;
         uint32_t node[FBR_PER], x[FBR_PER], y[FBR_PER], key[FBR_PER], rank[FBR_PER];
@@ -296,6 +297,8 @@ __global__ __launch_bounds__(FBR_THREADS) void k_fb_split(FullBinArgs a, uint32_
     uint32_t* const cnt = fbr_dyn;
     uint32_t* const base = fbr_dyn + nfine;
     for (uint32_t f = threadIdx.x; f < nfine; f += FBR_THREADS) base[f] = 0u;
+    SplitIn cur;  // sweep 2's first chunk, in flight through sweep 1 and the reservations
+    cur.load(a, ibase, q0, q1);
     __syncthreads();
     // sweep 1: fine tile of every message (target recomputed from the sender's
     // draw), two chunks per iteration
@@ -315,8 +318,6 @@ __global__ __launch_bounds__(FBR_THREADS) void k_fb_split(FullBinArgs a, uint32_
     }
     fbr_reserve(base, nfine, a.cnt2, f0, a.nb2);
     // sweep 2: into the fine tiles' runs, the next chunk loaded meanwhile
-    SplitIn cur;
-    cur.load(a, ibase, q0, q1);
     for (uint32_t c0 = q0; c0 < q1; c0 += FBR_CHUNK) {
         for (uint32_t f = threadIdx.x; f < nfine; f += FBR_THREADS) cnt[f] = 0u;
         uint32_t node[FBR_PER], x[FBR_PER], y[FBR_PER], key[FBR_PER], rank[FBR_PER];

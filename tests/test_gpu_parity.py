@@ -92,6 +92,24 @@ def test_live_parity(n, topo, alg, seed, rounds, chk):
     sim.close()
 
 
+@pytest.mark.parametrize("n", [1, 2, 3, 1023, 1024, 4095, 4096, 16383, 16384, 65535, 65536, 131071])
+def test_full_pushsum_boundary_sizes(n):
+    """Full push-sum (range binning, gp_fullbin.hip) at populations P = n + 1 on and
+    around its chunk (4096), work-item (16384 senders) and fine-tile (1024) sizes:
+    bit-exact state every 25 rounds through convergence."""
+    sim, orc = Sim(n, "full", "push-sum", seed=n + 3), Oracle(n, "full", "push-sum", n + 3)
+    done = 0
+    while done < 400:
+        ga, oa = sim.step(25), orc.step(25)
+        assert ga == oa, f"alerts differ in rounds {done}..{done + 25}"
+        assert_same_state("push-sum", sim.state(), orc.state())
+        done += 25
+        if len(ga) < 25:
+            break
+    assert sim.rounds == orc.rounds and sim.alerts_total == orc.alerts_total
+    sim.close()
+
+
 def test_step_chunking_is_invisible():
     a = Sim(27000, "Imp3D", "push-sum", seed=12)
     b = Sim(27000, "Imp3D", "push-sum", seed=12)
