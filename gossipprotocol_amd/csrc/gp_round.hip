@@ -529,15 +529,28 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                     // the draw selects, instead of a random bitmap read per edge
                     uint32_t x[FU], y[FU];
                     philox2_batch<FU>(isrc, r, S_PUSHSUM, a.k0, a.k1, x, y);
+                    // picks first, then every pick's bitmap word in flight together: loads
+                    // unconditional (non-picks read the slab's first word, one shared line),
+                    // since under a branch each load was waited on at once
+                    bool pick[FU];
 #pragma unroll
                     for (int m = 0; m < FU; ++m) {
                         const uint32_t q = threadIdx.x + m * TPB;
                         const uint32_t i = isrc[m];
                         const uint32_t di = packed ? (raw[m] >> 30) + 4u : popc6(present_mask<IMP3D>(i, G)) + 1u;
-                        sent[m] = false;
-                        if (q < cnt && (!REMOTE || i - a.lo < a.nloc) && uniform_from(x[m], y[m], di) == di - 1u)
-                            sent[m] = (rbc[(i >> 6) - (a.lo >> 6)] >> (i & 63)) & 1ull;
+                        pick[m] = q < cnt && (!REMOTE || i - a.lo < a.nloc) && uniform_from(x[m], y[m], di) == di - 1u;
                     }
+                    unsigned long long wbits[FU];
+#pragma unroll
+                    for (int m = 0; m < FU; ++m) wbits[m] = rbc[pick[m] ? (isrc[m] >> 6) - (a.lo >> 6) : 0u];
+                    // (the asm consumes every loaded word, so no load can be sunk into a
+                    // branch on pick; its memory clobber keeps all loads ahead of the first)
+#pragma unroll
+                    for (int m = 0; m < FU; ++m) asm volatile("" : "+v"(wbits[m])::"memory");
+#pragma unroll
+                    for (int m = 0; m < FU; ++m) wbits[m] = pick[m] ? wbits[m] : 0ull;
+#pragma unroll
+                    for (int m = 0; m < FU; ++m) sent[m] = (wbits[m] >> (isrc[m] & 63)) & 1ull;
                 }
                 if (REMOTE) {  // sender on another rank: the exchange tagged its message
 #pragma unroll
