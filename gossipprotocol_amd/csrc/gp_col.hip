@@ -25,7 +25,13 @@
 #include "gp_wavecommon.hpp"
 
 #ifndef GP_COL_MINW
-#define GP_COL_MINW 7  // gossip column kernel: waves per SIMD (measured 5..8, profiles/r02/s5_colw.txt)
+// gossip column kernel: waves per SIMD (measured 5..7 with the batched step loads,
+// profiles/r02/col_batch/: Imp3D best at 5, 3D at 7)
+#define GP_COL_MINW(TOPO) ((TOPO) == IMP3D ? 5 : 7)
+#else
+#define GP_COL_MINW_FIXED GP_COL_MINW
+#undef GP_COL_MINW
+#define GP_COL_MINW(TOPO) GP_COL_MINW_FIXED
 #endif
 
 namespace gp {
@@ -383,7 +389,7 @@ __global__ __launch_bounds__(BULK_THREADS) void k_ps_col(WaveArgs a, uint32_t r)
 // Deliveries to j = lattice senders pointing here + Imp3D random-edge senders
 // + the injector; all dropped if j was converged at round start (Program.fs:87).
 template <int TOPO>
-__global__ __launch_bounds__(BULK_THREADS, GP_COL_MINW) void k_gossip_col(WaveArgs a, uint32_t r) {
+__global__ __launch_bounds__(BULK_THREADS, GP_COL_MINW(TOPO)) void k_gossip_col(WaveArgs a, uint32_t r) {
     Ctl* ctl = a.ctl;
     if (ld_agent(&ctl->done)) return;
     const long long inj = ld_agent(&ctl->inj_target);
@@ -412,38 +418,72 @@ __global__ __launch_bounds__(BULK_THREADS, GP_COL_MINW) void k_gossip_col(WaveAr
             yo[k] = rv[k] ? y * g + z : 0u;
             myz[k] = (y + 1 < g ? 4u : 0u) | (y > 0 ? 8u : 0u) | (z + 1 < g ? 16u : 0u) | (z > 0 ? 32u : 0u);
         }
+        // planes xa - 1, xa, xa + 1 of the patch (unconditional loads, pinned, then masked:
+        // see the x-step below)
         uint32_t pb = 0, cb = 0, nb = 0;
+        {
+            uint32_t lp[NR], lc[NR], ln[NR];
 #pragma unroll
-        for (int k = 0; k < NR; ++k) {
-            const uint32_t jl = xa * g2 + yo[k] - base;
-            cb |= (rv[k] ? (uint32_t)nbc[jl] : (uint32_t)DIR_NONE) << (8 * k);
-            pb |= ((rv[k] && xa > 0) ? (uint32_t)nbc[jl - g2] : (uint32_t)DIR_NONE) << (8 * k);
-            nb |= ((rv[k] && xa + 1 < g) ? (uint32_t)nbc[jl + g2] : (uint32_t)DIR_NONE) << (8 * k);
+            for (int k = 0; k < NR; ++k) {
+                const uint32_t jl = xa * g2 + yo[k] - base;
+                lc[k] = nbc[jl];
+                lp[k] = nbc[xa > 0 ? jl - g2 : jl];
+                ln[k] = nbc[xa + 1 < g ? jl + g2 : jl];
+            }
+#pragma unroll
+            for (int k = 0; k < NR; ++k) asm volatile("" : "+v"(lc[k]), "+v"(lp[k]), "+v"(ln[k]));
+#pragma unroll
+            for (int k = 0; k < NR; ++k) {
+                cb |= (rv[k] ? lc[k] : (uint32_t)DIR_NONE) << (8 * k);
+                pb |= ((rv[k] && xa > 0) ? lp[k] : (uint32_t)DIR_NONE) << (8 * k);
+                nb |= ((rv[k] && xa + 1 < g) ? ln[k] : (uint32_t)DIR_NONE) << (8 * k);
+            }
         }
         for (uint32_t x = xa; x < xb; ++x) {
             const uint32_t px = x * g2;
             const bool pf = x + 1 < xb && x + 2 < g;
-            uint32_t nnb = 0;
+            // Every load of the step is issued unconditionally (indices clamped to a
+            // valid node of this plane), pinned by an asm use only after all are in
+            // flight, and masked afterwards: as `cond ? load : NONE` the compiler
+            // turned each into a branch and waited for it there -- a dozen serialized
+            // round trips per step.
+            // z +- 1 senders: the neighbour lanes' bytes of plane x (cb, by DPP); only the
+            // wave's end lanes load theirs (lane 0: z - 1, lane 63: z + 1, one register).
+            const uint32_t pxb = px - base;
+            uint32_t lnn[NR], led[NR], lrc[NR];
             int32_t cv[NR];
+            const bool ledge = (lane == 0 && z > 0) || (lane == 63 && z + 1 < g);
 #pragma unroll
             for (int k = 0; k < NR; ++k) {
-                nnb |= ((pf && rv[k]) ? (uint32_t)nbc[px + 2 * g2 + yo[k] - base] : (uint32_t)DIR_NONE) << (8 * k);
-                cv[k] = rv[k] ? a.c[px + yo[k] - lo] : (int32_t)GOSSIP_DONE;
+                const uint32_t jl = pxb + yo[k];  // yo = 0 on invalid lanes: the plane's first node
+                lnn[k] = nbc[(pf ? 2u * g2 : 0u) + jl];
+                cv[k] = a.c[px + yo[k] - lo];
+                led[k] = nbc[(rv[k] && ledge) ? (lane == 0 ? jl - 1 : jl + 1) : jl];
+                lrc[k] = TOPO == IMP3D ? (uint32_t)a.rcnt[px + yo[k] - lo] : 0u;
             }
-            const uint32_t hym = (zv && y0 > 0) ? nbc[px + (y0 - 1) * g + z - base] : DIR_NONE;
-            const uint32_t hyp = (zv && y0 + NR < g) ? nbc[px + (y0 + NR) * g + z - base] : DIR_NONE;
-            uint32_t zbm = 0, zbp = 0;
+            const bool hmv = zv && y0 > 0, hpv = zv && y0 + NR < g;
+            uint32_t hym = nbc[hmv ? pxb + (y0 - 1) * g + z : pxb];
+            uint32_t hyp = nbc[hpv ? pxb + (y0 + NR) * g + z : pxb];
 #pragma unroll
-            for (int k = 0; k < NR; ++k) {
-                const uint32_t jl = px + yo[k] - base;
-                zbm |= ((rv[k] && z > 0) ? (uint32_t)nbc[jl - 1] : (uint32_t)DIR_NONE) << (8 * k);
-                zbp |= ((rv[k] && z + 1 < g) ? (uint32_t)nbc[jl + 1] : (uint32_t)DIR_NONE) << (8 * k);
-            }
-            // Imp3D: the random-edge deliveries of the patch rows, counted per
-            // receiver by k_gossip_redges before this kernel
+            for (int k = 0; k < NR; ++k) asm volatile("" : "+v"(lnn[k]), "+v"(cv[k]), "+v"(led[k]), "+v"(lrc[k]));
+            asm volatile("" : "+v"(hym), "+v"(hyp));
+            if (!hmv) hym = DIR_NONE;
+            if (!hpv) hyp = DIR_NONE;
+            // lane - 1's and lane + 1's bytes of plane x (wave_shr:1 / wave_shl:1)
+            const uint32_t cbl = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)cb, 0x138, 0xF, 0xF, false);
+            const uint32_t cbr = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)cb, 0x130, 0xF, 0xF, false);
+            uint32_t nnb = 0, zbm = 0, zbp = 0;
             uint32_t rcv[NR];
 #pragma unroll
-            for (int k = 0; k < NR; ++k) rcv[k] = (TOPO == IMP3D && rv[k]) ? (uint32_t)a.rcnt[px + yo[k] - lo] : 0u;
+            for (int k = 0; k < NR; ++k) {
+                nnb |= ((pf && rv[k]) ? lnn[k] : (uint32_t)DIR_NONE) << (8 * k);
+                if (!rv[k]) cv[k] = (int32_t)GOSSIP_DONE;
+                const uint32_t bm = lane == 0 ? led[k] : byte_of(cbl, k);
+                const uint32_t bp = lane == 63 ? led[k] : byte_of(cbr, k);
+                zbm |= ((rv[k] && z > 0) ? bm : (uint32_t)DIR_NONE) << (8 * k);
+                zbp |= ((rv[k] && z + 1 < g) ? bp : (uint32_t)DIR_NONE) << (8 * k);
+                rcv[k] = (TOPO == IMP3D && rv[k]) ? lrc[k] : 0u;
+            }
 #pragma unroll
             for (int k = 0; k < NR; ++k) {
                 const uint32_t j = px + yo[k];
