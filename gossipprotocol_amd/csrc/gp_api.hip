@@ -89,12 +89,6 @@ struct Slab {
     std::vector<size_t> soff, sbytes, roff, rbytes;
     unsigned int* overflow = nullptr;  // device flag
     // full topology over several ranks (gp_full.hip)
-    uint32_t *key0 = nullptr, *val0 = nullptr, *key1 = nullptr, *val1 = nullptr, *seg = nullptr;
-    uint32_t *ckey = nullptr, *cidx = nullptr, *ckey2 = nullptr, *cidx2 = nullptr, *head = nullptr;
-    double2* cval = nullptr;
-    uint32_t ccap = 0, bits1 = 32, bits2 = 32;
-    void *tmp1 = nullptr, *tmp2 = nullptr;
-    size_t tmp1_bytes = 0, tmp2_bytes = 0;
 };
 
 size_t xbuf_bytes(uint32_t cap, bool push) {
@@ -300,8 +294,8 @@ int alloc_slab(gp_sim* s, Slab& sl, int r) {
                 return rc;
         }
     }
-    if (S.topo == FULL && S.alg == PUSHSUM && W == 1) {  // LDS-binned message staging (gp_fullbin.hip)
-        const FullBinPlan fp = full_bin_plan(S.G.P);
+    if (S.topo == FULL && S.alg == PUSHSUM) {  // LDS-binned message staging of this rank's receivers (gp_fullbin.hip)
+        const FullBinPlan fp = full_bin_plan(S.nloc);
         S.fb_s1 = fp.s1;
         S.fb_nb1 = fp.nb1;
         S.fb_nb2 = fp.nb2;
@@ -458,8 +452,10 @@ int setup_exchange(gp_sim* s) {
             const int a = sl.rank;
             const double na = (double)(s->bounds[a + 1] - s->bounds[a]);
             for (int b = 0; b < W; ++b) {
-                if (b == a) continue;
-                const double nb = (double)(s->bounds[b + 1] - s->bounds[b]);
+                // push-sum: a rank's messages to itself also pass through a buffer (its
+                // own receive buffer, gp_fullbin.hip k_fbm_send)
+                if (b == a && !push) continue;
+                const double nb = (double)(s->bounds[b + 1] - s->bounds[b]) - (b == a ? 1.0 : 0.0);
                 const double m = na * nb / (double)(s->P - 1);
                 const double c = std::ceil(m + 12.0 * std::sqrt(m) + 64.0);
                 caps[(size_t)a * W + b] = (uint32_t)std::min(c, na);
@@ -523,7 +519,7 @@ int setup_exchange(gp_sim* s) {
             sl.cap_out[b] = caps[(size_t)a * W + b];
             sl.cap_in[b] = caps[(size_t)b * W + a];
             sl.soff[b] = so;
-            sl.sbytes[b] = xbuf_bytes(sl.cap_out[b], push);
+            sl.sbytes[b] = b == a ? 0 : xbuf_bytes(sl.cap_out[b], push);  // own messages: straight to xrecv
             so += sl.sbytes[b];
             sl.roff[b] = ro;
             sl.rbytes[b] = xbuf_bytes(sl.cap_in[b], push);
@@ -533,30 +529,6 @@ int setup_exchange(gp_sim* s) {
         HIP_TRY(hipMemsetAsync(sl.xsend, 0, so ? so : 16, s->stream));
         HIP_TRY(hipMemsetAsync(sl.xrecv, 0, ro ? ro : 16, s->stream));
         sl.overflow = &sl.S.ctl->overflow;
-        if (full && push) {  // message staging of the two sorts (gp_full.hip)
-            const uint32_t nl = sl.S.nloc;
-            uint64_t cc = nl;
-            for (int b = 0; b < W; ++b)
-                if (b != a) cc += sl.cap_in[b];
-            if (cc > 0xFFFFFF00ull) {
-                set_err("full topology: %llu staged messages per rank exceed the 32-bit range", (unsigned long long)cc);
-                return GP_EINVAL;
-            }
-            sl.ccap = (uint32_t)cc;
-            if ((rc = dev_alloc_t(s, &sl.key0, nl)) || (rc = dev_alloc_t(s, &sl.val0, nl)) ||
-                (rc = dev_alloc_t(s, &sl.key1, nl)) || (rc = dev_alloc_t(s, &sl.val1, nl)) ||
-                (rc = dev_alloc_t(s, &sl.seg, XMAXW + 1)) || (rc = dev_alloc_t(s, &sl.ckey, sl.ccap)) ||
-                (rc = dev_alloc_t(s, &sl.cidx, sl.ccap)) || (rc = dev_alloc_t(s, &sl.ckey2, sl.ccap)) ||
-                (rc = dev_alloc_t(s, &sl.cidx2, sl.ccap)) || (rc = dev_alloc_t(s, &sl.cval, sl.ccap)) ||
-                (rc = dev_alloc_t(s, &sl.head, nl)))
-                return rc;
-            sl.bits1 = bits_for((uint64_t)s->P);  // inactive senders stage key ~0: sorts last
-            sl.bits2 = bits_for((uint64_t)nl);    // padding key ~0 sorts after every receiver
-            HIP_TRY(sort_pairs(nullptr, sl.tmp1_bytes, sl.key0, sl.key1, sl.val0, sl.val1, nl, sl.bits1, s->stream));
-            HIP_TRY(sort_pairs(nullptr, sl.tmp2_bytes, sl.ckey, sl.ckey2, sl.cidx, sl.cidx2, sl.ccap, sl.bits2,
-                               s->stream));
-            if ((rc = dev_alloc(s, &sl.tmp1, sl.tmp1_bytes)) || (rc = dev_alloc(s, &sl.tmp2, sl.tmp2_bytes))) return rc;
-        }
     }
     return GP_OK;
 }
@@ -595,18 +567,6 @@ FullArgs make_full_args(gp_sim* s, Slab& sl, uint32_t round) {
     a.swn = push ? S.sw[cur ^ 1] + d : nullptr;
     a.c = S.c;
     a.inc = S.inc;
-    a.key0 = sl.key0;
-    a.val0 = sl.val0;
-    a.key1 = sl.key1;
-    a.val1 = sl.val1;
-    a.seg = sl.seg;
-    a.ckey = sl.ckey;
-    a.cidx = sl.cidx;
-    a.ckey2 = sl.ckey2;
-    a.cidx2 = sl.cidx2;
-    a.cval = sl.cval;
-    a.head = sl.head;
-    a.ccap = sl.ccap;
     a.ctl = S.ctl;
     a.overflow = sl.overflow;
     a.P = S.G.P;
@@ -625,20 +585,66 @@ FullArgs make_full_args(gp_sim* s, Slab& sl, uint32_t round) {
     return a;
 }
 
-// Full topology on several ranks: one round (gp_full.hip).
+// Push-sum on the full topology, one rank of several (gp_fullbin.hip): this
+// rank's receivers [lo, lo + nloc), node arrays indexed by id - lo, the exchange
+// buffers as the destination-rank bins of k_fbm_send and the sources of
+// k_fbm_coarse.
+FullBinArgs make_fullbin_args(gp_sim* s, Slab& sl, uint32_t round) {
+    DevState& S = sl.S;
+    const int cur = round & 1;
+    const uint32_t d = S.lo - S.base;
+    FullBinArgs a{};
+    a.swc = S.sw[cur] + d;
+    a.swn = S.sw[cur ^ 1] + d;
+    a.nb = S.nb[0] + d;
+    a.ctl = S.ctl;
+    a.overflow = sl.overflow;
+    a.P = S.G.P;
+    a.k0 = S.k0;
+    a.k1 = S.k1;
+    a.s1 = S.fb_s1;
+    a.nb1 = S.fb_nb1;
+    a.nb2 = S.fb_nb2;
+    a.cap1 = S.fb_cap1;
+    a.cap2 = S.fb_cap2;
+    a.cnt1 = S.fb_cnt1;
+    a.cnt2 = S.fb_cnt2;
+    a.hdr1 = S.fb_hdr1;
+    a.pay1 = S.fb_pay1;
+    a.hdr2 = S.fb_hdr2;
+    a.pay2 = S.fb_pay2;
+    a.lo = S.lo;
+    a.nloc = S.nloc;
+    a.W = s->world;
+    a.me = sl.rank;
+    for (int w = 0; w <= s->world; ++w) a.bounds[w] = s->bounds[w];
+    const uint32_t item = full_bin_item_messages();
+    a.in_item0[0] = 0;
+    for (int p = 0; p < s->world; ++p) {
+        a.in[p] = xpeer(sl.xrecv, sl.roff[p], sl.cap_in[p]);
+        a.out[p] = p == sl.rank ? a.in[p] : xpeer(sl.xsend, sl.soff[p], sl.cap_out[p]);
+        a.in_item0[p + 1] = a.in_item0[p] + (item ? (sl.cap_in[p] + item - 1) / item : 0u);
+    }
+    return a;
+}
+
+// Full topology on several ranks: one round (push-sum gp_fullbin.hip, gossip gp_full.hip).
 int launch_round_full_multi(gp_sim* s, uint32_t r, hipEvent_t e0, hipEvent_t e1) {
     const bool push = s->cfg.algorithm == GP_PUSHSUM;
     int rc;
     if (e0) HIP_TRY(hipEventRecord(e0, s->stream));
     for (Slab& sl : s->slab) {
-        FullArgs a = make_full_args(s, sl, r);
         if (push) {
-            HIP_TRY(launch_fullm_ps_send(a, r, s->grid, s->stream));
-            HIP_TRY(sort_pairs(sl.tmp1, sl.tmp1_bytes, sl.key0, sl.key1, sl.val0, sl.val1, sl.S.nloc, sl.bits1,
-                               s->stream));
-            HIP_TRY(launch_fullm_split(a, s->stream));
-            HIP_TRY(launch_fullm_ps_pack(a, std::max(1, s->grid / 8), s->stream));
-        } else {
+            const FullBinArgs a = make_fullbin_args(s, sl, r);
+            ZeroArgs z{};
+            for (int p = 0; p < s->world; ++p) z.cnt[p] = a.out[p].cnt;
+            z.n = s->world;
+            HIP_TRY(launch_zero_counts(z, s->stream));
+            HIP_TRY(launch_full_bin_send_multi(a, r, s->stream));
+            continue;
+        }
+        FullArgs a = make_full_args(s, sl, r);
+        {
             ZeroArgs z{};
             for (int p = 0; p < s->world; ++p) z.cnt[p] = a.peer[p].cnt;
             z.n = s->world;
@@ -648,15 +654,12 @@ int launch_round_full_multi(gp_sim* s, uint32_t r, hipEvent_t e0, hipEvent_t e1)
     }
     if ((rc = transfer_xbufs(s))) return rc;
     for (Slab& sl : s->slab) {
-        FullArgs a = make_full_args(s, sl, r);
         if (push) {
-            HIP_TRY(launch_fullm_ps_combine(a, s->grid, s->stream));
-            HIP_TRY(sort_pairs(sl.tmp2, sl.tmp2_bytes, sl.ckey, sl.ckey2, sl.cidx, sl.cidx2, sl.ccap, sl.bits2,
-                               s->stream));
-            HIP_TRY(hipMemsetAsync(sl.head, 0xFF, sizeof(uint32_t) * sl.S.nloc, s->stream));
-            HIP_TRY(launch_fullm_ps_mark(a, s->grid, s->stream));
-            HIP_TRY(launch_fullm_ps_recv(a, s->grid, s->stream));
-        } else {
+            HIP_TRY(launch_full_bin_recv_multi(make_fullbin_args(s, sl, r), r, s->grid, s->stream));
+            continue;
+        }
+        FullArgs a = make_full_args(s, sl, r);
+        {
             HIP_TRY(launch_fullm_gossip_unpack(a, std::max(1, s->grid / 8), s->stream));
             HIP_TRY(launch_fullm_gossip_recv(a, s->grid, s->stream));
         }

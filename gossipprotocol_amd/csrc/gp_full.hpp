@@ -1,4 +1,4 @@
-// gp_full.hpp -- argument block of the multi-rank full-topology kernels
+// gp_full.hpp -- argument block of the multi-rank full-topology gossip kernels
 // (gp_full.hip).  Not part of the C-ABI.
 #pragma once
 
@@ -13,13 +13,6 @@ struct FullArgs {
     double2* swn;           // (s, w) after the round
     int32_t* c;             // gossip rumour counters
     int32_t* inc;           // gossip deliveries of the round
-    // push-sum message staging
-    uint32_t *key0, *val0, *key1, *val1;  // (target, sender) unsorted / sorted by target
-    uint32_t* seg;                        // W + 1 segment starts of the sorted messages per destination rank
-    uint32_t *ckey, *cidx, *ckey2, *cidx2;  // received + local messages in source-rank order / sorted
-    double2* cval;
-    uint32_t* head;         // first sorted position per local receiver (~0: none)
-    uint32_t ccap;          // capacity of the combined message arrays
     Ctl* ctl;
     unsigned int* overflow;
     uint32_t P, lo, nloc, k0, k1, seed_node;
@@ -29,12 +22,6 @@ struct FullArgs {
     XPeer rpeer[XMAXW];     // receive buffers
 };
 
-hipError_t launch_fullm_ps_send(const FullArgs& a, uint32_t r, int grid, hipStream_t st);
-hipError_t launch_fullm_split(const FullArgs& a, hipStream_t st);
-hipError_t launch_fullm_ps_pack(const FullArgs& a, int grid, hipStream_t st);
-hipError_t launch_fullm_ps_combine(const FullArgs& a, int grid, hipStream_t st);
-hipError_t launch_fullm_ps_mark(const FullArgs& a, int grid, hipStream_t st);
-hipError_t launch_fullm_ps_recv(const FullArgs& a, int grid, hipStream_t st);
 hipError_t launch_fullm_gossip_send(const FullArgs& a, uint32_t r, int grid, hipStream_t st);
 hipError_t launch_fullm_gossip_unpack(const FullArgs& a, int grid, hipStream_t st);
 hipError_t launch_fullm_gossip_recv(const FullArgs& a, int grid, hipStream_t st);

@@ -144,13 +144,14 @@ struct FbRangeLds {
 extern __shared__ uint32_t fbr_dyn[];
 
 // Sweep 2's tail for one chunk whose keys / ranks are in registers: LDS bin
-// order, running slots, coalesced write-out.  LDS-only barriers, so the next
-// chunk's loads (issued before this call) stay in flight.
-__device__ __forceinline__ void fbr_emit(FbRangeLds& L, uint32_t* cnt, uint32_t* base, uint32_t nbins, const uint32_t (&key)[FBR_PER],
-                                         const uint32_t (&rank)[FBR_PER], const uint32_t (&hdr)[FBR_PER],
-                                         const double2 (&pay)[FBR_PER], uint32_t* __restrict__ ohdr,
-                                         double2* __restrict__ opay, uint32_t cap, uint32_t obin0, uint32_t nbins_out,
-                                         unsigned int* overflow) {
+// order, running slots, coalesced write-out through store(bin, slot, header,
+// payload).  LDS-only barriers, so the next chunk's loads (issued before this
+// call) stay in flight.
+template <class Store>
+__device__ __forceinline__ void fbr_emit_to(FbRangeLds& L, uint32_t* cnt, uint32_t* base, uint32_t nbins,
+                                            const uint32_t (&key)[FBR_PER], const uint32_t (&rank)[FBR_PER],
+                                            const uint32_t (&hdr)[FBR_PER], const double2 (&pay)[FBR_PER],
+                                            const Store& store) {
     const uint32_t total = lds_excl_scan<FBR_THREADS, true>(cnt, nbins, L.tmp);
 #pragma unroll
     for (int k = 0; k < FBR_PER; ++k) {
@@ -170,16 +171,27 @@ __device__ __forceinline__ void fbr_emit(FbRangeLds& L, uint32_t* cnt, uint32_t*
     for (int k = 0; k < FBR_PER; ++k) {
         const uint32_t p = k * FBR_THREADS + threadIdx.x;
         if (p >= total) break;
-        const uint32_t b = obin0 + L.key[p], pos = L.pos[p];
-        if (pos >= cap || b >= nbins_out) {
-            atomicOr(overflow, 1u);
-            continue;
-        }
-        const size_t o = (size_t)b * cap + pos;
-        ohdr[o] = L.hdr[p];
-        opay[o] = L.pay[p];
+        store(L.key[p], L.pos[p], L.hdr[p], L.pay[p]);
     }
     lds_barrier();
+}
+
+// the bins as [nbins_out * cap] arrays from bin obin0 on (coarse bins, fine tiles)
+__device__ __forceinline__ void fbr_emit(FbRangeLds& L, uint32_t* cnt, uint32_t* base, uint32_t nbins,
+                                         const uint32_t (&key)[FBR_PER], const uint32_t (&rank)[FBR_PER],
+                                         const uint32_t (&hdr)[FBR_PER], const double2 (&pay)[FBR_PER],
+                                         uint32_t* __restrict__ ohdr, double2* __restrict__ opay, uint32_t cap,
+                                         uint32_t obin0, uint32_t nbins_out, unsigned int* overflow) {
+    fbr_emit_to(L, cnt, base, nbins, key, rank, hdr, pay, [&](uint32_t k, uint32_t pos, uint32_t h, double2 v) {
+        const uint32_t b = obin0 + k;
+        if (pos >= cap || b >= nbins_out) {
+            atomicOr(overflow, 1u);
+            return;
+        }
+        const size_t o = (size_t)b * cap + pos;
+        ohdr[o] = h;
+        opay[o] = v;
+    });
 }
 
 // one global reservation per bin with messages in this range (base: count -> first slot)
@@ -313,8 +325,9 @@ __global__ __launch_bounds__(FBR_THREADS) void k_fb_split(FullBinArgs a, uint32_
 #pragma unroll
         for (int k = 0; k < P2; ++k)
             if (c0 + k * FBR_THREADS + threadIdx.x < q1)
-                atomicAdd(&base[(full_target(node[k], uniform_from(x[k], y[k], a.P - 1)) >> FB_TB) & (nfine - 1u)],
-                          1u);
+                atomicAdd(
+                    &base[((full_target(node[k], uniform_from(x[k], y[k], a.P - 1)) - a.lo) >> FB_TB) & (nfine - 1u)],
+                    1u);
     }
     fbr_reserve(base, nfine, a.cnt2, f0, a.nb2);
     // sweep 2: into the fine tiles' runs, the next chunk loaded meanwhile
@@ -334,13 +347,179 @@ __global__ __launch_bounds__(FBR_THREADS) void k_fb_split(FullBinArgs a, uint32_
             key[k] = FB_NONE;
             rank[k] = 0;
             if (c0 + k * FBR_THREADS + threadIdx.x < q1) {
-                key[k] = (full_target(node[k], uniform_from(x[k], y[k], a.P - 1)) >> FB_TB) & (nfine - 1u);
+                key[k] = ((full_target(node[k], uniform_from(x[k], y[k], a.P - 1)) - a.lo) >> FB_TB) & (nfine - 1u);
                 rank[k] = atomicAdd(&cnt[key[k]], 1u);
             }
         }
         cur.load(a, ibase, c0 + FBR_CHUNK < q1 ? c0 + FBR_CHUNK : c0, q1);
         lds_barrier();  // ranks counted
         fbr_emit(L, cnt, base, nfine, key, rank, node, pay, a.hdr2, a.pay2, a.cap2, f0, a.nb2, a.overflow);
+    }
+}
+
+// ---------------------------------------------------------------- several ranks
+// Contiguous id slabs (gp_api.hip make_bounds); W <= XMAXW.
+__device__ __forceinline__ uint32_t owner_of(const uint32_t* bounds, int W, uint32_t t) {
+    uint32_t b = 0;
+    for (int w = 1; w < W; ++w) b += t >= bounds[w] ? 1u : 0u;
+    return b;
+}
+
+// A on several ranks: this rank's senders binned by destination rank straight
+// into the exchange buffers (slots = sender id, vals = (s/2, w/2); one counter per
+// buffer, one reservation per (range, rank)); rank me's share goes to its own
+// receive buffer.  Receivers recompute targets from the sender's Philox draw.
+__global__ __launch_bounds__(FBR_THREADS) void k_fbm_send(FullBinArgs a, uint32_t r) {
+    __shared__ FbRangeLds L;
+    __shared__ uint32_t* o_slots[XMAXW];
+    __shared__ double2* o_vals[XMAXW];
+    __shared__ uint32_t o_cap[XMAXW];
+    __shared__ uint32_t bnd[XMAXW + 1];
+    if (ld_agent(&a.ctl->done)) return;
+    const uint32_t P = a.P;
+    const int W = a.W;
+    const uint64_t i0 = (uint64_t)blockIdx.x * FBR_ITEM;
+    if (i0 >= a.nloc || P < 2) return;
+    const uint64_t i1 = std::min<uint64_t>(a.nloc, i0 + FBR_ITEM);
+    uint32_t* const cnt = fbr_dyn;
+    uint32_t* const base = fbr_dyn + W;
+    if (threadIdx.x < (uint32_t)W) {
+        o_slots[threadIdx.x] = a.out[threadIdx.x].slots;
+        o_vals[threadIdx.x] = a.out[threadIdx.x].vals;
+        o_cap[threadIdx.x] = a.out[threadIdx.x].cap;
+        base[threadIdx.x] = 0u;
+    }
+    if (threadIdx.x <= (uint32_t)W) bnd[threadIdx.x] = a.bounds[threadIdx.x];
+    SendIn cur;
+    cur.load(a, i0, i1);
+    __syncthreads();
+    // sweep 1: destination rank of every active sender, counted
+    for (uint64_t c0 = i0; c0 < i1; c0 += FBR_CHUNK) {
+        uint32_t node[FBR_PER], x[FBR_PER], y[FBR_PER];
+        uint8_t nbv[FBR_PER];
+#pragma unroll
+        for (int k = 0; k < FBR_PER; ++k) {
+            const uint64_t g = c0 + k * FBR_THREADS + threadIdx.x;
+            node[k] = a.lo + (uint32_t)g;
+            nbv[k] = a.nb[std::min<uint64_t>(g, i1 - 1)];
+        }
+        philox2_batch<FBR_PER>(node, r, S_PUSHSUM, a.k0, a.k1, x, y);
+#pragma unroll
+        for (int k = 0; k < FBR_PER; ++k)
+            if ((nbv[k] & B_ACTIVE) && c0 + k * FBR_THREADS + threadIdx.x < i1)  // Program.fs:213-215
+                atomicAdd(&base[owner_of(bnd, W, full_target(node[k], uniform_from(x[k], y[k], P - 1)))], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < (uint32_t)W) {
+        const uint32_t n = base[threadIdx.x];
+        uint32_t* c = a.out[threadIdx.x].cnt;  // null: no buffer (capacity 0)
+        base[threadIdx.x] = n && c ? atomicAdd(c, n) : 0u;
+        if (n && !c) atomicOr(a.overflow, 1u);
+    }
+    // sweep 2: into the buffers' runs
+    for (uint64_t c0 = i0; c0 < i1; c0 += FBR_CHUNK) {
+        if (threadIdx.x < (uint32_t)W) cnt[threadIdx.x] = 0u;
+        uint32_t node[FBR_PER], x[FBR_PER], y[FBR_PER], key[FBR_PER], rank[FBR_PER];
+        double2 pay[FBR_PER];
+#pragma unroll
+        for (int k = 0; k < FBR_PER; ++k) node[k] = a.lo + (uint32_t)(c0 + k * FBR_THREADS + threadIdx.x);
+        philox2_batch<FBR_PER>(node, r, S_PUSHSUM, a.k0, a.k1, x, y);
+        lds_barrier();  // counters zeroed
+#pragma unroll
+        for (int k = 0; k < FBR_PER; ++k) {
+            key[k] = FB_NONE;
+            rank[k] = 0;
+            if ((cur.nbv[k] & B_ACTIVE) && c0 + k * FBR_THREADS + threadIdx.x < i1) {
+                key[k] = owner_of(bnd, W, full_target(node[k], uniform_from(x[k], y[k], P - 1)));
+                rank[k] = atomicAdd(&cnt[key[k]], 1u);
+            }
+            pay[k] = make_double2(cur.sv[k].x * 0.5, cur.sv[k].y * 0.5);
+        }
+        cur.load(a, c0 + FBR_CHUNK < i1 ? c0 + FBR_CHUNK : c0, i1);
+        lds_barrier();  // ranks counted
+        fbr_emit_to(L, cnt, base, (uint32_t)W, key, rank, node, pay,
+                    [&](uint32_t b, uint32_t pos, uint32_t h, double2 v) {
+                        if (pos >= o_cap[b]) {
+                            atomicOr(a.overflow, 1u);
+                            return;
+                        }
+                        o_slots[b][pos] = h;
+                        o_vals[b][pos] = v;
+                    });
+    }
+}
+
+// A' on several ranks: every received message (this rank's own buffer included)
+// binned by coarse bin of its receiver ((t - lo) >> s1, the target recomputed
+// from the sender's draw) into hdr1 / pay1; then k_fb_split and k_fb_fold as on
+// one rank.  Work items: ranges of each source's buffer (in_item0).
+struct CoarseIn {
+    uint32_t node[FBR_PER];
+    double2 pv[FBR_PER];
+    __device__ __forceinline__ void load(const uint32_t* slots, const double2* vals, uint32_t c0, uint32_t q1) {
+#pragma unroll
+        for (int k = 0; k < FBR_PER; ++k) {
+            const uint32_t q = min(c0 + k * FBR_THREADS + threadIdx.x, q1 - 1);
+            node[k] = slots[q];
+            pv[k] = vals[q];
+        }
+    }
+};
+
+__global__ __launch_bounds__(FBR_THREADS) void k_fbm_coarse(FullBinArgs a, uint32_t r) {
+    __shared__ FbRangeLds L;
+    if (ld_agent(&a.ctl->done)) return;
+    int p = 0;
+    while (p + 1 < a.W && blockIdx.x >= a.in_item0[p + 1]) ++p;  // block-uniform
+    p = __builtin_amdgcn_readfirstlane(p);
+    const uint32_t* __restrict__ slots = a.in[p].slots;
+    const double2* __restrict__ vals = a.in[p].vals;
+    const uint32_t cap = a.in[p].cap;
+    if (!cap) return;
+    const uint32_t n_in = min(ld_agent(a.in[p].cnt), cap);
+    const uint32_t q0 = (blockIdx.x - a.in_item0[p]) * FBR_ITEM;
+    if (q0 >= n_in) return;
+    const uint32_t q1 = min(n_in, q0 + FBR_ITEM);
+    uint32_t* const cnt = fbr_dyn;
+    uint32_t* const base = fbr_dyn + a.nb1;
+    for (uint32_t b = threadIdx.x; b < a.nb1; b += FBR_THREADS) base[b] = 0u;
+    CoarseIn cur;
+    cur.load(slots, vals, q0, q1);
+    __syncthreads();
+    for (uint32_t c0 = q0; c0 < q1; c0 += FBR_CHUNK) {
+        uint32_t node[FBR_PER], x[FBR_PER], y[FBR_PER];
+#pragma unroll
+        for (int k = 0; k < FBR_PER; ++k) node[k] = slots[min(c0 + k * FBR_THREADS + threadIdx.x, q1 - 1)];
+        philox2_batch<FBR_PER>(node, r, S_PUSHSUM, a.k0, a.k1, x, y);
+#pragma unroll
+        for (int k = 0; k < FBR_PER; ++k)
+            if (c0 + k * FBR_THREADS + threadIdx.x < q1)
+                atomicAdd(&base[(full_target(node[k], uniform_from(x[k], y[k], a.P - 1)) - a.lo) >> a.s1], 1u);
+    }
+    fbr_reserve(base, a.nb1, a.cnt1, 0, a.nb1);
+    for (uint32_t c0 = q0; c0 < q1; c0 += FBR_CHUNK) {
+        for (uint32_t b = threadIdx.x; b < a.nb1; b += FBR_THREADS) cnt[b] = 0u;
+        uint32_t node[FBR_PER], x[FBR_PER], y[FBR_PER], key[FBR_PER], rank[FBR_PER];
+        double2 pay[FBR_PER];
+#pragma unroll
+        for (int k = 0; k < FBR_PER; ++k) {
+            node[k] = cur.node[k];
+            pay[k] = cur.pv[k];
+        }
+        philox2_batch<FBR_PER>(node, r, S_PUSHSUM, a.k0, a.k1, x, y);
+        lds_barrier();  // counters zeroed
+#pragma unroll
+        for (int k = 0; k < FBR_PER; ++k) {
+            key[k] = FB_NONE;
+            rank[k] = 0;
+            if (c0 + k * FBR_THREADS + threadIdx.x < q1) {
+                key[k] = (full_target(node[k], uniform_from(x[k], y[k], a.P - 1)) - a.lo) >> a.s1;
+                rank[k] = atomicAdd(&cnt[key[k]], 1u);
+            }
+        }
+        cur.load(slots, vals, c0 + FBR_CHUNK < q1 ? c0 + FBR_CHUNK : c0, q1);
+        lds_barrier();  // ranks counted
+        fbr_emit(L, cnt, base, a.nb1, key, rank, node, pay, a.hdr1, a.pay1, a.cap1, 0, a.nb1, a.overflow);
     }
 }
 #else
@@ -558,7 +737,7 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
         }
 #pragma unroll
         for (int k = 0; k < NPT; ++k) {
-            const uint32_t j = min(f * TILE + k * FBF_THREADS + threadIdx.x, P - 1);
+            const uint32_t j = min(f * TILE + k * FBF_THREADS + threadIdx.x, a.nloc - 1);
             bk[k] = nbp[j];
             svk[k] = swc[j];
         }
@@ -566,7 +745,7 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
 #pragma unroll
         for (int k = 0; k < FQ; ++k) {
             const uint32_t q = k * FBF_THREADS + threadIdx.x;
-            vr[k] = full_target(snd[k], uniform_from(x[k], y[k], P - 1)) & (TILE - 1);
+            vr[k] = (full_target(snd[k], uniform_from(x[k], y[k], P - 1)) - a.lo) & (TILE - 1);
             rk[k] = q < n ? atomicAdd(&cnt[vr[k]], 1u) : 0u;
         }
         __syncthreads();
@@ -586,7 +765,7 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
         for (int k = 0; k < NPT; ++k) {
             const uint32_t v = k * FBF_THREADS + threadIdx.x;
             const uint32_t j = f * TILE + v;
-            const uint32_t p0 = cnt[v], p1 = j < P ? cnt[v + 1] : p0;
+            const uint32_t p0 = cnt[v], p1 = j < a.nloc ? cnt[v + 1] : p0;
             // this receiver's messages in ascending sender id (canonical order)
             for (uint32_t p = p0 + 1; p < p1; ++p) {
                 const uint32_t s = src[p];
@@ -629,7 +808,7 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
                 }
                 nbp[j] = (uint8_t)flags;
             }
-            if (j < P) swn[j] = make_double2(acc_s, acc_w);
+            if (j < a.nloc) swn[j] = make_double2(acc_s, acc_w);
         }
         __syncthreads();
         for (uint32_t v = threadIdx.x; v < TILE; v += FBF_THREADS) cnt[v] = 0u;
@@ -801,6 +980,7 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_fold(FullBinArgs a, uint32_t 
 #endif  // GP_FB_V2
 
 // ---------------------------------------------------------------- host side
+// Bins for the nrecv receivers of a rank (one rank: nrecv = P).
 FullBinPlan full_bin_plan(uint32_t P) {
     FullBinPlan p{};
     uint32_t bits = 1;
@@ -819,6 +999,40 @@ FullBinPlan full_bin_plan(uint32_t P) {
     p.cap2 = FB_CAP2;
     return p;
 }
+
+uint32_t full_bin_item_messages() {
+#if GP_FB_V2
+    return FBR_ITEM;
+#else
+    return 0;
+#endif
+}
+
+#if GP_FB_V2
+hipError_t launch_full_bin_send_multi(const FullBinArgs& a, uint32_t round, hipStream_t st) {
+    const uint32_t items = (uint32_t)(((uint64_t)a.nloc + FBR_ITEM - 1) / FBR_ITEM);
+    if (items) hipLaunchKernelGGL(k_fbm_send, dim3(items), dim3(FBR_THREADS), 2 * sizeof(uint32_t) * a.W, st, a, round);
+    return hipGetLastError();
+}
+
+hipError_t launch_full_bin_recv_multi(const FullBinArgs& a, uint32_t round, int grid, hipStream_t st) {
+    hipError_t e;
+    if ((e = hipMemsetAsync(a.cnt1, 0, sizeof(uint32_t) * a.nb1, st)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(a.cnt2, 0, sizeof(uint32_t) * a.nb2, st)) != hipSuccess) return e;
+    if (a.in_item0[a.W])
+        hipLaunchKernelGGL(k_fbm_coarse, dim3(a.in_item0[a.W]), dim3(FBR_THREADS), 2 * sizeof(uint32_t) * a.nb1, st, a,
+                           round);
+    const uint32_t items_b = a.nb1 * ((a.cap1 + FBR_ITEM - 1) / FBR_ITEM);
+    hipLaunchKernelGGL(k_fb_split, dim3(items_b), dim3(FBR_THREADS), 2 * sizeof(uint32_t) * (1u << (a.s1 - FB_TB)), st,
+                       a, round);
+    hipLaunchKernelGGL(k_fb_fold, dim3(std::min<uint32_t>(a.nb2, (uint32_t)grid * 256 / FBF_THREADS)),
+                       dim3(FBF_THREADS), 0, st, a, round);
+    return hipGetLastError();
+}
+#else
+hipError_t launch_full_bin_send_multi(const FullBinArgs&, uint32_t, hipStream_t) { return hipErrorInvalidValue; }
+hipError_t launch_full_bin_recv_multi(const FullBinArgs&, uint32_t, int, hipStream_t) { return hipErrorInvalidValue; }
+#endif
 
 hipError_t launch_full_bin_round(const FullBinArgs& a, uint32_t round, int grid, hipStream_t st) {
     hipError_t e;

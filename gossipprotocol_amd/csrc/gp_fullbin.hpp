@@ -2,7 +2,7 @@
 // binning (gp_fullbin.hip).  Not part of the C-ABI.
 #pragma once
 
-#include "gp_internal.hpp"
+#include "gp_xchg.hpp"
 
 namespace gp {
 
@@ -35,9 +35,25 @@ struct FullBinArgs {
     double2* pay1;       // [nb1 * cap1] {s / 2, w / 2}
     uint32_t* hdr2;      // [nb2 * cap2] sender id
     double2* pay2;
+    // receivers of this rank: global ids [lo, lo + nloc) (one rank: 0, P); node
+    // arrays (swc, swn, nb) are indexed by id - lo, coarse bins and fine tiles count
+    // from lo
+    uint32_t lo, nloc;
+    // several ranks (k_fbm_send / k_fbm_coarse): senders' messages binned by
+    // destination rank into the exchange buffers, then the received ones by coarse bin
+    int W, me;
+    uint32_t bounds[XMAXW + 1];
+    XPeer out[XMAXW];       // this rank's messages to rank b (b == me: its own receive buffer)
+    XPeer in[XMAXW];        // messages from rank b (after the exchange)
+    uint32_t in_item0[XMAXW + 1];  // first k_fbm_coarse work item of each source rank
 };
 
-FullBinPlan full_bin_plan(uint32_t P);
+FullBinPlan full_bin_plan(uint32_t nrecv);
 hipError_t launch_full_bin_round(const FullBinArgs& a, uint32_t round, int grid, hipStream_t st);
+// several ranks: messages into the exchange buffers (before the exchange) ...
+hipError_t launch_full_bin_send_multi(const FullBinArgs& a, uint32_t round, hipStream_t st);
+// ... and the received messages binned, split and folded (after it)
+hipError_t launch_full_bin_recv_multi(const FullBinArgs& a, uint32_t round, int grid, hipStream_t st);
+uint32_t full_bin_item_messages();
 
 }  // namespace gp

@@ -460,6 +460,9 @@ hipError_t launch_full_pushsum_round(const DevState& S, uint32_t round, int grid
     a.pay1 = S.fb_pay1;
     a.hdr2 = S.fb_hdr2;
     a.pay2 = S.fb_pay2;
+    a.lo = S.lo;      // one rank: 0
+    a.nloc = S.nloc;  // one rank: P
+    a.W = 1;
     return launch_full_bin_round(a, round, grid, st);
 }
 }  // namespace gp

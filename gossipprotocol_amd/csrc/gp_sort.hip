@@ -1,8 +1,9 @@
-// gp_sort.hip -- rocPRIM device primitives used off the steady-state path:
+// gp_sort.hip -- rocPRIM device primitives used once, at create (never per round):
 //   * Imp3D setup: stable sort of the random edges (rnd[i] -> i) by target, so
 //     each receiver's in-list holds its senders in ascending id order (the
-//     canonical fold order of SRS v1 B.4);
-//   * full-topology push-sum: the per-round stable sort of (target, sender).
+//     canonical fold order of SRS v1 B.4), and the scan of the in-degrees into
+//     the in-list offsets.  Per-round message binning is hand-written
+//     (gp_fullbin.hip).
 // Kept in its own translation unit because rocPRIM's templates dominate the
 // library's compile time.
 #include <rocprim/device/device_radix_sort.hpp>
