@@ -647,6 +647,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                     pf_lo = a.in_off[max(a.lo, nT)];
                     pf_hi = a.in_off[min(a.lo + a.nloc, nT + TILE)];
                     pf_tile = nti;
+                    pf_next = GP_PF_SRC && pf_hi - pf_lo <= cap;  // senders loaded after the directions
                 }
             }
         }
