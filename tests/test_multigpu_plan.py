@@ -93,25 +93,46 @@ def test_c5_imp3d_pushsum_1e9_world8_plan():
     assert 1e5 * W * (W - 1) * GAUSS_12SIGMA_TAIL < 1e-25
 
 
+def full_bin_plan(nrecv):
+    """gp_fullbin.hip full_bin_plan: coarse bins of 2^s1 receivers, fine tiles of 1024."""
+    fb_tb, cap2 = 10, 1536
+    bits = 1
+    while bits < 32 and (1 << bits) < nrecv:
+        bits += 1
+    s1 = max((bits + fb_tb + 1) // 2, fb_tb)
+    while (nrecv >> s1) >= 4096:
+        s1 += 1
+    while s1 - fb_tb > 12:
+        s1 -= 1
+    nb1 = (nrecv + (1 << s1) - 1) >> s1
+    nb2 = (nrecv + (1 << fb_tb) - 1) >> fb_tb
+    m1 = (1 << s1) * (nrecv / max(nrecv - 1, 1))
+    return nb1, int(m1 + 12.0 * math.sqrt(m1) + 1024.0), nb2, cap2
+
+
 def test_c4_full_pushsum_1e8_world8_plan():
+    """Several ranks (gp_fullbin.hip k_fbm_send / k_fbm_coarse): every rank's messages to
+    rank b -- itself included -- go through a fixed-capacity buffer, then the receiver bins
+    them by coarse bin and fine tile of its own receivers."""
     P, T, _ = resolve(10**8, "full")
     W = 8
     bounds, halo = slab_bounds(P, 0, "full", W)
     assert halo == 0 and bounds[-1] == P
     for a in range(W):
         na = bounds[a + 1] - bounds[a]
-        caps_in = [full_capacity(bounds[b + 1] - bounds[b], na, P) for b in range(W) if b != a]
+        caps_in = []
         for b in range(W):
-            if b == a:
-                continue
-            nb = bounds[b + 1] - bounds[b]
+            nb = bounds[b + 1] - bounds[b] - (1 if b == a else 0)  # no message to oneself
             m = na * nb / (P - 1)
             sd = math.sqrt(m * (1 - nb / (P - 1)))
             assert (full_capacity(na, nb, P) - m) / sd >= 12.0
-        ccap = na + sum(caps_in)  # staged messages of the receive-side sort (gp_api.hip setup_exchange)
-        assert ccap < 0xFFFFFF00
-        # node arrays + send sort (key/val x2) + receive staging (ckey/cidx x2, cval) + buffers + sort scratch
-        steady = na * (2 * 16 + 1 + 4 * 4 + 4) + ccap * (4 * 4 + 16) + 2 * sum(20 * c for c in caps_in) + 2e9
+            nsrc = bounds[b + 1] - bounds[b]
+            caps_in.append(full_capacity(nsrc, na - (1 if b == a else 0), P))
+        nb1, cap1, nb2, cap2 = full_bin_plan(na)
+        assert nb1 < 4096 and nb2 * cap2 < 2**32
+        # a coarse bin receives Binomial(sum of senders, 2^s1 / (P - 1)) messages: 12 sigma + 1024
+        # node arrays (s, w) x2 + byte + buffers out (W - 1) and in (W) + coarse and fine bins
+        steady = na * (2 * 16 + 1 + 4) + 20 * (sum(caps_in) * 2) + 20 * (nb1 * cap1 + nb2 * cap2)
         assert steady < 0.5 * HBM_BYTES
 
 
