@@ -17,13 +17,13 @@ ranks only through the library's exchange plan:
   * bookkeeping: {alerts, newly active, injector pick converged} summed over
     ranks (k_finalize_pre / all-reduce / k_finalize_post); the gossip
     injector's live list is replicated on every rank;
-  * full topology (gp_full.hip): contiguous id slabs, no halo; every round each
-    rank stably sorts its senders' messages by target, cuts them into one
-    segment per destination rank (fixed per-pair capacity: expected + 12 sigma
-    + 64, an overflow fails), the destination concatenates the segments in
-    ascending source rank and sorts stably by target again -- every receiver's
-    messages then come by ascending sender id (push-sum); gossip deliveries
-    are counts added by the owner.
+  * full topology: contiguous id slabs, no halo.  Push-sum (gp_fullbin.hip
+    k_fbm_send / k_fbm_coarse): every rank bins its messages {sender id, s/2,
+    w/2} by destination rank -- its own share included -- into fixed-capacity
+    buffers (expected + 12 sigma + 64, an overflow fails) in no particular
+    order (shuffled here); the receiver recomputes every target from the
+    sender's Philox draw and folds each receiver's messages by ascending sender
+    id.  Gossip (gp_full.hip): deliveries are counts added by the owner.
 
 It never calls the HIP library: it checks the decomposition itself (slab
 plan, slot arithmetic, fold order with remote messages, replicated injector)
@@ -372,9 +372,9 @@ class RankSim:
 
     # ---------------------------------------------------------------- full topology
     def _full_exchange(self, targets, payload):
-        """Messages (targets ascending-sender order) -> this rank's receivers: the
-        per-destination segments of a stable sort by target, capacity-checked,
-        concatenated by ascending source rank and stably sorted by target again."""
+        """Gossip deliveries (targets) -> this rank's receivers: per-destination
+        segments, capacity-checked, concatenated by source rank (counts are
+        order-independent)."""
         order = np.argsort(targets, kind="stable")
         t = targets[order]
         pl = [p[order] for p in payload]
@@ -397,6 +397,32 @@ class RankSim:
         o2 = np.argsort(tt, kind="stable")
         return tt[o2], [c[o2] for c in cols]
 
+    def _full_pushsum_exchange(self, snd, t, payload):
+        """Push-sum messages -> this rank's receivers (gp_fullbin.hip several ranks):
+        binned by destination rank in arbitrary order, capacity-checked (own share
+        included), targets recomputed by the receiver, each receiver's messages put
+        in ascending sender order.  Returns local receiver ids and payload columns."""
+        owner = np.searchsorted(np.array(self.bounds), t, side="right") - 1
+        rng = np.random.default_rng(self.round * 7919 + self.rank)  # buffer order is arbitrary
+        packets = {}
+        for b in range(self.W):
+            sel = np.nonzero(owner == b)[0]
+            nb = self.bounds[b + 1] - self.bounds[b] - (1 if b == self.rank else 0)
+            assert len(sel) <= full_capacity(self.hi - self.lo, nb, self.P), "exchange capacity exceeded"
+            sel = rng.permutation(sel)
+            packets[b] = (snd[sel],) + tuple(p[sel] for p in payload)
+        got = [None] * self.W
+        if self.W > 1:
+            self.dist.all_gather_object(got, packets)
+        else:
+            got = [packets]
+        parts = [got[src][self.rank] for src in range(self.W)]
+        src = np.concatenate([p[0] for p in parts]).astype(np.int64)
+        cols = [np.concatenate([p[1 + q] for p in parts]) for q in range(len(payload))]
+        tt = full_target(src, uniform(self.seed, S_PUSHSUM, src, self.round, self.P - 1)) - self.lo
+        o = np.lexsort((src, tt))  # by receiver, then ascending sender: the canonical fold order
+        return tt[o], [c[o] for c in cols] + [src[o]]
+
     def _full_pushsum_round(self):
         r = self.round
         j = self.ids
@@ -405,7 +431,7 @@ class RankSim:
         snd = j[act] if self.P > 1 else j[:0]
         t = full_target(snd, uniform(self.seed, S_PUSHSUM, snd, r, self.P - 1))
         li = self._local(snd)
-        tt, (ms, mw, src) = self._full_exchange(t, [self.s[li] * 0.5, self.w[li] * 0.5, snd])
+        tt, (ms, mw, src) = self._full_pushsum_exchange(snd, t, [self.s[li] * 0.5, self.w[li] * 0.5])
         halve = act & (self.P > 1)
         acc_s = np.where(halve, self.s[lj] * 0.5, self.s[lj])
         acc_w = np.where(halve, self.w[lj] * 0.5, self.w[lj])
