@@ -124,7 +124,13 @@ __device__ uint32_t lds_excl_scan(uint32_t* cnt, uint32_t n, uint32_t* tmp) {
 #define GP_FBR_THREADS 1024
 #endif
 constexpr int FBR_THREADS = GP_FBR_THREADS;
-constexpr int FBR_PER = 4;
+#ifndef GP_FBR_PER
+#define GP_FBR_PER 4
+#endif
+#ifndef GP_FBR_MINB
+#define GP_FBR_MINB 1  // __launch_bounds__ minimum waves per SIMD (8: two 1024-thread blocks per CU)
+#endif
+constexpr int FBR_PER = GP_FBR_PER;
 constexpr int FBR_CHUNK = FBR_THREADS * FBR_PER;
 #ifndef GP_FB_RANGE
 #define GP_FB_RANGE 4
@@ -221,7 +227,7 @@ struct SendIn {
     }
 };
 
-__global__ __launch_bounds__(FBR_THREADS) void k_fb_send(FullBinArgs a, uint32_t r) {
+__global__ __launch_bounds__(FBR_THREADS, GP_FBR_MINB) void k_fb_send(FullBinArgs a, uint32_t r) {
     __shared__ FbRangeLds L;
     if (ld_agent(&a.ctl->done)) return;
     const uint32_t P = a.P;
@@ -295,7 +301,7 @@ struct SplitIn {
     }
 };
 
-__global__ __launch_bounds__(FBR_THREADS) void k_fb_split(FullBinArgs a, uint32_t r) {
+__global__ __launch_bounds__(FBR_THREADS, GP_FBR_MINB) void k_fb_split(FullBinArgs a, uint32_t r) {
     __shared__ FbRangeLds L;
     if (ld_agent(&a.ctl->done)) return;
     const uint32_t per_bin = (a.cap1 + FBR_ITEM - 1) / FBR_ITEM;
@@ -369,7 +375,7 @@ __device__ __forceinline__ uint32_t owner_of(const uint32_t* bounds, int W, uint
 // into the exchange buffers (slots = sender id, vals = (s/2, w/2); one counter per
 // buffer, one reservation per (range, rank)); rank me's share goes to its own
 // receive buffer.  Receivers recompute targets from the sender's Philox draw.
-__global__ __launch_bounds__(FBR_THREADS) void k_fbm_send(FullBinArgs a, uint32_t r) {
+__global__ __launch_bounds__(FBR_THREADS, GP_FBR_MINB) void k_fbm_send(FullBinArgs a, uint32_t r) {
     __shared__ FbRangeLds L;
     __shared__ uint32_t* o_slots[XMAXW];
     __shared__ double2* o_vals[XMAXW];
@@ -466,7 +472,7 @@ struct CoarseIn {
     }
 };
 
-__global__ __launch_bounds__(FBR_THREADS) void k_fbm_coarse(FullBinArgs a, uint32_t r) {
+__global__ __launch_bounds__(FBR_THREADS, GP_FBR_MINB) void k_fbm_coarse(FullBinArgs a, uint32_t r) {
     __shared__ FbRangeLds L;
     if (ld_agent(&a.ctl->done)) return;
     int p = 0;
