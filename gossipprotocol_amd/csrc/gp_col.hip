@@ -550,7 +550,10 @@ __device__ __forceinline__ void redges_src(const WaveArgs& a, uint32_t e_lo, uin
 
 __device__ __forceinline__ void lds_barrier_only() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-__global__ __launch_bounds__(BULK_THREADS) void k_gossip_redges(WaveArgs a, uint32_t r) {
+#ifndef GP_RE_MINW
+#define GP_RE_MINW 5  // delivery pass: waves per SIMD (5: 96 VGPRs, no spills; 4 measured slower, profiles/r02/c3_redges/minw.txt)
+#endif
+__global__ __launch_bounds__(BULK_THREADS, GP_RE_MINW) void k_gossip_redges(WaveArgs a, uint32_t r) {
     __shared__ uint8_t sent[BULK_THREADS * RE_FU];
     if (ld_agent(&a.ctl->done)) return;
     const uint32_t lo = a.lo, nloc = a.nloc;
