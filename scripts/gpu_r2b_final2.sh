@@ -3,7 +3,7 @@
 # bench (HBM-traffic passes inside) + its rocprofv3 kernel trace, kernel traces of the
 # other BASELINE configurations, and the C5 workload run to convergence.
 export TMPDIR=/tmp
-O=gpurun_out/final2
+O=${O:-gpurun_out/final2}
 mkdir -p $O
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
 timeout -k 10 1500 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
