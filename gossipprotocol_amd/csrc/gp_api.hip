@@ -307,9 +307,16 @@ int alloc_slab(gp_sim* s, Slab& sl, int r) {
             (rc = dev_alloc_t(s, &S.fb_hdr2, m2)) || (rc = dev_alloc_t(s, &S.fb_pay2, m2)))
             return rc;
     }
-    if (S.topo == IMP3D && S.alg == GOSSIP && S.kernel == KERNEL_COL &&
-        (rc = dev_alloc_t(s, &S.rcnt, (size_t)S.nloc + 64)))
-        return rc;
+    if (S.topo == IMP3D && S.alg == GOSSIP && S.kernel == KERNEL_COL) {
+        if (W == 1) {  // senders count their random-edge deliveries (k_gossip_col, push form)
+            for (int q = 0; q < 2; ++q) {
+                if ((rc = dev_alloc_t(s, &S.rq[q], (size_t)S.nloc + 64))) return rc;
+                HIP_TRY(hipMemsetAsync(S.rq[q], 0, sizeof(uint32_t) * ((size_t)S.nloc + 64), s->stream));
+            }
+        } else if ((rc = dev_alloc_t(s, &S.rcnt, (size_t)S.nloc + 64))) {  // receivers decide (k_gossip_redges)
+            return rc;
+        }
+    }
     if (S.topo == IMP3D) {
         S.rbits_words = S.kernel == KERNEL_COL ? col_rbits_words(S.nloc / S.G.g2, S.G.g)
                                                : rbits_words_for(S.lo, S.nloc);
@@ -821,7 +828,7 @@ double alg_bytes(const gp_sim* s) {
     // gossip: counter r+w 8, direction byte r+w 2 (+ Imp3D in-list 8, and with the
     // separate random-edge delivery pass of the column kernel its per-node count
     // written and read, 2 + 2)
-    if (S.topo == IMP3D) return S.rcnt ? 22.0 : 18.0;
+    if (S.topo == IMP3D) return S.rq[0] ? 22.0 : S.rcnt ? 22.0 : 18.0;
     if (S.topo != FULL) return 10.0;
     return 4.0 + 8.0 + 8.0 + 8.0;  // send: c + atomic RMW; recv: inc r+w, c r+w
 }

@@ -24,14 +24,13 @@
 // Built with -ffp-contract=off: the fold must round exactly like the oracle.
 #include "gp_wavecommon.hpp"
 
-#ifndef GP_COL_MINW
 // gossip column kernel: waves per SIMD (measured 5..7 with the batched step loads,
-// profiles/r02/col_batch/: Imp3D best at 5, 3D at 7)
-#define GP_COL_MINW(TOPO) ((TOPO) == IMP3D ? 5 : 7)
+// profiles/r02/col_batch/: Imp3D best at 5, 3D at 7); GP_COL_WAVES (experiments)
+// sets one value for both
+#ifdef GP_COL_WAVES
+#define GP_COL_MINW(TOPO) GP_COL_WAVES
 #else
-#define GP_COL_MINW_FIXED GP_COL_MINW
-#undef GP_COL_MINW
-#define GP_COL_MINW(TOPO) GP_COL_MINW_FIXED
+#define GP_COL_MINW(TOPO) ((TOPO) == IMP3D ? 5 : 7)
 #endif
 
 namespace gp {
@@ -396,6 +395,7 @@ __global__ __launch_bounds__(BULK_THREADS, GP_COL_MINW(TOPO)) void k_gossip_col(
     const int lane = threadIdx.x & 63;
     const uint8_t* __restrict__ nbc = a.nbc;
     const uint32_t g = a.G.g, g2 = a.G.g2, base = a.base, lo = a.lo;
+    const bool push = a.rq_cur != nullptr;  // one rank: senders count random-edge deliveries (no k_gossip_redges)
     uint32_t alerts = 0;
 
     uint32_t it, it_end, it_step;
@@ -450,7 +450,7 @@ __global__ __launch_bounds__(BULK_THREADS, GP_COL_MINW(TOPO)) void k_gossip_col(
             // z +- 1 senders: the neighbour lanes' bytes of plane x (cb, by DPP); only the
             // wave's end lanes load theirs (lane 0: z - 1, lane 63: z + 1, one register).
             const uint32_t pxb = px - base;
-            uint32_t lnn[NR], led[NR], lrc[NR];
+            uint32_t lnn[NR], led[NR], lrc[NR], lrd[NR];
             int32_t cv[NR];
             const bool ledge = (lane == 0 && z > 0) || (lane == 63 && z + 1 < g);
 #pragma unroll
@@ -459,13 +459,22 @@ __global__ __launch_bounds__(BULK_THREADS, GP_COL_MINW(TOPO)) void k_gossip_col(
                 lnn[k] = nbc[(pf ? 2u * g2 : 0u) + jl];
                 cv[k] = a.c[px + yo[k] - lo];
                 led[k] = nbc[(rv[k] && ledge) ? (lane == 0 ? jl - 1 : jl + 1) : jl];
-                lrc[k] = TOPO == IMP3D ? (uint32_t)a.rcnt[px + yo[k] - lo] : 0u;
+                lrc[k] = lrd[k] = 0u;
+                if (TOPO == IMP3D) {
+                    if (push) {
+                        lrc[k] = a.rq_cur[px + yo[k] - lo];
+                        lrd[k] = a.rnd[px + yo[k] - lo];
+                    } else {
+                        lrc[k] = a.rcnt[px + yo[k] - lo];
+                    }
+                }
             }
             const bool hmv = zv && y0 > 0, hpv = zv && y0 + NR < g;
             uint32_t hym = nbc[hmv ? pxb + (y0 - 1) * g + z : pxb];
             uint32_t hyp = nbc[hpv ? pxb + (y0 + NR) * g + z : pxb];
 #pragma unroll
-            for (int k = 0; k < NR; ++k) asm volatile("" : "+v"(lnn[k]), "+v"(cv[k]), "+v"(led[k]), "+v"(lrc[k]));
+            for (int k = 0; k < NR; ++k)
+                asm volatile("" : "+v"(lnn[k]), "+v"(cv[k]), "+v"(led[k]), "+v"(lrc[k]), "+v"(lrd[k]));
             asm volatile("" : "+v"(hym), "+v"(hyp));
             if (!hmv) hym = DIR_NONE;
             if (!hpv) hyp = DIR_NONE;
@@ -509,6 +518,13 @@ __global__ __launch_bounds__(BULK_THREADS, GP_COL_MINW(TOPO)) void k_gossip_col(
                     if (deg > 0) dir = slot_to_dir(mask, uniform(a.k0, a.k1, S_GOSSIP, j, r + 1, deg));
                 }
                 if (rv[k]) a.nbn[j - base] = (uint8_t)dir;
+                if (TOPO == IMP3D && push && rv[k]) {
+                    // one rank, push form: this round's count consumed, and a send on the
+                    // random edge next round counted at its target now (the receiver
+                    // drops it at round start if converged, Program.fs:87)
+                    if (lrc[k]) a.rq_cur[j - lo] = 0u;
+                    if (dir == DIR_RANDOM) atomicAdd(&a.rq_next[lrd[k] - lo], 1u);
+                }
                 if (TOPO == IMP3D) {
                     const unsigned long long bits = __ballot(rv[k] && dir == DIR_RANDOM);
                     if (lane == 0 && y0 + k < g) a.rbn[col_rb_word(a, x, y0 + k, zs * 64)] = bits;
@@ -659,6 +675,8 @@ __global__ __launch_bounds__(BULK_THREADS) void k_col_rbits_init(WaveArgs a, con
     }
     for (uint32_t w = blockIdx.x * BULK_THREADS + threadIdx.x; w < words; w += gridDim.x * BULK_THREADS)
         a.rbn[w] = w == sw ? sbit : 0ull;
+    // one rank, push form: the seed's round-0 send on its random edge, counted at the target
+    if (a.rq_cur && sbit && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&a.rq_cur[a.rnd[i - a.lo] - a.lo], 1u);
 }
 
 uint32_t col_rbits_words(uint32_t planes, uint32_t g) { return planes * g * ((g + 63) / 64) + 16u; }
@@ -689,9 +707,11 @@ hipError_t launch_round_col(const WaveArgs& a, int topo, int alg, uint32_t round
         if (topo == GRID3D) {
             hipLaunchKernelGGL(k_gossip_col<GRID3D>, g, b, 0, st, a, round);
         } else {
-            if (!a.rcnt) return hipErrorInvalidValue;
-            const uint32_t ge = std::min<uint32_t>((a.nloc + RE_TILE - 1) / RE_TILE, 256u * 16u);
-            hipLaunchKernelGGL(k_gossip_redges, dim3(std::max(1u, ge)), b, 0, st, a, round);
+            if (!a.rq_cur) {  // several ranks: receivers decide their in-edges (exchange tags for remote senders)
+                if (!a.rcnt) return hipErrorInvalidValue;
+                const uint32_t ge = std::min<uint32_t>((a.nloc + RE_TILE - 1) / RE_TILE, 256u * 16u);
+                hipLaunchKernelGGL(k_gossip_redges, dim3(std::max(1u, ge)), b, 0, st, a, round);
+            }
             hipLaunchKernelGGL(k_gossip_col<IMP3D>, g, b, 0, st, a, round);
         }
     }

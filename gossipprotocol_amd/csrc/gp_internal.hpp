@@ -134,6 +134,7 @@ struct DevState {
     // gossip, Imp3D, column kernel: random-edge rumours each local node receives
     // this round (k_gossip_redges, before the round kernel), indexed from lo
     uint16_t* rcnt;
+    uint32_t* rq[2];      // gossip Imp3D column kernel, one rank: random-edge deliveries per node, by round parity
     // Imp3D: bit i of rbits[b] = node i sends on its random edge in the round
     // of buffer b (ballot-packed by the round kernel)
     uint64_t* rbits[2];
@@ -233,6 +234,9 @@ struct WaveArgs {
     const double2* rmsg;
     int32_t* c;
     uint16_t* rcnt;          // gossip Imp3D (column kernel): random-edge deliveries per local node
+    uint32_t* rq_cur;        // one rank: this round's random-edge deliveries per node (read, then zeroed)
+    uint32_t* rq_next;       // one rank: next round's, counted by their senders with atomics
+    const uint32_t* rnd;     // random edge of each local sender (id - lo)
     Ctl* ctl;
     Geom G;
     uint32_t k0, k1, seed_node;

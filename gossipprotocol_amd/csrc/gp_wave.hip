@@ -414,6 +414,9 @@ WaveArgs make_wave_args(const DevState& S, uint32_t round) {
     a.rmsg = S.rmsg;
     a.c = S.c;
     a.rcnt = S.rcnt;
+    a.rq_cur = S.rq[round & 1];
+    a.rq_next = S.rq[(round + 1) & 1];
+    a.rnd = S.rnd;
     a.ctl = S.ctl;
     a.G = S.G;
     a.k0 = S.k0;
