@@ -406,16 +406,6 @@ int build_imp3d(gp_sim* s) {
             HIP_TRY(launch_pack_ind4(S, wide_at, s->grid, s->stream));
         }
         S.nedges = ne;
-        S.eb = nullptr;
-        // separate dense edge-decision pass (k_edge_decide): measured slower than the
-        // tile kernel's own batched redraw (1.4 + 14.9 vs 14.5 ms/round at P = 1e9), opt-in
-        bool edge_pass = false;
-#ifdef GP_EXPERIMENTS
-        if (const char* e = std::getenv("GP_EDGE_PASS")) edge_pass = e[0] == '1';
-#endif
-        if (S.alg == PUSHSUM && S.kernel == KERNEL_TILE && edge_pass &&
-            (rc = dev_alloc_t(s, &S.eb, (size_t)ne / 64 + 8)))
-            return rc;
         if (W > 1) {
             if ((rc = dev_alloc_t(s, &sl.pos, S.nloc)) || (rc = dev_alloc_t(s, &S.rtag, ne)) ||
                 (S.alg == PUSHSUM && (rc = dev_alloc_t(s, &S.rmsg, ne))))
@@ -851,18 +841,13 @@ void choose_kernel(gp_sim* s, int64_t nloc_max, int& kernel, uint32_t& col_xsegs
 #ifdef GP_EXPERIMENTS
     if (const char* e = std::getenv("GP_KERNEL")) {
         if (!std::strcmp(e, "tile")) kernel = KERNEL_TILE;
-        else if (!std::strcmp(e, "wave")) kernel = KERNEL_WAVE;
-        else if (!std::strcmp(e, "col") && lattice) kernel = KERNEL_COL;
+        else if (!std::strcmp(e, "col") && lattice && cfg->algorithm == GP_GOSSIP) kernel = KERNEL_COL;
     }
 #endif
     col_xsegs = 1;
     if (cfg->topology != GP_FULL && kernel != KERNEL_TILE) {
         // exactly the resident grid (a persistent sweep), a multiple of the 8 XCDs
-        int bpc = 1;
-        if (kernel == KERNEL_COL) bpc = col_blocks_per_cu(cfg->topology, cfg->algorithm);
-#ifdef GP_EXPERIMENTS
-        else bpc = wave_blocks_per_cu(cfg->topology, cfg->algorithm);
-#endif
+        const int bpc = col_blocks_per_cu(cfg->topology, cfg->algorithm);
         cap = (int64_t)prop.multiProcessorCount * bpc;
         if (kernel == KERNEL_COL) {
             // x segments per patch: enough work items for every resident wave, >= 16 planes each

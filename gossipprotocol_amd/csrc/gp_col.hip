@@ -1,7 +1,7 @@
 // gp_col.hip -- column-march round kernels for the 3D / Imp3D lattice (gfx950).
 //
-// One synchronous round of SRS v1 in PULL form with 2.5-D
-// blocking.  A wave owns a patch of 4 y-rows x 64 z-columns (one node per lane
+// Gossip: one synchronous round of SRS v1 in PULL form with 2.5-D
+// blocking (push-sum: gp_pscol.hip).  A wave owns a patch of 4 y-rows x 64 z-columns (one node per lane
 // and row; node id = x*g^2 + y*g + z, lanes = consecutive z, so every row of a
 // patch is one coalesced 64-node segment) and marches it along x through its
 // x-segment.  Planes x and x+1 of the patch stay in registers and plane x+2 is
@@ -10,12 +10,10 @@
 //   x-1 was streamed by this same wave one step ago (L2), and
 //   z+-1 sit in the lines this wave just loaded (L1),
 // and only the two y-halo rows touch another wave's data.  Per node and round
-// the compulsory stream is own (s, w) + node byte in and out; the lattice
-// costs no HBM traffic of its own.  Imp3D in-edges are swept per step exactly
-// like the chunk kernel (gp_wave.hip): flattened over the patch's four row
-// segments, decided by Philox / bitmap / exchange tag, gathered with all loads
-// of the sweep in flight, parked in wave-private LDS, folded per node in
-// canonical order.
+// the compulsory stream is the rumour counter + node byte in and out; the
+// lattice costs no HBM traffic of its own.  Imp3D random-edge deliveries are
+// integer counts: counted by their senders a round ahead (one rank) or by the
+// receivers' delivery pass k_gossip_redges (several ranks).
 //
 // Work items (patch, x-segment) are dealt XCD-contiguously: the waves of one
 // XCD own one y-band of every plane, so y-halo rows come from the XCD's L2.
@@ -78,311 +76,7 @@ __device__ __forceinline__ void item_range(uint32_t n, uint32_t& it, uint32_t& e
 
 __device__ __forceinline__ uint32_t byte_of(uint32_t packed, int k) { return (packed >> (8 * k)) & 0xFFu; }
 
-// In-edge sweep of one patch-step: rows k = 0..NR-1 own the edges
-// [e0[k], e0[k] + cnt) of the CSR; flat index q = P[k] + (e - e0[k]).
-// PUSH: park (s, w) of senders that used their random edge; gossip: 0/1 codes.
-template <bool PUSH>
-__device__ __forceinline__ void sweep_in_edges(const WaveArgs& a, WaveLds& L, const uint32_t (&e0)[NR],
-                                               const uint32_t (&P)[NR + 1], uint32_t r, bool all_active,
-                                               uint32_t stream) {
-    const int lane = threadIdx.x & 63;
-    const uint32_t lo = a.lo, nloc = a.nloc, base = a.base;
-    const uint32_t nst = min(P[NR], ECAP);
-    uint32_t nmsg = 0;
-    for (uint32_t q0 = 0; q0 < nst; q0 += EU * 64) {
-        uint32_t eidx[EU], src[EU];
-        bool sent[EU];
-#pragma unroll
-        for (int m = 0; m < EU; ++m) {
-            const uint32_t q = q0 + m * 64 + lane;
-            const uint32_t k = (q >= P[1] ? 1u : 0u) + (q >= P[2] ? 1u : 0u) + (q >= P[3] ? 1u : 0u);
-            const uint32_t eb = k == 0 ? e0[0] : k == 1 ? e0[1] : k == 2 ? e0[2] : e0[3];
-            const uint32_t pb = k == 0 ? P[0] : k == 1 ? P[1] : k == 2 ? P[2] : P[3];
-            eidx[m] = eb + (q - pb);
-            src[m] = q < nst ? a.in_src[eidx[m]] : lo;
-        }
-        // decisions: every sender's direction draw of round r as one Philox batch
-        // (interleaved chains), the bitmap read only where the draw picks the
-        // random slot (col_sent_random)
-        {
-            const Geom& G = a.G;
-            uint32_t xs[EU], ys[EU], wrd[EU], di[EU];
-#pragma unroll
-            for (int m = 0; m < EU; ++m) {
-                const uint32_t i = src[m];
-                const uint32_t x = fastdiv(i, G.div_g2);
-                const uint32_t rem = i - x * G.g2;
-                const uint32_t y = fastdiv(rem, G.div_g);
-                const uint32_t z = rem - y * G.g;
-                di[m] = popc6(mask_xyz(x, y, z, G.g - 1)) + 1u;
-                wrd[m] = z;
-                xs[m] = x;
-                ys[m] = y;
-            }
-            uint32_t X[EU], Y[EU];
-            philox2_batch<EU>(src, r, stream, a.k0, a.k1, X, Y);
-#pragma unroll
-            for (int m = 0; m < EU; ++m) {
-                const uint32_t q = q0 + m * 64 + lane;
-                bool s = false;
-                if (q < nst) {
-                    const uint32_t i = src[m];
-                    if (i - lo >= nloc) {
-                        s = a.rtag[eidx[m]] == r;  // sender on another rank
-                    } else if (uniform_from(X[m], Y[m], di[m]) == di[m] - 1u) {
-                        const uint32_t z = wrd[m];
-                        s = all_active || ((a.rbc[col_rb_word(a, xs[m], ys[m], z)] >> (z & 63)) & 1ull);
-                    }
-                }
-                sent[m] = s;
-            }
-        }
-        if (PUSH) {
-            double2 val[EU];
-#pragma unroll
-            for (int m = 0; m < EU; ++m) {
-                const uint32_t i = src[m];
-                val[m] = make_double2(0.0, 0.0);
-                if (sent[m]) val[m] = (i - lo >= nloc) ? a.rmsg[eidx[m]] : a.swc[i - base];
-            }
-#pragma unroll
-            for (int m = 0; m < EU; ++m) {
-                const uint32_t q = q0 + m * 64 + lane;
-                const unsigned long long bal = __ballot(sent[m]);
-                const uint32_t slot = nmsg + lane_prefix(bal);
-                nmsg += (uint32_t)__popcll(bal);
-                if (q < nst) L.code[q] = !sent[m] ? CODE_NONE : (slot < MCAP ? slot : CODE_GLOBAL);
-                if (sent[m] && slot < MCAP) L.msg[slot] = val[m];
-            }
-        } else {
-#pragma unroll
-            for (int m = 0; m < EU; ++m) {
-                const uint32_t q = q0 + m * 64 + lane;
-                if (q < nst) L.code[q] = sent[m] ? 1u : 0u;
-            }
-        }
-    }
-    wave_lds_sync();
-}
-
-// Row k's CSR bounds of the patch-step: per-lane offset and the row's end.
-[[maybe_unused]] __device__ __forceinline__ void row_offsets(const WaveArgs& a, uint32_t rs, uint32_t nz, bool row_ok, uint32_t& off,
-                                            uint32_t& rend) {
-    const int lane = threadIdx.x & 63;
-    if (row_ok) {
-        off = a.in_off[rs + min((uint32_t)lane, nz) - a.lo];
-        rend = a.in_off[rs + nz - a.lo];
-    } else {
-        off = 0;
-        rend = 0;
-    }
-}
-
 }  // namespace
-
-// ---------------------------------------------------------------- push-sum
-// Experiment variant (push-sum runs the tiled kernel):
-// experiments library only.
-#ifdef GP_EXPERIMENTS
-template <int TOPO>
-__global__ __launch_bounds__(BULK_THREADS) void k_ps_col(WaveArgs a, uint32_t r) {
-    __shared__ WaveLds Lw[WPB];
-    Ctl* ctl = a.ctl;
-    if (ld_agent(&ctl->done)) return;
-    const bool all_active = ld_agent(&ctl->all_active) != 0;
-    const int lane = threadIdx.x & 63;
-    WaveLds& L = Lw[threadIdx.x >> 6];
-    const double2* __restrict__ swc = a.swc;
-    double2* __restrict__ swn = a.swn;
-    const uint8_t* __restrict__ nbc = a.nbc;
-    const uint32_t g = a.G.g, g2 = a.G.g2, base = a.base, lo = a.lo, nloc = a.nloc;
-    uint32_t alerts = 0, newly = 0;
-
-    uint32_t it, it_end, it_step;
-    item_range(a.nitems, it, it_end, it_step);
-    for (; it < it_end; it += it_step) {
-        const uint32_t zs = it % a.zsegs;
-        const uint32_t t = it / a.zsegs;
-        const uint32_t yb = t % a.yblocks;
-        const uint32_t xa = a.x_lo + (t / a.yblocks) * a.xs_len;
-        const uint32_t xb = min(a.x_hi, xa + a.xs_len);
-        const uint32_t z = zs * 64 + (uint32_t)lane;
-        const uint32_t nz = min(64u, g - zs * 64);
-        const uint32_t y0 = yb * NR;
-        const bool zv = z < g;
-        bool rv[NR];
-        uint32_t yo[NR], myz[NR];
-#pragma unroll
-        for (int k = 0; k < NR; ++k) {
-            const uint32_t y = y0 + k;
-            rv[k] = zv && y < g;
-            yo[k] = rv[k] ? y * g + z : 0u;
-            myz[k] = (y + 1 < g ? 4u : 0u) | (y > 0 ? 8u : 0u) | (z + 1 < g ? 16u : 0u) | (z > 0 ? 32u : 0u);
-        }
-        // planes xa (cur) and xa+1 (nxt), direction bytes of xa-1 (pb)
-        double2 cur[NR], nxt[NR];
-        uint32_t pb = 0, cb = 0, nb = 0;
-#pragma unroll
-        for (int k = 0; k < NR; ++k) {
-            const uint32_t jl = xa * g2 + yo[k] - base;
-            cur[k] = rv[k] ? swc[jl] : make_double2(0.0, 1.0);
-            cb |= (rv[k] ? (uint32_t)nbc[jl] : (uint32_t)DIR_NONE) << (8 * k);
-            pb |= ((rv[k] && xa > 0) ? (uint32_t)nbc[jl - g2] : (uint32_t)DIR_NONE) << (8 * k);
-            const bool hn = rv[k] && xa + 1 < g;
-            nxt[k] = hn ? swc[jl + g2] : make_double2(0.0, 1.0);
-            nb |= (hn ? (uint32_t)nbc[jl + g2] : (uint32_t)DIR_NONE) << (8 * k);
-        }
-        for (uint32_t x = xa; x < xb; ++x) {
-            const uint32_t px = x * g2;
-            // prefetch plane x+2 (the nxt of the next step)
-            const bool pf = x + 1 < xb && x + 2 < g;
-            double2 nn[NR];
-            uint32_t nnb = 0;
-#pragma unroll
-            for (int k = 0; k < NR; ++k) {
-                const bool h = pf && rv[k];
-                const uint32_t jl = px + 2 * g2 + yo[k] - base;
-                nn[k] = h ? swc[jl] : make_double2(0.0, 1.0);
-                nnb |= (h ? (uint32_t)nbc[jl] : (uint32_t)DIR_NONE) << (8 * k);
-            }
-            // halo direction bytes of plane x: rows y0-1, y0+NR and columns z-+1
-            const uint32_t hym = (zv && y0 > 0) ? nbc[px + (y0 - 1) * g + z - base] : DIR_NONE;
-            const uint32_t hyp = (zv && y0 + NR < g) ? nbc[px + (y0 + NR) * g + z - base] : DIR_NONE;
-            uint32_t zbm = 0, zbp = 0;
-#pragma unroll
-            for (int k = 0; k < NR; ++k) {
-                const uint32_t jl = px + yo[k] - base;
-                zbm |= ((rv[k] && z > 0) ? (uint32_t)nbc[jl - 1] : (uint32_t)DIR_NONE) << (8 * k);
-                zbp |= ((rv[k] && z + 1 < g) ? (uint32_t)nbc[jl + 1] : (uint32_t)DIR_NONE) << (8 * k);
-            }
-            uint32_t off[NR], rend[NR], e0[NR], P[NR + 1];
-            if (TOPO == IMP3D) {
-#pragma unroll
-                for (int k = 0; k < NR; ++k) row_offsets(a, px + (y0 + k) * g + zs * 64, nz, y0 + k < g, off[k], rend[k]);
-                P[0] = 0;
-#pragma unroll
-                for (int k = 0; k < NR; ++k) {
-                    e0[k] = __builtin_amdgcn_readlane(off[k], 0);
-                    P[k + 1] = P[k] + (rend[k] - e0[k]);
-                }
-                sweep_in_edges<true>(a, L, e0, P, r, all_active, S_PUSHSUM);
-            }
-#pragma unroll
-            for (int k = 0; k < NR; ++k) {
-                const uint32_t j = px + yo[k];
-                const uint32_t jl = j - base;
-                const uint32_t mask = rv[k] ? (myz[k] | (x > 0 ? 1u : 0u) | (x + 1 < g ? 2u : 0u)) : 0u;
-                uint32_t f = 0;
-                f |= ((mask & 1u) && (byte_of(pb, k) & DIR_MASK) == 1u) ? 1u : 0u;
-                f |= ((mask & 2u) && (byte_of(nb, k) & DIR_MASK) == 0u) ? 2u : 0u;
-                f |= ((mask & 4u) && ((k + 1 < NR ? byte_of(cb, k + 1) : hyp) & DIR_MASK) == 3u) ? 4u : 0u;
-                f |= ((mask & 8u) && ((k > 0 ? byte_of(cb, k - 1) : hym) & DIR_MASK) == 2u) ? 8u : 0u;
-                f |= ((mask & 16u) && (byte_of(zbp, k) & DIR_MASK) == 5u) ? 16u : 0u;
-                f |= ((mask & 32u) && (byte_of(zbm, k) & DIR_MASK) == 4u) ? 32u : 0u;
-                const uint32_t b = byte_of(cb, k);
-                const uint32_t deg = popc6(mask) + (TOPO == IMP3D ? 1u : 0u);
-                bool active = (b & B_ACTIVE) != 0;
-                const double2 sv = cur[k];
-                const bool halve = active && deg > 0;
-                double acc_s = halve ? sv.x * 0.5 : sv.x;
-                double acc_w = halve ? sv.y * 0.5 : sv.y;
-                const double2 z2 = make_double2(0.0, 0.0);
-                double2 m[6];
-                m[0] = (f & 1u) ? swc[jl - g2] : z2;
-                m[1] = (f & 2u) ? nxt[k] : z2;
-                if (k + 1 < NR) m[2] = (f & 4u) ? cur[k + 1 < NR ? k + 1 : k] : z2;
-                else m[2] = (f & 4u) ? swc[jl + g] : z2;
-                if (k > 0) m[3] = (f & 8u) ? cur[k > 0 ? k - 1 : k] : z2;
-                else m[3] = (f & 8u) ? swc[jl - g] : z2;
-                m[4] = (f & 16u) ? swc[jl + 1] : z2;
-                m[5] = (f & 32u) ? swc[jl - 1] : z2;
-#pragma unroll
-                for (int d = 0; d < 6; ++d) {
-                    if ((f >> d) & 1u) {
-                        acc_s = acc_s + m[d].x * 0.5;
-                        acc_w = acc_w + m[d].y * 0.5;
-                    }
-                }
-                bool recv = f != 0;
-                if (TOPO == IMP3D) {
-                    const uint32_t ebk = off[k];
-                    uint32_t ee = __shfl_down(ebk, 1, 64);
-                    if (lane == 63) ee = rend[k];
-                    for (uint32_t e = ebk; e < ee; ++e) {
-                        const uint32_t q = P[k] + (e - e0[k]);
-                        bool s;
-                        double2 mi = z2;
-                        if (q < ECAP) {
-                            const uint32_t code = L.code[q];
-                            s = code != CODE_NONE;
-                            if (code < MCAP) {
-                                mi = L.msg[code];
-                            } else if (s) {  // parked-message overflow: reload
-                                const uint32_t i = a.in_src[e];
-                                mi = (i - lo >= nloc) ? a.rmsg[e] : swc[i - base];
-                            }
-                        } else {  // beyond the staged edges: decide here
-                            const uint32_t i = a.in_src[e];
-                            if (i - lo >= nloc) {
-                                s = a.rtag[e] == r;
-                                if (s) mi = a.rmsg[e];
-                            } else {
-                                s = col_sent_random(a, i, r, all_active, S_PUSHSUM);
-                                if (s) mi = swc[i - base];
-                            }
-                        }
-                        if (s) {
-                            acc_s = acc_s + mi.x * 0.5;
-                            acc_w = acc_w + mi.y * 0.5;
-                            recv = true;
-                        }
-                    }
-                }
-                uint32_t flags = b & (B_ACTIVE | B_CONV | (3u << CNT_SHIFT));
-                if (recv) {
-                    if (!(b & B_CONV)) {
-                        const double r_old = sv.x / sv.y;
-                        const double r_new = acc_s / acc_w;
-                        uint32_t cnt = (b >> CNT_SHIFT) & 3u;
-                        cnt = fabs(r_new - r_old) > 1e-10 ? 0u : cnt + 1u;
-                        flags = (flags & ~(3u << CNT_SHIFT)) | (cnt << CNT_SHIFT);
-                        if (cnt == 3) {
-                            flags |= B_CONV;
-                            ++alerts;
-                        }
-                    }
-                    if (!active) {
-                        ++newly;
-                        flags |= B_ACTIVE;
-                        active = true;
-                    }
-                }
-                uint32_t dir = DIR_NONE;
-                if (active && deg > 0) dir = slot_to_dir(mask, uniform(a.k0, a.k1, S_PUSHSUM, j, r + 1, deg));
-                if (rv[k]) {
-                    a.nbn[jl] = (uint8_t)(flags | dir);
-                    swn[jl] = make_double2(acc_s, acc_w);
-                }
-                if (TOPO == IMP3D && !all_active) {
-                    const unsigned long long bits = __ballot(rv[k] && dir == DIR_RANDOM);
-                    if (lane == 0 && y0 + k < g) a.rbn[col_rb_word(a, x, y0 + k, zs * 64)] = bits;
-                }
-            }
-            if (TOPO == IMP3D) wave_lds_sync();  // the next step's sweep overwrites L
-            // rotate the plane window
-            pb = cb;
-            cb = nb;
-            nb = nnb;
-#pragma unroll
-            for (int k = 0; k < NR; ++k) {
-                cur[k] = nxt[k];
-                nxt[k] = nn[k];
-            }
-        }
-    }
-    block_add2(alerts, newly, &ctl->round_alerts, &ctl->round_active);
-}
-#endif  // GP_EXPERIMENTS
 
 // ---------------------------------------------------------------- gossip
 // Deliveries to j = lattice senders pointing here + Imp3D random-edge senders
@@ -682,13 +376,8 @@ __global__ __launch_bounds__(BULK_THREADS) void k_col_rbits_init(WaveArgs a, con
 uint32_t col_rbits_words(uint32_t planes, uint32_t g) { return planes * g * ((g + 63) / 64) + 16u; }
 
 int col_blocks_per_cu(int topo, int alg) {
-    const void* f;
-    f = topo == GRID3D ? (const void*)k_gossip_col<GRID3D> : (const void*)k_gossip_col<IMP3D>;
-#ifdef GP_EXPERIMENTS
-    if (alg == PUSHSUM) f = topo == GRID3D ? (const void*)k_ps_col<GRID3D> : (const void*)k_ps_col<IMP3D>;
-#else
     (void)alg;
-#endif
+    const void* f = topo == GRID3D ? (const void*)k_gossip_col<GRID3D> : (const void*)k_gossip_col<IMP3D>;
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, BULK_THREADS, 0) != hipSuccess || n < 1) n = 1;
     return n;
@@ -697,12 +386,7 @@ int col_blocks_per_cu(int topo, int alg) {
 hipError_t launch_round_col(const WaveArgs& a, int topo, int alg, uint32_t round, int grid, hipStream_t st) {
     const dim3 g(grid), b(BULK_THREADS);
     if (alg == PUSHSUM) {
-#ifdef GP_EXPERIMENTS
-        if (topo == GRID3D) hipLaunchKernelGGL(k_ps_col<GRID3D>, g, b, 0, st, a, round);
-        else hipLaunchKernelGGL(k_ps_col<IMP3D>, g, b, 0, st, a, round);
-#else
-        return hipErrorInvalidValue;
-#endif
+        return hipErrorInvalidValue;  // push-sum column kernel: launch_round_pscol (gp_pscol.hip)
     } else {
         if (topo == GRID3D) {
             hipLaunchKernelGGL(k_gossip_col<GRID3D>, g, b, 0, st, a, round);
@@ -723,6 +407,48 @@ hipError_t launch_col_rbits_init(const DevState& S, hipStream_t st) {
     a.rbn = S.rbits[0];  // the bits of round 0's sends
     hipLaunchKernelGGL(k_col_rbits_init, dim3(256), dim3(BULK_THREADS), 0, st, a, S.nb[0], S.rbits_words);
     return hipGetLastError();
+}
+
+WaveArgs make_wave_args(const DevState& S, uint32_t round) {
+    const int cur = round & 1;
+    WaveArgs a;
+    a.swc = S.sw[cur];
+    a.swn = S.sw[cur ^ 1];
+    a.nbc = S.nb[cur];
+    a.nbn = S.nb[cur ^ 1];
+    a.rbc = S.rbits[cur];
+    a.rbn = S.rbits[cur ^ 1];
+    a.in_off = S.in_off;
+    a.in_src = S.in_src;
+    a.rtag = S.rtag;
+    a.rmsg = S.rmsg;
+    a.c = S.c;
+    a.rcnt = S.rcnt;
+    a.rq_cur = S.rq[round & 1];
+    a.rq_next = S.rq[(round + 1) & 1];
+    a.rnd = S.rnd;
+    a.ctl = S.ctl;
+    a.G = S.G;
+    a.k0 = S.k0;
+    a.k1 = S.k1;
+    a.seed_node = S.seed_node;
+    a.lo = S.lo;
+    a.nloc = S.nloc;
+    a.base = S.base;
+    a.x_lo = a.x_hi = a.zsegs = a.yblocks = a.xs_len = a.nitems = 0;
+    if (S.G.g2) {  // column kernels (3D / Imp3D)
+        const uint32_t g = S.G.g;
+        a.x_lo = S.lo / S.G.g2;
+        a.x_hi = (S.lo + S.nloc) / S.G.g2;
+        a.zsegs = (g + 63) / 64;
+        a.yblocks = (g + 3) / 4;
+        const uint32_t planes = a.x_hi - a.x_lo;
+        const uint32_t xs = S.col_xsegs ? S.col_xsegs : 1u;
+        a.xs_len = (planes + xs - 1) / xs;
+        const uint32_t nseg = a.xs_len ? (planes + a.xs_len - 1) / a.xs_len : 0u;
+        a.nitems = a.zsegs * a.yblocks * nseg;
+    }
+    return a;
 }
 
 }  // namespace gp

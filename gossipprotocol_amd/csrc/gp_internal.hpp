@@ -173,10 +173,8 @@ struct DevState {
     uint32_t tile_wx;    // RoundArgs::wx
     uint32_t tile_stage_cap;  // RoundArgs::stage_cap (experiments build only; default: no limit)
     uint32_t fuse_finalize;   // the round kernel closes its own round (single rank push-sum)
-    // Imp3D push-sum, tile kernel: the rank's in-edge count and the steady-state
-    // edge-decision bitmap (k_edge_decide), one bit per in-edge
+    // Imp3D: the rank's in-edge count
     uint32_t nedges;
-    uint64_t* eb;
     // walk 3 (dynamic tile queue): per round parity, 8 per-XCD item counters,
     // TQ_STRIDE words apart (one 256-byte line each)
     uint32_t* tq;
@@ -211,16 +209,15 @@ struct RoundArgs {
     uint32_t wx;    // walk 2: planes per x-window
     uint32_t stage_cap;  // k_ps_tile: tiles with more in-edges take the unstaged path (tests force it)
     uint32_t fuse;       // k_ps_tile: the last block closes the round (no k_finalize launch)
-    const uint64_t* eb;  // Imp3D: this round's edge decisions (k_edge_decide), or null
     const uint32_t* wt;  // walk 3: tile list (DevState::wtiles), XCD c's items at [wo[c], wo[c + 1])
     uint32_t wo[9];
     uint32_t* tq;        // walk 3: this round's 8 per-XCD tile-item counters (TQ_STRIDE apart)
     uint32_t* tq_next;   // walk 3: the next round's counters, zeroed by block 0 this round
 };
 
-enum KernelVariant : int { KERNEL_WAVE = 0, KERNEL_TILE = 1, KERNEL_COL = 2 };
+enum KernelVariant : int { KERNEL_TILE = 1, KERNEL_COL = 2 };
 
-// Arguments of the wave-autonomous round kernels (gp_wave.hip, gp_col.hip).
+// Arguments of the column-march gossip kernels (gp_col.hip).
 struct WaveArgs {
     const double2* swc;
     double2* swn;
@@ -240,19 +237,14 @@ struct WaveArgs {
     Ctl* ctl;
     Geom G;
     uint32_t k0, k1, seed_node;
-    uint32_t lo, nloc, base, nchunks;
+    uint32_t lo, nloc, base;
     // column kernels (gp_col.hip): planes [x_lo, x_hi) of this rank, patches of
     // 64 z x 4 y rows, x split into segments of xs_len planes
     uint32_t x_lo, x_hi, zsegs, yblocks, xs_len, nitems;
 };
 
-// ---- wave-autonomous round kernels (gp_wave.hip)
-uint32_t wave_chunks(uint32_t lo, uint32_t nloc);
-int wave_blocks_per_cu(int topo, int alg);
-hipError_t launch_round_wave(const WaveArgs& a, int topo, int alg, uint32_t round, int grid, hipStream_t st);
-WaveArgs make_wave_args(const DevState& S, uint32_t round);
-
 // ---- column-march round kernels (gp_col.hip): 3D / Imp3D
+WaveArgs make_wave_args(const DevState& S, uint32_t round);
 hipError_t launch_round_col(const WaveArgs& a, int topo, int alg, uint32_t round, int grid, hipStream_t st);
 int col_blocks_per_cu(int topo, int alg);
 // random-edge bitmap words of the column layout (one 64-bit word per 64-node row segment)

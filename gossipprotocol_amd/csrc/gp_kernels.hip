@@ -381,11 +381,7 @@ hipError_t launch_bulk(const DevState& S, uint32_t round, int grid, hipStream_t 
     if (S.topo != FULL) {
         if (S.kernel == KERNEL_TILE) return launch_round_tile(S, round, grid, st);
         if (S.kernel == KERNEL_COL) return launch_round_col(make_wave_args(S, round), S.topo, S.alg, round, grid, st);
-#ifdef GP_EXPERIMENTS
-        return launch_round_wave(make_wave_args(S, round), S.topo, S.alg, round, grid, st);
-#else
         return hipErrorInvalidValue;
-#endif
     }
     if (S.alg == PUSHSUM) {
         return launch_full_pushsum_round(S, round, grid, st);
@@ -397,19 +393,13 @@ hipError_t launch_bulk(const DevState& S, uint32_t round, int grid, hipStream_t 
 }
 
 const char* bulk_kernel_name(const DevState& S) {
-    static const char* ps[3][4] = {{"k_ps_wave<LINE>", "k_fb_send+split+fold", "k_ps_wave<GRID3D>",
-                                    "k_ps_wave<IMP3D>"},
-                                   {"k_ps_tile<LINE>", "k_fb_send+split+fold", "k_ps_tile<GRID3D>",
-                                    "k_ps_tile<IMP3D>"},
-                                   {"k_ps_wave<LINE>", "k_fb_send+split+fold", "k_ps_col<GRID3D>",
-                                    "k_ps_col<IMP3D>"}};
-    static const char* go[3][4] = {{"k_gossip_wave<LINE>", "k_full_gossip_send+recv", "k_gossip_wave<GRID3D>",
-                                    "k_gossip_wave<IMP3D>"},
-                                   {"k_gossip_tile<LINE>", "k_full_gossip_send+recv", "k_gossip_tile<GRID3D>",
+    static const char* ps[2][4] = {{"k_ps_tile<LINE>", "k_fb_send+split+fold", "k_ps_tile<GRID3D>", "k_ps_tile<IMP3D>"},
+                                   {"k_ps_tile<LINE>", "k_fb_send+split+fold", "k_ps_col<GRID3D>", "k_ps_col<IMP3D>"}};
+    static const char* go[2][4] = {{"k_gossip_tile<LINE>", "k_full_gossip_send+recv", "k_gossip_tile<GRID3D>",
                                     "k_gossip_tile<IMP3D>"},
-                                   {"k_gossip_wave<LINE>", "k_full_gossip_send+recv", "k_gossip_col<GRID3D>",
+                                   {"k_gossip_tile<LINE>", "k_full_gossip_send+recv", "k_gossip_col<GRID3D>",
                                     "k_gossip_col<IMP3D>"}};
-    const int v = S.kernel;
+    const int v = S.kernel == KERNEL_COL ? 1 : 0;
     return S.alg == PUSHSUM ? ps[v][S.topo] : go[v][S.topo];
 }
 

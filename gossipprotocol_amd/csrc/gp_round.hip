@@ -41,23 +41,8 @@ namespace gp {
 #ifndef GP_NT_STORES
 #define GP_NT_STORES 1
 #endif
-#ifndef GP_BATCH_EDGE
-#define GP_BATCH_EDGE 1  // in-edge Philox redraws of a thread as one interleaved batch
-#endif
-#ifndef GP_BATCH_DIR
-#define GP_BATCH_DIR 1   // next-round direction draws of a thread as one interleaved batch
-#endif
-#ifndef GP_PF_SRC
-#define GP_PF_SRC 0      // the next tile's senders loaded during this tile (measured slower: 14.9 vs 14.4 ms)
-#endif
 #ifndef GP_FMA_FOLD
 #define GP_FMA_FOLD 1    // fold as fma(m, 0.5, acc) (exact for |m| >= 2^-1021, guarded)
-#endif
-#ifndef GP_NGROUP
-#define GP_NGROUP 1      // nodes per thread whose lattice gathers are issued together
-#endif
-#ifndef GP_LMASK
-#define GP_LMASK 0       // lattice gathers exec-masked to the lanes with a sender (else: zero sentinel)
 #endif
 #ifndef GP_ABL_DIRS
 #define GP_ABL_DIRS 0    // ablation (wrong results, timing only): bit d set = skip the lattice gathers of slot d
@@ -65,28 +50,12 @@ namespace gp {
 #ifndef GP_STAMPS
 #define GP_STAMPS 0      // diagnostics (experiments build): per-phase cycle counts of the push-sum tile kernel
 #endif
-#ifndef GP_OWN_EARLY
-#define GP_OWN_EARLY 0   // own (s, w) loaded ahead of the staging copies (1) or with the lattice gathers (0)
-#endif
-#ifndef GP_EDGE_BATCH
-#define GP_EDGE_BATCH GP_NPT  // in-edge redraws per thread in the first Philox batch (the rest one at a time)
-#endif
 #ifndef GP_ZDPP
 #define GP_ZDPP 1        // push-sum tile kernel: the j+-1 messages from the neighbour lane's registers (DPP)
 #endif
-#ifndef GP_DEFER_ST
-#define GP_DEFER_ST 0    // a node slot's (s, w) store issued after the next slot's loads (measured: no gain)
-#endif
-#ifndef GP_OWN_LDS
-#define GP_OWN_LDS 0     // the tile's own (s, w) staged in LDS by DMA with the other staging copies
-#endif
 #ifndef GP_MINB
-#if GP_OWN_LDS
-#define GP_MINB 3  // 16 KB more LDS per tile: 3 resident workgroups per CU
-#else
 #define GP_MINB 5  // __launch_bounds__ minimum waves per SIMD (= resident 256-thread blocks per CU):
                    // the LDS tile allows 5, so keep VGPRs <= 96 to not lose the fifth
-#endif
 #endif
 
 namespace {
@@ -136,9 +105,6 @@ struct TileLdsP {
     uint32_t red[2][TPB / 64];
     uint32_t qn[2];                   // walk 3: the block's next item, by iteration parity
     double2 zb[TPB / 64][NPT][2];     // GP_ZDPP: (s, w) across each wave's ends, slot k: [0] node - 1, [1] node + 64
-#if GP_OWN_LDS
-    double2 own[TILE];                // the tile's (s, w) at round start
-#endif
 };
 
 
@@ -441,7 +407,6 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
         }
         const uint32_t cnt = e_hi - e_lo;
         const bool staged = cnt <= cap;
-        bool pf_next = false;
         if (TOPO == IMP3D && !dyn) {
             TileWalk nw = tw;
             nw.t += nw.step;
@@ -452,38 +417,26 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                 pf_lo = a.in_off[max(a.lo, nT)];
                 pf_hi = a.in_off[min(a.lo + a.nloc, nT + TILE)];
                 pf_tile = nti;
-                pf_next = GP_PF_SRC && pf_hi - pf_lo <= cap;
             }
         }
         if constexpr (TOPO == IMP3D) {
             if (staged) {
                 // in-edge q = m * TPB + wave * 64 + lane is bit `lane` of bitmap word
                 // m * 4 + wave; its message (if used) lands in slot q
-                if (!have_pf || !GP_PF_SRC) {
 #pragma unroll
-                    for (int m = 0; m < FU; ++m) {
-                        const uint32_t q = threadIdx.x + m * TPB;
-                        raw[m] = q < cnt ? __builtin_nontemporal_load(srcp + e_lo + q) : 0u;
-                    }
+                for (int m = 0; m < FU; ++m) {
+                    const uint32_t q = threadIdx.x + m * TPB;
+                    raw[m] = q < cnt ? __builtin_nontemporal_load(srcp + e_lo + q) : 0u;
                 }
                 uint32_t isrc[FU];
                 bool sent[FU];
 #pragma unroll
                 for (int m = 0; m < FU; ++m) isrc[m] = packed ? raw[m] & 0x3FFFFFFFu : raw[m];
-                if (all_active && a.eb) {
-                    // decided by k_edge_decide (this round's Philox redraws, one dense
-                    // pass): bit e_lo + q of the rank's edge bitmap
-#pragma unroll
-                    for (int m = 0; m < FU; ++m) {
-                        const uint32_t q = threadIdx.x + m * TPB;
-                        const uint32_t e = e_lo + q;
-                        sent[m] = q < cnt && ((a.eb[e >> 6] >> (e & 63u)) & 1ull);
-                    }
-                } else if (all_active && GP_BATCH_EDGE) {
+                if (all_active) {
                     // the first NPT edges per thread cover a tile's mean in-degree (TILE);
                     // the slots above are drawn only by waves that hold an edge there
                     // (a wave-uniform test: most tiles have fewer than TILE + 64 in-edges)
-                    constexpr int F0 = FU < GP_EDGE_BATCH ? FU : GP_EDGE_BATCH;
+                    constexpr int F0 = FU < NPT ? FU : NPT;
                     uint32_t x[FU], y[FU];
                     {
                         uint32_t n0[F0], x0[F0], y0[F0];
@@ -511,16 +464,6 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                         const uint32_t q = threadIdx.x + m * TPB;
                         const uint32_t di = packed ? (raw[m] >> 30) + 4u : popc6(present_mask<IMP3D>(isrc[m], G)) + 1u;
                         sent[m] = q < cnt && uniform_from(x[m], y[m], di) == di - 1u;
-                    }
-                } else if (all_active) {
-#pragma unroll
-                    for (int m = 0; m < FU; ++m) {
-                        const uint32_t q = threadIdx.x + m * TPB;
-                        sent[m] = false;
-                        if (q < cnt) {
-                            const uint32_t di = packed ? (raw[m] >> 30) + 4u : popc6(present_mask<IMP3D>(isrc[m], G)) + 1u;
-                            sent[m] = uniform(a.k0, a.k1, S_PUSHSUM, isrc[m], r, di) == di - 1u;
-                        }
                     }
                 } else {
                     // activation: the sender sends on its random edge iff its draw picks
@@ -574,15 +517,9 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
             }
         }
         GP_STAMP(t1);
-        // own (s, w): consumed after staging
-        // (loaded here, ahead of the staging copies, or -- GP_OWN_EARLY 0 -- with
-        // the node's lattice gathers, which keeps 12 fewer VGPRs live)
+        // own (s, w): loaded with the node's lattice gathers (ahead of the staging
+        // copies it kept 12 more VGPRs live and measured slower)
         double2 own[NPT];
-#pragma unroll
-        for (int k = 0; k < NPT; ++k) {
-            const uint32_t j = T + k * TPB + threadIdx.x;
-            if (GP_OWN_EARLY) own[k] = (j >= j0 && j < j1) ? swc[j] : make_double2(0.0, 1.0);
-        }
         // every staging copy of the tile in flight at once (LDS-DMA)
         const uint32_t b_rows = dma_stage_bytes(L.rows, a.nbc, (int64_t)j0 - H, (int64_t)j1 + H, a.ext_lo, a.ext_hi);
         uint32_t b_xm = 0, b_xp = 0;
@@ -601,10 +538,6 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
         // the tile's in-degrees, a nibble per node (512 bytes; the slab's arrays
         // cover whole tiles, ids outside the slab are 0)
         if (TOPO == IMP3D) dma_copy<DMA_ONCE>(L.ind, reinterpret_cast<const char*>(a.ind4 + T / 2), TILE / 2);
-#if GP_OWN_LDS
-        // own (s, w) of the tile (default cache policy: neighbouring tiles gather from these lines)
-        dma_copy(L.own + (j0 - T), reinterpret_cast<const char*>(swc + j0), (j1 - j0) * 16u);
-#endif
         GP_STAMP(t2);
         if (dyn && threadIdx.x == 0) L.qn[it & 1] = claim;
         __syncthreads();  // staging copies, in-edge bitmap and gathered messages retired
@@ -647,7 +580,6 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                     pf_lo = a.in_off[max(a.lo, nT)];
                     pf_hi = a.in_off[min(a.lo + a.nloc, nT + TILE)];
                     pf_tile = nti;
-                    pf_next = GP_PF_SRC && pf_hi - pf_lo <= cap;  // senders loaded after the directions
                 }
             }
         }
@@ -675,15 +607,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
             // lattice directions gathered from HBM / L2; with GP_ZDPP the j +- 1 ones
             // (z +- 1, or both line neighbours) are the neighbour lanes' own (s, w)
             constexpr uint32_t NDG = GP_ZDPP ? (TOPO == LINE ? 0u : 4u) : ND;
-            constexpr int NG = GP_NGROUP;  // nodes whose lattice gathers are in flight together
-            static_assert(NPT % NG == 0, "node groups");
-            // GP_DEFER_ST: slot k's next-round (s, w) is stored after slot k + 1's loads
-            // are issued.  Stored before them, it sat in the in-order vmcnt queue ahead of
-            // those loads, and the compiler's conservative vmcnt(0) before the next slot
-            // (merged loop paths) then waited for the store's completion too.
-            double2 st_v = make_double2(0.0, 0.0);
-            uint32_t st_j = 0;
-            bool st_ok = false;
+            constexpr int NG = 1;  // nodes per slot group (two groups in flight spilled 49 VGPRs)
 #pragma unroll
             for (int k0 = 0; k0 < NPT; k0 += NG) {
                 // phase A: node byte, present mask, lattice senders (from the staged
@@ -757,26 +681,14 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                     // unconditional (index clamped into the tile's valid range; invalid lanes'
                     // values are never used): a load under a branch made the compiler wait
                     // for it before issuing the lattice gathers
-#if GP_OWN_LDS
-                    own[k] = L.own[k * TPB + threadIdx.x];  // (invalid lanes: never used)
-#else
-                    if (!GP_OWN_EARLY) own[k] = swc[min(max(j, j0), j1 - 1u)];
-#endif
+                    own[k] = swc[min(max(j, j0), j1 - 1u)];
 #pragma unroll
                     for (uint32_t d = 0; d < NDG; ++d)
                         if ((GP_ABL_DIRS >> d) & 1) {  // ablation (timing only): no gathers in slot d
                             m[h][d] = make_double2(0.0, 0.0);
-                        } else if (GP_LMASK) {  // only lanes with a sender load (exec-masked gather)
-                            m[h][d] = make_double2(0.0, 0.0);
-                            if ((from >> d) & 1u) m[h][d] = ld_sw(swc + nbr<TOPO>(j, d, G));
                         } else {
                             m[h][d] = ld_sw(swc + ((from >> d) & 1u ? nbr<TOPO>(j, d, G) : a.ext_hi));
                         }
-                }
-                if (GP_DEFER_ST) {  // the previous slot's store, behind this slot's loads
-                    __builtin_amdgcn_sched_barrier(0);
-                    if (st_ok) st_stream(swn + st_j, st_v);
-                    st_ok = false;
                 }
                 // phase B: canonical fold (own half, lattice slots in slot order, random
                 // edges by ascending sender; every message contributes the sender's half),
@@ -787,7 +699,6 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                     const uint32_t jl = k * TPB + threadIdx.x;
                     const uint32_t j = T + jl;
                     const bool valid = j >= j0 && j < j1;
-                    uint32_t dir = DIR_NONE;
                     // j + 1 / j - 1: the neighbour lane's own (s, w) by DPP (all lanes active
                     // here), across the wave's ends from the values staged in L.zb; a load
                     // only where that lane's node is outside the tile's valid range
@@ -874,9 +785,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                                         sent = a.rtag[e] == r;
                                         if (sent) mi = a.rmsg[e];
                                     } else {
-                                        if (all_active && a.eb) {
-                                            sent = (a.eb[e >> 6] >> (e & 63u)) & 1ull;
-                                        } else if (all_active) {
+                                        if (all_active) {
                                             const uint32_t di = popc6(present_mask<IMP3D>(i, G)) + 1u;
                                             sent = uniform(a.k0, a.k1, S_PUSHSUM, i, r, di) == di - 1u;
                                         } else {
@@ -910,34 +819,16 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                                 active = true;
                             }
                         }
-                        if (GP_BATCH_DIR) {
-                            pend[k >> 1] |= (mask | (active && deg > 0 ? 64u : 0u) | ((flags >> 3) << 7)) << (16 * (k & 1));
-                        } else {
-                            if (active && deg > 0) dir = slot_to_dir_fast(mask, uniform(a.k0, a.k1, S_PUSHSUM, j, r + 1, deg));
-                            reinterpret_cast<uint8_t*>(L.out)[jl] = (uint8_t)(flags | dir);
-                        }
-                        if (GP_DEFER_ST) {
-                            st_v = make_double2(acc_s, acc_w);
-                            st_j = j;
-                            st_ok = true;
-                        } else {
-                            st_stream(swn + j, make_double2(acc_s, acc_w));
-                        }
-                    }
-                    if (TOPO == IMP3D && !GP_BATCH_DIR) {
-                        const unsigned long long bits = __ballot(valid && dir == DIR_RANDOM);
-                        if (lane == 0) {
-                            const int64_t wi = (int64_t)((T + k * TPB + (threadIdx.x & ~63u)) >> 6) - (int64_t)(a.lo >> 6);
-                            if (wi >= 0) a.rbn[wi] = bits;
-                        }
+                        // next-round direction drawn below, one Philox batch for the thread's nodes
+                        pend[k >> 1] |= (mask | (active && deg > 0 ? 64u : 0u) | ((flags >> 3) << 7)) << (16 * (k & 1));
+                        st_stream(swn + j, make_double2(acc_s, acc_w));
                     }
                 }
             }
-            if (GP_DEFER_ST && st_ok) st_stream(swn + st_j, st_v);
         }
         GP_STAMP(t4);
         // next-round directions of this thread's nodes: one Philox batch
-        if (GP_BATCH_DIR) {
+        {
             uint32_t node[NPT], x[NPT], y[NPT];
 #pragma unroll
             for (int k = 0; k < NPT; ++k) node[k] = T + k * TPB + threadIdx.x;
@@ -958,15 +849,6 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                         if (wi >= 0) a.rbn[wi] = bits;
                     }
                 }
-            }
-        }
-        // the next tile's senders (staged tiles only), while this tile's bytes leave
-        if (TOPO == IMP3D && pf_next) {
-            const uint32_t pcnt = pf_hi - pf_lo;
-#pragma unroll
-            for (int m = 0; m < FU; ++m) {
-                const uint32_t q = threadIdx.x + m * TPB;
-                raw[m] = q < pcnt ? __builtin_nontemporal_load(srcp + pf_lo + q) : 0u;
             }
         }
         __syncthreads();
@@ -1060,41 +942,6 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t 
         } else {
             if (alerts) atomicAdd(&ctl->round_alerts, (unsigned long long)alerts);
             if (newly) atomicAdd(&ctl->round_active, (unsigned long long)newly);
-        }
-    }
-}
-
-// ---------------------------------------------------------------- push-sum, edge decisions (Imp3D)
-// Steady-state in-edge decisions of round r for one rank: bit e of `eb` = "the
-// sender of in-edge e (receiver-sorted CSR) uses its random edge in round r",
-// i.e. the sender's own Philox draw U(deg) == deg - 1 (SRS v1 B.4,
-// Program.fs:125-128).  One dense pass over the in-lists (coalesced sender
-// loads, 4 interleaved Philox chains per lane, one ballot word per 64 edges),
-// so the round kernel's in-edge pass reads bits instead of redrawing on its
-// latency-critical path.  Exits at once while some node is inactive (the round
-// kernel then reads the ballot bitmap of the senders' directions).
-template <bool PACKED>
-__global__ __launch_bounds__(256) void k_edge_decide(const uint32_t* __restrict__ src, uint32_t nedges,
-                                                     uint64_t* __restrict__ eb, Geom G, uint32_t k0, uint32_t k1,
-                                                     const Ctl* ctl, uint32_t r) {
-    if (ld_agent(&ctl->done) || !ld_agent(&ctl->all_active)) return;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = (blockIdx.x * 256u + threadIdx.x) >> 6, nwaves = gridDim.x * 4u;
-    for (uint64_t base = (uint64_t)wave * 256u; base < nedges; base += (uint64_t)nwaves * 256u) {
-        uint32_t raw[4], node[4], x[4], y[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint64_t e = base + k * 64u + lane;
-            raw[k] = e < nedges ? __builtin_nontemporal_load(src + e) : 0u;
-            node[k] = PACKED ? raw[k] & 0x3FFFFFFFu : raw[k];
-        }
-        philox2_batch<4>(node, r, S_PUSHSUM, k0, k1, x, y);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint64_t e = base + k * 64u + lane;
-            const uint32_t di = PACKED ? (raw[k] >> 30) + 4u : popc6(present_mask<IMP3D>(node[k], G)) + 1u;
-            const unsigned long long bal = __ballot(e < nedges && uniform_from(x[k], y[k], di) == di - 1u);
-            if (lane == (uint32_t)k) eb[(base >> 6) + k] = bal;
         }
     }
 }
@@ -1310,7 +1157,6 @@ RoundArgs make_round_args(const DevState& S, uint32_t round) {
     a.stage_cap = S.tile_stage_cap;
     a.wx = S.tile_wx;
     a.fuse = S.fuse_finalize;
-    a.eb = S.eb;
     a.wt = S.wtiles;
     for (int c = 0; c <= 8; ++c) a.wo[c] = S.woff[c];
     a.tq = S.tq + (round & 1) * 8 * TQ_STRIDE;
@@ -1368,16 +1214,6 @@ hipError_t launch_round_tile(const DevState& S, uint32_t round, int grid, hipStr
     const RoundArgs a = make_round_args(S, round);
     const dim3 g(grid), b(TPB);
     const bool remote = S.rtag != nullptr;  // Imp3D slabs of a multi-rank run
-    if (S.alg == PUSHSUM && S.topo == IMP3D && S.eb) {  // this round's edge decisions first
-        const uint32_t* src = S.in_srcd ? S.in_srcd : S.in_src;
-        const dim3 ge(std::min<uint32_t>(4096u, (S.nedges + 1023u) / 1024u + 1u));
-        if (S.in_srcd)
-            hipLaunchKernelGGL((k_edge_decide<true>), ge, dim3(256), 0, st, src, S.nedges, S.eb, S.G, S.k0, S.k1, S.ctl,
-                               round);
-        else
-            hipLaunchKernelGGL((k_edge_decide<false>), ge, dim3(256), 0, st, src, S.nedges, S.eb, S.G, S.k0, S.k1,
-                               S.ctl, round);
-    }
     if (S.alg == PUSHSUM && S.topo == IMP3D && !S.ind4) return hipErrorInvalidValue;
     if (S.alg == PUSHSUM) {
         switch (S.topo) {

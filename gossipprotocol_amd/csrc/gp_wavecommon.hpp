@@ -1,5 +1,5 @@
-// gp_wavecommon.hpp -- helpers shared by the wave-autonomous round kernels
-// (gp_wave.hip, gp_col.hip).  Included by those translation units only.
+// gp_wavecommon.hpp -- helpers shared by the column-march round kernels
+// (gp_col.hip, gp_pscol.hip).  Included by those translation units only.
 #pragma once
 
 #include "gp_internal.hpp"
@@ -8,17 +8,6 @@ namespace gp {
 namespace wk {
 
 constexpr int WPB = BULK_THREADS / 64;  // waves per 256-thread block
-constexpr int EU = 5;                   // in-edge sweeps issued together (mean in-degree 1 -> 256 edges)
-constexpr uint32_t ECAP = 384;          // staged in-edge codes per wave work unit (mean 256, sd 16)
-constexpr uint32_t MCAP = 128;          // parked random-edge messages per work unit (mean ~37)
-constexpr uint32_t CODE_NONE = 0xFFFFFFFFu;
-constexpr uint32_t CODE_GLOBAL = 0x80000000u;
-
-// Wave-private LDS: in-edge decisions and the parked random-edge messages.
-struct alignas(16) WaveLds {
-    double2 msg[MCAP];
-    uint32_t code[ECAP];
-};
 
 template <typename T>
 __device__ __forceinline__ T ld_agent(const T* p) {

@@ -41,7 +41,7 @@ CASES = [  # (num_nodes, topology, algorithm, seed, rounds, checkpoint, ranks)
 ]
 
 
-@pytest.mark.parametrize("kernel", ["default", "tile", "wave", "col"])
+@pytest.mark.parametrize("kernel", ["default", "tile", "col"])
 @pytest.mark.parametrize("n,topo,alg,seed,rounds,chk,ranks", CASES, ids=lambda v: str(v))
 def test_virtual_ranks_parity(kernel, n, topo, alg, seed, rounds, chk, ranks, monkeypatch):
     """default: the product library's own kernel choice; the others force a

@@ -190,10 +190,10 @@ KERNEL_CASES = [  # (num_nodes, topology, algorithm, seed, rounds, checkpoint, x
 ]
 
 
-@pytest.mark.parametrize("kernel", ["wave", "col", "tile"])
+@pytest.mark.parametrize("kernel", ["col", "tile"])
 @pytest.mark.parametrize("n,topo,alg,seed,rounds,chk,xsegs", KERNEL_CASES, ids=lambda v: str(v))
 def test_kernel_variant_parity(kernel, n, topo, alg, seed, rounds, chk, xsegs, monkeypatch):
-    """Every round-kernel variant (chunk / column march / tiled; experiments build,
+    """Every round-kernel variant (column march / tiled; experiments build,
     GP_KERNEL) bit-exact vs the oracle, the column march also with its
     x-segmentation forced."""
     monkeypatch.setenv("GP_KERNEL", kernel)
@@ -261,7 +261,7 @@ def test_nibble_wide_tile_fallback_parity(wide_at, monkeypatch):
     sim.close()
 
 
-@pytest.mark.parametrize("kernel", ["col", "tile", "wave"])
+@pytest.mark.parametrize("kernel", ["col", "tile"])
 def test_seed_random_edge_round0(kernel, monkeypatch):
     """Many seeds, so that several seed nodes send their round-0 rumour on the random
     edge: the round-0 random-edge bitmap (k_col_rbits_init / k_rbits_init) must carry

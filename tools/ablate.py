@@ -22,26 +22,18 @@ VARIANTS = {  # name -> extra -D flags for gp_round.hip
     "base": [],
     "stamps": ["-DGP_STAMPS=1"],
     "nofma": ["-DGP_FMA_FOLD=0"],
-    "lmask": ["-DGP_LMASK=1"],
     "noz": ["-DGP_ABL_DIRS=48"],
     "nox": ["-DGP_ABL_DIRS=3"],
     "noy": ["-DGP_ABL_DIRS=12"],
     "nolat": ["-DGP_ABL_DIRS=63"],
-    "ng2": ["-DGP_NGROUP=2"],
     "n2m6": ["-DGP_NPT=2", "-DGP_MINB=6"],
     "n2m5": ["-DGP_NPT=2", "-DGP_MINB=5"],
-    "n2m6g2": ["-DGP_NPT=2", "-DGP_MINB=6", "-DGP_NGROUP=2"],
-    "ng2m4": ["-DGP_NGROUP=2", "-DGP_MINB=4"],
-    "ng4m4": ["-DGP_NGROUP=4", "-DGP_MINB=4"],
-    "ng1m4": ["-DGP_MINB=4"],
     "minb4": ["-DGP_MINB=4"],
     "minb6": ["-DGP_MINB=6"],
     "npt2": ["-DGP_NPT=2"],
     "plainld": ["-DGP_NT_LOADS=0"],
     "plainst": ["-DGP_NT_STORES=0"],
-    "ownearly": ["-DGP_OWN_EARLY=1"],
     "nozdpp": ["-DGP_ZDPP=0"],
-    "nozdpp_oe": ["-DGP_ZDPP=0", "-DGP_OWN_EARLY=1"],
     "t512m6": ["-DGP_TPB=512", "-DGP_NPT=2", "-DGP_MINB=6"],
     "t1024m8": ["-DGP_TPB=1024", "-DGP_NPT=1", "-DGP_MINB=8"],
 }
