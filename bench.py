@@ -11,7 +11,7 @@ every node is active (steady state: every node sends a message each round),
 then W warmup rounds; convergence is never reached inside the timed window.
 
 One JSON line on stdout (rank 0).  `roofline` is measured live: HIP events on
-the library's stream bracket every round kernel (k_pushsum_round<IMP3D>); its
+the library's stream bracket every round kernel (k_ps_col<IMP3D> at this size); its
 algorithmic bytes per node-round are DESIGN.md §4's figure.  `traffic` is
 measured in the same run: before the bench, the workload is re-run as a child
 under three rocprofv3 --pmc passes and the round kernel's HBM bytes are read
@@ -126,7 +126,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--converge", action="store_true", help="also run a fresh simulation to convergence")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 HBM-traffic passes")
-    ap.add_argument("--traffic-kernel", default="k_ps_tile", help="round-kernel name substring in the counters")
+    ap.add_argument("--traffic-kernel", default="auto",
+                    help="round-kernel name substring in the counters (auto: the kernel that writes the most)")
     ap.add_argument("--traffic-timeout", type=float, default=240.0)
     args = ap.parse_args()
 

@@ -132,6 +132,7 @@ struct gp_sim {
     std::vector<hipEvent_t> ev;
     double kernel_ms = 0.0;
     int64_t launches = 0;
+    bool force_tile = false;  // push-sum lattice: the column kernel's capacities were exceeded (build_imp3d)
 };
 
 namespace {
@@ -317,7 +318,8 @@ int alloc_slab(gp_sim* s, Slab& sl, int r) {
             return rc;
         }
     }
-    if (S.topo == IMP3D) {
+    // random-edge bitmaps; not needed by one-rank gossip on the column kernel (push form)
+    if (S.topo == IMP3D && !(S.alg == GOSSIP && S.kernel == KERNEL_COL && W == 1)) {
         S.rbits_words = S.kernel == KERNEL_COL ? col_rbits_words(S.nloc / S.G.g2, S.G.g)
                                                : rbits_words_for(S.lo, S.nloc);
         if ((rc = dev_alloc_t(s, &S.rbits[0], S.rbits_words)) || (rc = dev_alloc_t(s, &S.rbits[1], S.rbits_words)))
@@ -327,39 +329,73 @@ int alloc_slab(gp_sim* s, Slab& sl, int r) {
 }
 
 // Imp3D: draw rnd[] for every node (Program.fs:258-260), then a stable sort of
-// (rnd[i], i) by rnd gives every receiver's senders in ascending id order and
-// in_off = exclusive scan of the in-degrees.  Every rank builds the global
-// order (it is deterministic) and keeps its receivers' slice; with several
-// ranks, each local sender also learns the position of its message in the
-// destination's in-edge array (pos).
+// (key(rnd[i]), i) by key gives every receiver's senders in ascending id order,
+// and the exclusive scan of the per-key in-degrees the CSR offsets.  The key is
+// the receiver id (tile / gossip kernels: in_off, in_src in id order) or, for
+// the push-sum column kernel, its patch key (gp_pscol.hip: one contiguous edge
+// range per plane of a patch, pc_soff / pc_src / pc_ind4).  Every rank builds
+// the global order (it is deterministic; ranks own consecutive key ranges) and
+// keeps its receivers' slice; with several ranks, each local sender also learns
+// the position of its message in the destination's in-edge array (pos).
+// Returns GP_ERETRY_TILE when the patch-order lists exceed the column kernel's
+// static capacities (a receiver with >= 15 in-edges, or a step with more
+// in-edges than it stages): the caller rebuilds with the tile kernel.
+constexpr int GP_ERETRY_TILE = -100;
+
 int build_imp3d(gp_sim* s) {
     const uint32_t P = (uint32_t)s->P;
     const int W = s->world;
     DevState& S0 = s->slab[0].S;
+    const bool pscol = S0.alg == PUSHSUM && S0.kernel == KERNEL_COL;
     Scratch tmp_mem;  // setup temporaries, freed on every exit path
     uint32_t *rnd_all = nullptr, *iota = nullptr, *keys_sorted = nullptr, *src_sorted = nullptr, *counts = nullptr,
-             *off_all = nullptr, *inv = nullptr;
+             *off_all = nullptr, *inv = nullptr, *key_all = nullptr;
+    // key space: receiver ids, or patch keys (planes x patch rows x z-segments x 64)
+    PcKeyPlan kp{};
+    uint64_t nkeys = P;
+    if (pscol) {
+        const uint32_t rows = pscol_patch_rows(), g = (uint32_t)s->g;
+        const uint64_t per_plane = (uint64_t)((g + rows - 1) / rows) * ((g + 63) / 64) * rows * 64;
+        kp.W = W;
+        kp.zs = (g + 63) / 64;
+        uint64_t kb = 0;
+        for (int w = 0; w <= W; ++w) {
+            kp.x_lo[w] = (uint32_t)(s->bounds[w] / (s->g * s->g));
+            kp.kbase[w] = (uint32_t)kb;
+            if (w < W) kb += per_plane * ((s->bounds[w + 1] - s->bounds[w]) / (s->g * s->g));
+        }
+        nkeys = kb;
+        if (nkeys >= 0xFFFFFFFFull) {
+            set_err("internal: patch key space of %llu keys", (unsigned long long)nkeys);
+            return GP_ERETRY_TILE;
+        }
+    }
     HIP_TRY(tmp_mem.alloc(&rnd_all, P));
     HIP_TRY(tmp_mem.alloc(&iota, P));
     HIP_TRY(tmp_mem.alloc(&keys_sorted, P));
     HIP_TRY(tmp_mem.alloc(&src_sorted, P));
-    HIP_TRY(tmp_mem.alloc(&counts, (size_t)P + 1));
-    HIP_TRY(tmp_mem.alloc(&off_all, (size_t)P + 1));
+    HIP_TRY(tmp_mem.alloc(&counts, (size_t)nkeys + 1));
+    HIP_TRY(tmp_mem.alloc(&off_all, (size_t)nkeys + 1));
     HIP_TRY(launch_topo_rnd_range(S0.k0, S0.k1, P, 0, P, rnd_all, s->grid, s->stream));
     HIP_TRY(launch_iota(iota, P, s->grid, s->stream));
-    const uint32_t bits = bits_for(P > 1 ? P - 2 : 0);
+    key_all = rnd_all;
+    if (pscol) {
+        HIP_TRY(tmp_mem.alloc(&key_all, P));
+        HIP_TRY(launch_pc_keys(rnd_all, P, key_all, S0.G, kp, s->grid, s->stream));
+    }
+    const uint32_t bits = bits_for(nkeys > 1 ? nkeys - 1 : 0);
     size_t tmp_bytes = 0;
-    HIP_TRY(sort_pairs(nullptr, tmp_bytes, rnd_all, keys_sorted, iota, src_sorted, P, bits, s->stream));
+    HIP_TRY(sort_pairs(nullptr, tmp_bytes, key_all, keys_sorted, iota, src_sorted, P, bits, s->stream));
     uint8_t* tmp = nullptr;
     HIP_TRY(tmp_mem.alloc(&tmp, tmp_bytes ? tmp_bytes : 4));
-    HIP_TRY(sort_pairs(tmp, tmp_bytes, rnd_all, keys_sorted, iota, src_sorted, P, bits, s->stream));
-    HIP_TRY(hipMemsetAsync(counts, 0, sizeof(uint32_t) * ((size_t)P + 1), s->stream));
-    HIP_TRY(launch_histogram(rnd_all, P, counts, s->grid, s->stream));
+    HIP_TRY(sort_pairs(tmp, tmp_bytes, key_all, keys_sorted, iota, src_sorted, P, bits, s->stream));
+    HIP_TRY(hipMemsetAsync(counts, 0, sizeof(uint32_t) * ((size_t)nkeys + 1), s->stream));
+    HIP_TRY(launch_histogram(key_all, P, counts, s->grid, s->stream));
     size_t scan_bytes = 0;
-    HIP_TRY(exclusive_scan_u32(nullptr, scan_bytes, counts, off_all, P + 1, s->stream));
+    HIP_TRY(exclusive_scan_u32(nullptr, scan_bytes, counts, off_all, (uint32_t)nkeys + 1, s->stream));
     uint8_t* scan_tmp = nullptr;
     HIP_TRY(tmp_mem.alloc(&scan_tmp, scan_bytes ? scan_bytes : 4));
-    HIP_TRY(exclusive_scan_u32(scan_tmp, scan_bytes, counts, off_all, P + 1, s->stream));
+    HIP_TRY(exclusive_scan_u32(scan_tmp, scan_bytes, counts, off_all, (uint32_t)nkeys + 1, s->stream));
     if (W > 1) {
         HIP_TRY(tmp_mem.alloc(&inv, P));
         HIP_TRY(launch_inverse(src_sorted, P, inv, s->grid, s->stream));
@@ -367,8 +403,8 @@ int build_imp3d(gp_sim* s) {
     // first global edge of every rank
     std::vector<uint32_t> edge0(W + 1);
     for (int w = 0; w <= W; ++w)
-        HIP_TRY(hipMemcpyAsync(&edge0[w], off_all + s->bounds[w], sizeof(uint32_t), hipMemcpyDeviceToHost,
-                               s->stream));
+        HIP_TRY(hipMemcpyAsync(&edge0[w], off_all + (pscol ? kp.kbase[w] : s->bounds[w]), sizeof(uint32_t),
+                               hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
     int rc;
     for (Slab& sl : s->slab) {
@@ -376,17 +412,47 @@ int build_imp3d(gp_sim* s) {
         const int r = sl.rank;
         const uint32_t ne = edge0[r + 1] - edge0[r];
         sl.nedges = ne;
-        // in-lists padded by 4 words: the tile kernels stage them with 16-byte LDS-DMA
-        if ((rc = dev_alloc_t(s, &S.rnd, S.nloc)) || (rc = dev_alloc_t(s, &S.in_off, (size_t)S.nloc + 1 + 4)) ||
-            (rc = dev_alloc_t(s, &S.in_src, (size_t)ne + 4)))
-            return rc;
+        S.nedges = ne;
+        if ((rc = dev_alloc_t(s, &S.rnd, S.nloc))) return rc;
         HIP_TRY(hipMemcpyAsync(S.rnd, rnd_all + S.lo, sizeof(uint32_t) * S.nloc, hipMemcpyDeviceToDevice, s->stream));
-        HIP_TRY(hipMemcpyAsync(S.in_off, off_all + S.lo, sizeof(uint32_t) * ((size_t)S.nloc + 1),
-                               hipMemcpyDeviceToDevice, s->stream));
-        HIP_TRY(launch_sub(S.in_off, S.nloc + 1, edge0[r], s->grid, s->stream));
-        if (ne)
-            HIP_TRY(hipMemcpyAsync(S.in_src, src_sorted + edge0[r], sizeof(uint32_t) * ne, hipMemcpyDeviceToDevice,
-                                   s->stream));
+        if (pscol) {
+            // patch-order lists (gp_pscol.hip); the senders carry deg - 4 in bits 30-31
+            const uint32_t nsteps = (uint32_t)((kp.kbase[r + 1] - kp.kbase[r]) / pscol_step_receivers());
+            S.pc_nsteps = nsteps;
+            uint32_t* stat = nullptr;
+            if ((rc = dev_alloc_t(s, &S.pc_src, (size_t)ne + 8)) ||
+                (rc = dev_alloc_t(s, &S.pc_soff, (size_t)nsteps + 2)) ||
+                (rc = dev_alloc_t(s, &S.pc_ind4, (size_t)nsteps * (pscol_step_receivers() / 2) + 64)))
+                return rc;
+            HIP_TRY(tmp_mem.alloc(&stat, 2));
+            HIP_TRY(hipMemsetAsync(stat, 0, sizeof(uint32_t) * 2, s->stream));
+            HIP_TRY(hipMemsetAsync(S.pc_src, 0, sizeof(uint32_t) * ((size_t)ne + 8), s->stream));
+            if (ne) HIP_TRY(launch_pack_src_deg(src_sorted + edge0[r], S.pc_src, ne, S.G, s->grid, s->stream));
+            HIP_TRY(launch_pc_slab(off_all, counts, kp.kbase[r], nsteps, edge0[r], S.pc_soff, S.pc_ind4, stat,
+                                   s->grid, s->stream));
+            uint32_t hs[2] = {0, 0};
+            HIP_TRY(hipMemcpyAsync(hs, stat, sizeof hs, hipMemcpyDeviceToHost, s->stream));
+            HIP_TRY(hipStreamSynchronize(s->stream));
+            uint32_t deg_cap = 14;
+#ifdef GP_EXPERIMENTS
+            if (const char* e = std::getenv("GP_PSCOL_DEGCAP")) deg_cap = (uint32_t)std::atoi(e);  // tests: force the fallback
+#endif
+            if (hs[0] > deg_cap || hs[1] > pscol_step_capacity()) {
+                set_err("push-sum column kernel: in-degree %u / step in-edges %u above its capacity", hs[0], hs[1]);
+                return GP_ERETRY_TILE;
+            }
+        } else {
+            // in-lists padded by 4 words: the tile kernels stage them with 16-byte LDS-DMA
+            if ((rc = dev_alloc_t(s, &S.in_off, (size_t)S.nloc + 1 + 4)) ||
+                (rc = dev_alloc_t(s, &S.in_src, (size_t)ne + 4)))
+                return rc;
+            HIP_TRY(hipMemcpyAsync(S.in_off, off_all + S.lo, sizeof(uint32_t) * ((size_t)S.nloc + 1),
+                                   hipMemcpyDeviceToDevice, s->stream));
+            HIP_TRY(launch_sub(S.in_off, S.nloc + 1, edge0[r], s->grid, s->stream));
+            if (ne)
+                HIP_TRY(hipMemcpyAsync(S.in_src, src_sorted + edge0[r], sizeof(uint32_t) * ne,
+                                       hipMemcpyDeviceToDevice, s->stream));
+        }
         S.in_srcd = nullptr;
         bool pack = true;
 #ifdef GP_EXPERIMENTS
@@ -405,7 +471,6 @@ int build_imp3d(gp_sim* s) {
 #endif
             HIP_TRY(launch_pack_ind4(S, wide_at, s->grid, s->stream));
         }
-        S.nedges = ne;
         if (W > 1) {
             if ((rc = dev_alloc_t(s, &sl.pos, S.nloc)) || (rc = dev_alloc_t(s, &S.rtag, ne)) ||
                 (S.alg == PUSHSUM && (rc = dev_alloc_t(s, &S.rmsg, ne))))
@@ -815,10 +880,13 @@ double alg_bytes(const gp_sim* s) {
         // (gp_fullbin.hip, range binning)
         return 1.0 + 1.0 + 16.0 + 20.0 + 4.0 + 40.0 + 20.0 + 32.0 + 2.0;
     }
-    // gossip: counter r+w 8, direction byte r+w 2 (+ Imp3D in-list 8, and with the
-    // separate random-edge delivery pass of the column kernel its per-node count
-    // written and read, 2 + 2)
-    if (S.topo == IMP3D) return S.rq[0] ? 22.0 : S.rcnt ? 22.0 : 18.0;
+    // gossip: counter r+w 8, direction byte r+w 2; Imp3D:
+    //   one rank, push form (k_gossip_col counts random-edge sends at their targets a
+    //   round ahead): rnd 4 + delivery count read 4, its zeroing where non-zero and the
+    //   senders' atomic increments (~1/7 of nodes each, 4 B) -> 18 + 8/7;
+    //   several ranks (k_gossip_redges + k_gossip_col): in-list 8, per-node count w+r 4;
+    //   tile kernel: in-list 8
+    if (S.topo == IMP3D) return S.rq[0] ? 18.0 + 8.0 / 7.0 : S.rcnt ? 22.0 : 18.0;
     if (S.topo != FULL) return 10.0;
     return 4.0 + 8.0 + 8.0 + 8.0;  // send: c + atomic RMW; recv: inc r+w, c r+w
 }
@@ -834,30 +902,37 @@ void choose_kernel(gp_sim* s, int64_t nloc_max, int& kernel, uint32_t& col_xsegs
     // 64 workgroups per CU: measured best for the tiled round kernels (tools/ablate.py:
     // 2048 -> 27.5, 8192 -> 22.1, 16384 -> 21.2 ms/round at P = 1e9)
     int64_t cap = (int64_t)prop.multiProcessorCount * 64;
-    // (measured, profiles/r01: push-sum -> tiled; gossip on a large lattice -> column march)
+    // (measured: gossip on a large lattice -> column march, profiles/r01; push-sum on
+    // a large lattice -> column march, profiles/r03; small lattices and line -> tiled)
     kernel = KERNEL_TILE;
     const bool lattice = cfg->topology == GP_3D || cfg->topology == GP_IMP3D;
-    if (lattice && cfg->algorithm == GP_GOSSIP && g >= 200) kernel = KERNEL_COL;
+    const bool push = cfg->algorithm == GP_PUSHSUM;
+    // push-sum column kernel: Imp3D senders carry their degree in 2 bits (P <= 2^30)
+    const bool pscol_ok = !s->force_tile && (cfg->topology == GP_3D || s->P <= (1ll << 30));
+    if (lattice && g >= 200 && (!push || pscol_ok)) kernel = KERNEL_COL;
 #ifdef GP_EXPERIMENTS
     if (const char* e = std::getenv("GP_KERNEL")) {
         if (!std::strcmp(e, "tile")) kernel = KERNEL_TILE;
-        else if (!std::strcmp(e, "col") && lattice && cfg->algorithm == GP_GOSSIP) kernel = KERNEL_COL;
+        else if (!std::strcmp(e, "col") && lattice && (!push || pscol_ok)) kernel = KERNEL_COL;
     }
 #endif
     col_xsegs = 1;
     if (cfg->topology != GP_FULL && kernel != KERNEL_TILE) {
-        // exactly the resident grid (a persistent sweep), a multiple of the 8 XCDs
-        const int bpc = col_blocks_per_cu(cfg->topology, cfg->algorithm);
+        // gossip: exactly the resident grid (a persistent sweep), a multiple of the 8 XCDs;
+        // push-sum: one block per work item (gp_pscol.hip pscol_grid)
+        const bool remote = s->world > 1 && cfg->topology == GP_IMP3D;
+        const int bpc = push ? pscol_blocks_per_cu(cfg->topology == GP_3D ? GRID3D : IMP3D, remote)
+                             : col_blocks_per_cu(cfg->topology, cfg->algorithm);
         cap = (int64_t)prop.multiProcessorCount * bpc;
-        if (kernel == KERNEL_COL) {
-            // x segments per patch: enough work items for every resident wave, >= 16 planes each
-            const int64_t patches = ((g + 63) / 64) * ((g + 3) / 4);
-            const int64_t waves = cap * (BULK_THREADS / 64);
-            const int64_t planes = std::max<int64_t>(1, g / s->world);
-            int64_t xs = std::max<int64_t>(1, waves / std::max<int64_t>(1, patches));
-            xs = std::min<int64_t>(xs, std::max<int64_t>(1, planes / 16));
-            col_xsegs = (uint32_t)xs;
-        }
+        // x segments per patch: enough work items for every resident wave (gossip) or
+        // workgroup (push-sum), >= 16 planes each
+        const int64_t rows = push ? pscol_patch_rows() : 4;
+        const int64_t patches = ((g + 63) / 64) * ((g + rows - 1) / rows);
+        const int64_t slots = push ? cap : cap * (BULK_THREADS / 64);
+        const int64_t planes = std::max<int64_t>(1, g / s->world);
+        int64_t xs = std::max<int64_t>(1, slots / std::max<int64_t>(1, patches));
+        xs = std::min<int64_t>(xs, std::max<int64_t>(1, planes / 16));
+        col_xsegs = (uint32_t)xs;
     }
     if (kernel == KERNEL_TILE)  // 1024-node tiles (+1: a slab may start mid-tile), a multiple of the 8 XCDs
         blocks = ((nloc_max + 1023) / 1024 + 1 + 7) / 8 * 8;
@@ -913,7 +988,7 @@ int build_sim(gp_sim* s) {
         // only -- serialises ~16k returning atomics per round: measured 1.93 vs
         // 0.40 ms/round at P = 2.7e7, profiles/r02/round_close.txt)
         sl.S.fuse_finalize = (s->mode == MODE_SINGLE && s->cfg.algorithm == GP_PUSHSUM &&
-                              s->cfg.topology != GP_FULL && kernel == KERNEL_TILE) ? 2u : 0u;
+                              s->cfg.topology != GP_FULL) ? 2u : 0u;
 #ifdef GP_EXPERIMENTS
         if (const char* e = std::getenv("GP_FUSE")) sl.S.fuse_finalize = sl.S.fuse_finalize ? (uint32_t)(e[0] - '0') : 0u;
         if (const char* e = std::getenv("GP_STAGE_CAP")) sl.S.tile_stage_cap = (uint32_t)std::max(0, std::atoi(e));
@@ -1005,7 +1080,29 @@ int create_common(const gp_config* cfg, int mode, int world, int rank, const uin
             return GP_ENCCL;
         }
     }
-    if ((rc = build_sim(s))) {
+    if ((rc = build_sim(s)) == GP_ERETRY_TILE) {
+        // the push-sum column kernel cannot take this topology (build_imp3d): the tile kernel
+        gp_sim* t = new gp_sim();
+        t->cfg = s->cfg;
+        t->device = s->device;
+        t->P = s->P;
+        t->T = s->T;
+        t->g = s->g;
+        t->mode = s->mode;
+        t->world = s->world;
+        t->rank = s->rank;
+        t->timing = s->timing;
+        t->stream = s->stream;
+        t->comm = s->comm;
+        t->force_tile = true;
+        (void)hipStreamSynchronize(s->stream);
+        s->stream = nullptr;
+        s->comm = nullptr;
+        gp_destroy(s);
+        s = t;
+        rc = build_sim(s);
+    }
+    if (rc) {
         const std::string msg = g_err;
         gp_destroy(s);
         g_err = msg;

@@ -219,7 +219,7 @@ __global__ __launch_bounds__(BULK_THREADS, GP_COL_MINW(TOPO)) void k_gossip_col(
                     if (lrc[k]) a.rq_cur[j - lo] = 0u;
                     if (dir == DIR_RANDOM) atomicAdd(&a.rq_next[lrd[k] - lo], 1u);
                 }
-                if (TOPO == IMP3D) {
+                if (TOPO == IMP3D && !push) {  // several ranks: the delivery pass reads these bits
                     const unsigned long long bits = __ballot(rv[k] && dir == DIR_RANDOM);
                     if (lane == 0 && y0 + k < g) a.rbn[col_rb_word(a, x, y0 + k, zs * 64)] = bits;
                 }
@@ -367,8 +367,9 @@ __global__ __launch_bounds__(BULK_THREADS) void k_col_rbits_init(WaveArgs a, con
         sw = col_rb_word(a, x, y, z);
         sbit = 1ull << (z & 63);
     }
-    for (uint32_t w = blockIdx.x * BULK_THREADS + threadIdx.x; w < words; w += gridDim.x * BULK_THREADS)
-        a.rbn[w] = w == sw ? sbit : 0ull;
+    if (a.rbn)  // (gossip, one rank, push form: no bitmap)
+        for (uint32_t w = blockIdx.x * BULK_THREADS + threadIdx.x; w < words; w += gridDim.x * BULK_THREADS)
+            a.rbn[w] = w == sw ? sbit : 0ull;
     // one rank, push form: the seed's round-0 send on its random edge, counted at the target
     if (a.rq_cur && sbit && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&a.rq_cur[a.rnd[i - a.lo] - a.lo], 1u);
 }

@@ -623,3 +623,133 @@ int or_read_state(const or_sim* s, int64_t first, int64_t count, int32_t* c,
     }
     return 0;
 }
+
+/* ---------------------------------------------------------------- sampled receivers */
+/* One push-sum round r for a sample of receivers, from a full round-r state
+ * supplied by the caller (e.g. read back from the HIP path): the same rules as
+ * pushsum_round (SRS v1 B.4, restating MainPushSum, Program.fs:101-131), pulled
+ * per receiver instead of pushed per sender, so that the product's round can be
+ * checked at populations the whole-network oracle cannot hold (P = 1e9):
+ *   - every lattice neighbour n of receiver j (j's slot order, Program.fs:246-257)
+ *     sends to j iff it is active with degree > 0 and its round-r draw
+ *     U_PUSHSUM(n, r, deg n) picks the slot whose target is j;
+ *   - Imp3D random in-senders of j = every i with rnd[i] == j (Program.fs:258-260,
+ *     rnd recomputed here from the TOPO stream, not taken from the product), each
+ *     sending iff its draw picks its random slot; folded by ascending i;
+ *   - own half, the fold, the ratio test and the flags as pushsum_round.
+ * Inputs s, w, flags (bit0 active, bit1 converged, bits2-3 count) hold all P
+ * nodes at the start of round r; ids are distinct receivers.  Outputs per id.
+ * Returns the number of sampled receivers that converge in this round, or -1. */
+int64_t or_pushsum_receivers(int topology, int64_t num_nodes, uint64_t seed, uint32_t round,
+                             const double* sv, const double* wv, const uint8_t* flags,
+                             const int64_t* ids, int64_t nids, double* s_out, double* w_out,
+                             uint8_t* flags_out, int threads) {
+    or_sim c;
+    memset(&c, 0, sizeof c);
+    int64_t P, T, g;
+    if (topology == OR_FULL || or_resolve(num_nodes, topology, &P, &T, &g)) return -1;
+    c.topo = topology; c.alg = OR_PUSHSUM; c.threads = threads; c.seed = seed;
+    c.P = P; c.T = T; c.g = g;
+    const int nt = nthreads(&c);
+    int32_t* pos = (int32_t*)malloc(sizeof(int32_t) * P);
+    int64_t* roff = (int64_t*)calloc(nids + 1, sizeof(int64_t));
+    int64_t* rcur = (int64_t*)calloc(nids + 1, sizeof(int64_t));
+    uint32_t* rsrc = NULL;
+    if (!pos || !roff || !rcur) { free(pos); free(roff); free(rcur); return -1; }
+    #pragma omp parallel for num_threads(nt) schedule(static)
+    for (int64_t i = 0; i < P; ++i) pos[i] = -1;
+    for (int64_t q = 0; q < nids; ++q) {
+        if (ids[q] < 0 || ids[q] >= P || pos[ids[q]] >= 0) { free(pos); free(roff); free(rcur); return -1; }
+        pos[ids[q]] = (int32_t)q;
+    }
+    if (topology == OR_IMP3D) {
+        c.rnd = (uint32_t*)malloc(sizeof(uint32_t) * P);
+        if (!c.rnd) { free(pos); free(roff); free(rcur); return -1; }
+        #pragma omp parallel for num_threads(nt) schedule(static)
+        for (int64_t i = 0; i < P; ++i)
+            c.rnd[i] = or_uniform(seed, OR_STREAM_TOPO, (uint64_t)i, 0, (uint32_t)(P - 1));
+        /* random in-senders of the sampled receivers, grouped per receiver */
+        #pragma omp parallel for num_threads(nt) schedule(static)
+        for (int64_t i = 0; i < P; ++i) {
+            int32_t q = pos[c.rnd[i]];
+            if (q >= 0) {
+                #pragma omp atomic
+                roff[q + 1] += 1;
+            }
+        }
+        for (int64_t q = 0; q < nids; ++q) roff[q + 1] += roff[q];
+        memcpy(rcur, roff, sizeof(int64_t) * (nids + 1));
+        rsrc = (uint32_t*)malloc(sizeof(uint32_t) * (roff[nids] + 1));
+        if (!rsrc) { free(c.rnd); free(pos); free(roff); free(rcur); return -1; }
+        #pragma omp parallel for num_threads(nt) schedule(static)
+        for (int64_t i = 0; i < P; ++i) {
+            int32_t q = pos[c.rnd[i]];
+            if (q >= 0) {
+                int64_t at;
+                #pragma omp atomic capture
+                at = rcur[q]++;
+                rsrc[at] = (uint32_t)i;
+            }
+        }
+    }
+    int64_t alerts = 0;
+    #pragma omp parallel for num_threads(nt) schedule(dynamic, 256) reduction(+ : alerts)
+    for (int64_t q = 0; q < nids; ++q) {
+        const int64_t j = ids[q];
+        const uint8_t fj = flags[j];
+        int active = fj & 1, conv = (fj >> 1) & 1, cnt = (fj >> 2) & 3;
+        const int halve = active && degree(&c, j) > 0;
+        double acc_s = halve ? sv[j] * 0.5 : sv[j];
+        double acc_w = halve ? wv[j] * 0.5 : wv[j];
+        int recv = 0;
+        /* lattice senders in j's slot order */
+        int64_t nb[7];
+        const int d = topology == OR_LINE ? line_nbrs(P, j, nb) : lattice_nbrs(g, j, nb);
+        for (int k = 0; k < d; ++k) {
+            const int64_t n = nb[k];
+            if (!(flags[n] & 1)) continue;
+            const int64_t dn = degree(&c, n);
+            if (dn <= 0) continue;
+            int rnd_slot;
+            const uint32_t kk = or_uniform(seed, OR_STREAM_PUSHSUM, (uint64_t)n, round, (uint32_t)dn);
+            if (slot_target(&c, n, kk, &rnd_slot) != j || rnd_slot) continue;
+            acc_s = acc_s + sv[n] * 0.5;
+            acc_w = acc_w + wv[n] * 0.5;
+            recv = 1;
+        }
+        /* random in-senders by ascending id */
+        if (topology == OR_IMP3D) {
+            const int64_t b = roff[q], e = roff[q + 1];
+            for (int64_t p = b + 1; p < e; ++p) { /* insertion sort: a handful per receiver */
+                uint32_t v = rsrc[p];
+                int64_t t = p;
+                while (t > b && rsrc[t - 1] > v) { rsrc[t] = rsrc[t - 1]; --t; }
+                rsrc[t] = v;
+            }
+            for (int64_t p = b; p < e; ++p) {
+                const int64_t i = rsrc[p];
+                if (!(flags[i] & 1)) continue;
+                const int64_t di = degree(&c, i);
+                const uint32_t kk = or_uniform(seed, OR_STREAM_PUSHSUM, (uint64_t)i, round, (uint32_t)di);
+                if (kk != (uint32_t)(di - 1)) continue; /* the random slot is the last one */
+                acc_s = acc_s + sv[i] * 0.5;
+                acc_w = acc_w + wv[i] * 0.5;
+                recv = 1;
+            }
+        }
+        if (recv) {
+            if (!conv) {
+                const double r_old = sv[j] / wv[j];
+                const double r_new = acc_s / acc_w;
+                cnt = (fabs(r_new - r_old) > 1e-10) ? 0 : cnt + 1;
+                if (cnt == 3) { conv = 1; alerts += 1; }
+            }
+            active = 1;
+        }
+        s_out[q] = acc_s;
+        w_out[q] = acc_w;
+        flags_out[q] = (uint8_t)(active | (conv << 1) | ((cnt & 3) << 2));
+    }
+    free(rsrc); free(c.rnd); free(pos); free(roff); free(rcur);
+    return alerts;
+}

@@ -65,6 +65,15 @@ int or_neighbors(const or_sim* s, int64_t i, int64_t* out);
 int or_read_state(const or_sim* s, int64_t first, int64_t count, int32_t* c,
                   double* sv, double* wv, uint8_t* flags);
 
+/* Push-sum round `round` for the distinct receivers ids[0..nids) from a full
+ * round-start state (all P nodes: s, w, flags as or_read_state) -- the check of
+ * the product's round at populations the whole-network oracle cannot run.
+ * Returns how many sampled receivers converge in the round, -1 on bad input. */
+int64_t or_pushsum_receivers(int topology, int64_t num_nodes, uint64_t seed, uint32_t round,
+                             const double* sv, const double* wv, const uint8_t* flags,
+                             const int64_t* ids, int64_t nids, double* s_out, double* w_out,
+                             uint8_t* flags_out, int threads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -46,6 +46,8 @@ def lib():
         L.or_uniform.argtypes = [u64, u32, u64, u32, u32]
         L.or_icbrt_ceil.restype = i64
         L.or_icbrt_ceil.argtypes = [i64]
+        L.or_pushsum_receivers.restype = i64
+        L.or_pushsum_receivers.argtypes = [i32, i64, u64, u32, vp, vp, vp, vp, i64, vp, vp, vp, i32]
         _lib = L
     return _lib
 
@@ -57,6 +59,26 @@ def philox(ctr, key):
     o = (C.c_uint32 * 4)()
     L.or_philox4x32_10(c, k, o)
     return tuple(o)
+
+
+def pushsum_receivers(topology, num_nodes, seed, rnd, s, w, flags, ids, threads=0):
+    """Round `rnd` of push-sum for the receivers `ids`, from the full round-start
+    state (s, w, flags of all P nodes): or_pushsum_receivers.  Returns
+    (s_out, w_out, flags_out, converging) for the ids."""
+    topology = "Imp3D" if topology.lower() == "imp3d" else topology
+    s = np.ascontiguousarray(s, np.float64)
+    w = np.ascontiguousarray(w, np.float64)
+    flags = np.ascontiguousarray(flags, np.uint8)
+    ids = np.ascontiguousarray(ids, np.int64)
+    so = np.zeros(len(ids), np.float64)
+    wo = np.zeros(len(ids), np.float64)
+    fo = np.zeros(len(ids), np.uint8)
+    a = lib().or_pushsum_receivers(TOPO[topology], num_nodes, seed, rnd, s.ctypes.data, w.ctypes.data,
+                                   flags.ctypes.data, ids.ctypes.data, len(ids), so.ctypes.data, wo.ctypes.data,
+                                   fo.ctypes.data, threads)
+    if a < 0:
+        raise ValueError("or_pushsum_receivers: bad input")
+    return so, wo, fo, a
 
 
 class Oracle:

@@ -149,3 +149,27 @@ def test_gossip_invariants(topo):
         assert np.all(c >= prev)
         assert (c >= 11).sum() == o.alerts_total
         prev = c
+
+
+@pytest.mark.parametrize("n,topo,seed", [(27000, "Imp3D", 3), (64000, "Imp3D", 11), (8000, "3D", 5), (3000, "line", 2)])
+def test_pushsum_receivers_matches_whole_network_round(n, topo, seed):
+    """or_pushsum_receivers (one round for sampled receivers, pulled from a full
+    round-start state -- the checker of the P = 1e9 GPU round) equals the whole-
+    network oracle's round, bit for bit, during activation and in steady state."""
+    from tests.oracle_ctypes import pushsum_receivers
+    orc = Oracle(n, topo, "push-sum", seed)
+    P = orc.P
+    rng = np.random.default_rng(seed)
+    for warm in (3, 25, 150):
+        orc.step(warm - orc.rounds) if warm > orc.rounds else None
+        st = orc.state()
+        r = orc.rounds
+        ids = np.unique(np.concatenate([rng.choice(P, size=min(P, 2000), replace=False),
+                                        np.arange(min(P, 300)), np.arange(P - 300, P)]))
+        so, wo, fo, _ = pushsum_receivers(topo, n, seed, r, st["s"], st["w"], st["flags"], ids)
+        orc.step(1)
+        nx = orc.state()
+        np.testing.assert_array_equal(so, nx["s"][ids])
+        np.testing.assert_array_equal(wo, nx["w"][ids])
+        np.testing.assert_array_equal(fo, nx["flags"][ids])
+    orc.close()

@@ -49,9 +49,26 @@ def mean_last(rows, key, last):
     return sum(vals) / len(vals) if vals else None, len(vals)
 
 
+def dominant_kernel(root):
+    """Name of the kernel with the largest total WRITE_SIZE in a pass directory
+    (the round kernel: it writes the next state)."""
+    tot = {}
+    for path in sorted(glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True)):
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                if row["Counter_Name"] == "WRITE_SIZE":
+                    tot[row["Kernel_Name"]] = tot.get(row["Kernel_Name"], 0.0) + float(row["Counter_Value"])
+    return max(tot, key=tot.get) if tot else None
+
+
 def bytes_per_dispatch(dirs, sub, last=None):
     """dirs: {pass name: output dir}.  Mean bytes per dispatch over the last
-    `last` dispatches of the matching kernel in every pass."""
+    `last` dispatches of the matching kernel in every pass.  sub == "auto": the
+    kernel that writes the most (dominant_kernel); its name is returned too."""
+    if sub == "auto":
+        sub = dominant_kernel(dirs["wr"])
+        if sub is None:
+            return None
     rows = {name: per_dispatch(d, sub) for name, d in dirs.items()}
     n32, c1 = mean_last(rows["rdA"], "TCC_EA0_RDREQ_32B_sum", last)
     nall, _ = mean_last(rows["rdA"], "TCC_EA0_RDREQ_sum", last)
@@ -70,6 +87,7 @@ def bytes_per_dispatch(dirs, sub, last=None):
         "rdreq_unclassified": nall - n32 - n64 - n128,
         "fetch_size_equivalent_bytes": (64.0 * (nall - n32) + 32.0 * n32),
         "dispatches": min(c1, c2, c3),
+        "kernel": sub,
     }
 
 
