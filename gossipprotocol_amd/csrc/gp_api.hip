@@ -909,7 +909,7 @@ void choose_kernel(gp_sim* s, int64_t nloc_max, int& kernel, uint32_t& col_xsegs
     const bool push = cfg->algorithm == GP_PUSHSUM;
     // push-sum column kernel: Imp3D senders carry their degree in 2 bits (P <= 2^30)
     const bool pscol_ok = !s->force_tile && (cfg->topology == GP_3D || s->P <= (1ll << 30));
-    if (lattice && g >= 200 && (!push || pscol_ok)) kernel = KERNEL_COL;
+    if (lattice && g >= 200 && !push) kernel = KERNEL_COL;
 #ifdef GP_EXPERIMENTS
     if (const char* e = std::getenv("GP_KERNEL")) {
         if (!std::strcmp(e, "tile")) kernel = KERNEL_TILE;
