@@ -52,12 +52,19 @@ constexpr int PC_F0 = PC_Q / BULK_THREADS;   // in-edges per thread at the mean 
 constexpr int PC_FU = PC_F0 + 1;             // staged in-edges per thread: 11-16 sigma above the mean
 constexpr uint32_t PC_NW = PC_FU * WPB;      // 64-bit used-edge words per step
 constexpr uint32_t PC_MW = 16 + 16 * PC_NR;  // message slots per wave and step (mean 64 PC_NR / 7 used)
+#ifndef GP_PC_AHEAD
+#define GP_PC_AHEAD 2
+#endif
+constexpr int PC_AHEAD = GP_PC_AHEAD;        // steps between a step's in-edge decisions (message gathers) and its fold
+constexpr int PC_NE = PC_AHEAD + 1;          // LDS sets of in-edge data in use
 
 struct PsColLds {
-    double2 msg[2][WPB * PC_MW];             // used random-edge messages, compacted per wave
-    unsigned long long bits[2][PC_NW + 1];   // bit q % 64 of word q / 64: in-edge q of the step was used; then 0
-    uint32_t wb[2][PC_NW];                   // slot of the first used edge of each word
-    uint32_t ind[2][PC_Q / 8];               // the step's in-degrees, a nibble per receiver
+    // in-edge data of a step, set step % PC_NE
+    double2 msg[PC_NE][WPB * PC_MW];         // used random-edge messages, compacted per wave
+    unsigned long long bits[PC_NE][PC_NW + 1];  // bit q % 64 of word q / 64: in-edge q of the step was used; then 0
+    uint32_t wb[PC_NE][PC_NW];               // slot of the first used edge of each word
+    uint32_t ind[PC_NE][PC_Q / 8];           // the step's in-degrees, a nibble per receiver
+    // plane data by parity
     double2 ydn[2][WPB][64];                 // [b]: (s, w) of row y0 + 4b - 1 where it sends +y
     double2 yup[2][WPB][64];                 // [b]: (s, w) of row y0 + 4b + 4 where it sends -y
     uint8_t ydnf[2][WPB][64];                //       ... and whether it does
@@ -150,26 +157,22 @@ __device__ __forceinline__ void pscol_item(const PsColArgs& a, uint32_t r, PsCol
     for (int m = 0; m < PC_FU; ++m) raw[m] = 0u;
     uint32_t hb = DIR_NONE, zhb = DIR_NONE;
     uint32_t dslot = 0, dslot_n = 0;  // direction slots of planes i, i + 1 (a byte per row)
-    const int64_t ia = (int64_t)xa - 3;
-    // in-edge ranges: e_a = step(i), e_b = step(i + 1), e_c = step(i + 2), e_d = step(i + 3)
-    uint32_t e_a = 0, e_b = 0, e_c = 0, e_d = 0;
-    if (TOPO == IMP3D) {
-        e_a = soff_at(ia);
-        e_b = soff_at(ia + 1);
-        e_c = soff_at(ia + 2);
-        e_d = soff_at(ia + 3);
-    }
+    const int64_t ia = (int64_t)xa - (PC_AHEAD + 1 > 3 ? PC_AHEAD + 1 : 3);
+    // first edges of the steps i .. i + PC_AHEAD + 2 (pc_soff read ahead of use)
+    uint32_t ev[PC_AHEAD + 3];
+#pragma unroll
+    for (int t = 0; t < PC_AHEAD + 3; ++t) ev[t] = TOPO == IMP3D ? soff_at(ia + t) : 0u;
 
     for (int64_t i = ia; i < (int64_t)xb; ++i) {
-        // ---- (2) decide step i + 1: in-edge draws and message gathers, halo gathers, boundary rows
-        const int64_t dx = i + 1;
-        if (dx >= (int64_t)xa && dx < (int64_t)xb) {
-            const int par = (int)(dx & 1);
-            const uint32_t px = (uint32_t)dx * g2;
-            if (TOPO == IMP3D) {
+        // ---- (2a) decide step i + PC_AHEAD's in-edges: sender draws, message gathers
+        const int64_t ex_ = i + PC_AHEAD;
+        if (TOPO == IMP3D && ex_ >= (int64_t)xa && ex_ < (int64_t)xb) {
+            const int es = (int)(ex_ % PC_NE);
+            const uint32_t e_b = ev[PC_AHEAD];
+            {
                 if (wv == 0 && lane < PC_Q / 32)  // the step's nibble in-degrees (PC_Q / 2 bytes)
-                    dma16(a.ind4 + ((uint64_t)(sbase + dx) * (PC_Q / 2) + lane * 16), &L.ind[par][0]);
-                const uint32_t cnt = e_c - e_b;
+                    dma16(a.ind4 + ((uint64_t)(sbase + ex_) * (PC_Q / 2) + lane * 16), &L.ind[es][0]);
+                const uint32_t cnt = ev[PC_AHEAD + 1] - e_b;
                 uint32_t isrc[PC_FU];
                 bool sent[PC_FU];
 #pragma unroll
@@ -243,8 +246,8 @@ __device__ __forceinline__ void pscol_item(const PsColArgs& a, uint32_t r, PsCol
                     const uint32_t nb_ = (uint32_t)__popcll(bal);
                     const uint32_t rk = lane_prefix(bal);
                     if (lane == 0) {
-                        L.bits[par][m * WPB + wv] = bal;
-                        L.wb[par][m * WPB + wv] = wv * PC_MW + run;
+                        L.bits[es][m * WPB + wv] = bal;
+                        L.wb[es][m * WPB + wv] = wv * PC_MW + run;
                     }
                     if (nb_ && run < PC_MW) {  // wave-uniform
                         const uint32_t q = threadIdx.x + m * BULK_THREADS;
@@ -254,12 +257,18 @@ __device__ __forceinline__ void pscol_item(const PsColArgs& a, uint32_t r, PsCol
                         const uint32_t alo = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst * 4u), (int)(uint32_t)ad);
                         const uint32_t ahi = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst * 4u), (int)(uint32_t)(ad >> 32));
                         if (lane < nb_ && run + lane < PC_MW)
-                            dma16(reinterpret_cast<const void*>(((uint64_t)ahi << 32) | alo), &L.msg[par][wv * PC_MW + run]);
+                            dma16(reinterpret_cast<const void*>(((uint64_t)ahi << 32) | alo), &L.msg[es][wv * PC_MW + run]);
                     }
                     run += nb_;
                 }
-                if (threadIdx.x == 0) L.bits[par][PC_NW] = 0ull;
+                if (threadIdx.x == 0) L.bits[es][PC_NW] = 0ull;
             }
+        }
+        // ---- (2b) decide plane i + 1: halo gathers, direction draws, boundary rows
+        const int64_t dx = i + 1;
+        if (dx >= (int64_t)xa && dx < (int64_t)xb) {
+            const int par = (int)(dx & 1);
+            const uint32_t px = (uint32_t)dx * g2;
             // halo rows and columns of plane i + 1: gathered only where that node sends into the patch
             {
                 const bool up = wv == 0;  // wave 0: row y0 - 1 sending +y (dir 2); wave 3: row y0 + 16 sending -y (dir 3)
@@ -327,23 +336,25 @@ __device__ __forceinline__ void pscol_item(const PsColArgs& a, uint32_t r, PsCol
                 zhb2 = zhv ? lz : DIR_NONE;
             }
         }
-        uint32_t raw2[PC_FU];
-        uint32_t e_e = 0;
+        uint32_t raw2[PC_FU];  // in-edge senders of step i + PC_AHEAD + 1
+        uint32_t e_new = 0;
         if (TOPO == IMP3D) {
-            const uint32_t cnt2 = e_d - e_c;
-            const bool ed_ok = i + 2 >= (int64_t)xa && i + 2 < (int64_t)xb;
+            const uint32_t e_c = ev[PC_AHEAD + 1], cnt2 = ev[PC_AHEAD + 2] - e_c;
+            const bool ed_ok = i + PC_AHEAD + 1 >= (int64_t)xa && i + PC_AHEAD + 1 < (int64_t)xb;
 #pragma unroll
             for (int m = 0; m < PC_FU; ++m) {
                 const uint32_t q = threadIdx.x + m * BULK_THREADS;
                 raw2[m] = __builtin_nontemporal_load(a.src + e_c + (cnt2 && ed_ok ? min(q, cnt2 - 1u) : 0u));
             }
-            e_e = soff_at(i + 4);
+            e_new = soff_at(i + PC_AHEAD + 3);
         }
 
         // ---- (3) fold plane i
         if (i >= (int64_t)xa) {
             const uint32_t xi = (uint32_t)i;
             const int par = (int)(i & 1);
+            const int es = (int)(i % PC_NE);
+            const uint32_t e_a = ev[0];
             const uint32_t px = xi * g2;
             const uint32_t xbits = (xi > 0 ? 1u : 0u) | (xi + 1 < g ? 2u : 0u);
             // Imp3D: receiver q's in-edges are [pre(q), pre(q) + d(q)) of the step, pre = the
@@ -353,7 +364,7 @@ __device__ __forceinline__ void pscol_item(const PsColArgs& a, uint32_t r, PsCol
             // create)
             uint32_t cinc = 0;
             if (TOPO == IMP3D) {
-                const uint2 w2 = lane < PC_Q / 16 ? reinterpret_cast<const uint2*>(L.ind[par])[lane] : make_uint2(0u, 0u);
+                const uint2 w2 = lane < PC_Q / 16 ? reinterpret_cast<const uint2*>(L.ind[es])[lane] : make_uint2(0u, 0u);
                 auto nsum = [](uint32_t w_) { return (((w_ & 0x0F0F0F0Fu) + ((w_ >> 4) & 0x0F0F0F0Fu)) * 0x01010101u) >> 24; };
                 uint32_t incl = nsum(w2.x) + nsum(w2.y);
 #pragma unroll
@@ -400,7 +411,7 @@ __device__ __forceinline__ void pscol_item(const PsColArgs& a, uint32_t r, PsCol
                 uint32_t epre = 0, edeg = 0;
                 if (TOPO == IMP3D) {
                     const uint32_t ql = (PC_NR * wv + k) * 64u + lane;
-                    const uint32_t d = (reinterpret_cast<const uint8_t*>(L.ind[par])[ql >> 1] >> ((ql & 1u) * 4u)) & 15u;
+                    const uint32_t d = (reinterpret_cast<const uint8_t*>(L.ind[es])[ql >> 1] >> ((ql & 1u) * 4u)) & 15u;
                     uint32_t ex = lane_prefix(__ballot(d & 1u)) + 2u * lane_prefix(__ballot(d & 2u));
                     if (__ballot(d >= 4u)) ex += 4u * lane_prefix(__ballot(d & 4u)) + 8u * lane_prefix(__ballot(d & 8u));
                     epre = (uint32_t)__builtin_amdgcn_readlane((int)cinc, (int)(4u * (PC_NR * wv + k))) + ex;
@@ -430,7 +441,7 @@ __device__ __forceinline__ void pscol_item(const PsColArgs& a, uint32_t r, PsCol
                     if (TOPO == IMP3D) {
                         // used in-edges: the node's window of the step bitmap, 32 bits at a time,
                         // walked set bit by set bit (ascending sender = canonical order)
-                        const uint32_t* bw = reinterpret_cast<const uint32_t*>(L.bits[par]);
+                        const uint32_t* bw = reinterpret_cast<const uint32_t*>(L.bits[es]);
                         const uint32_t qe = epre + edeg;
                         for (uint32_t q0 = epre; q0 < qe; q0 += 32u) {
                             uint32_t win = __builtin_amdgcn_alignbit(bw[(q0 >> 5) + 1], bw[q0 >> 5], q0 & 31u);
@@ -439,11 +450,11 @@ __device__ __forceinline__ void pscol_item(const PsColArgs& a, uint32_t r, PsCol
                                 const uint32_t q = q0 + (uint32_t)__builtin_ctz(win);
                                 win &= win - 1u;
                                 const uint32_t wd = q >> 6;
-                                const unsigned long long below = L.bits[par][wd] & ((1ull << (q & 63u)) - 1ull);
-                                const uint32_t slot = L.wb[par][wd] + (uint32_t)__popcll(below);
+                                const unsigned long long below = L.bits[es][wd] & ((1ull << (q & 63u)) - 1ull);
+                                const uint32_t slot = L.wb[es][wd] + (uint32_t)__popcll(below);
                                 // (unconditional LDS read with a clamped slot: as two branches the
                                 // compiler merged the LDS and HBM reads into one flat load)
-                                double2 mi = L.msg[par][min(slot, WPB * PC_MW - 1u)];
+                                double2 mi = L.msg[es][min(slot, WPB * PC_MW - 1u)];
                                 asm volatile("" : "+v"(mi.x), "+v"(mi.y));
                                 if (slot >= ((wd % WPB) + 1u) * PC_MW) {  // the wave's slots overflowed (never expected): HBM
                                     const uint32_t i_ = a.src[e_a + q] & 0x3FFFFFFFu;
@@ -510,10 +521,9 @@ __device__ __forceinline__ void pscol_item(const PsColArgs& a, uint32_t r, PsCol
         if (TOPO == IMP3D) {
 #pragma unroll
             for (int m = 0; m < PC_FU; ++m) raw[m] = raw2[m];
-            e_a = e_b;
-            e_b = e_c;
-            e_c = e_d;
-            e_d = e_e;
+#pragma unroll
+            for (int t = 0; t + 1 < PC_AHEAD + 3; ++t) ev[t] = ev[t + 1];
+            ev[PC_AHEAD + 2] = e_new;
         }
     }
 }

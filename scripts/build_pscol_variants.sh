@@ -7,8 +7,10 @@ make -s -C gossipprotocol_amd/csrc >/dev/null
 mkdir -p build/ablate
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -DGP_EXPERIMENTS"
 others=$(ls build/obj_exp/*.o | grep -v gp_pscol.o)
-declare -A V=( [nr2m4]="-DGP_PC_NR=2 -DGP_PC_MINW=4" [nr4m3]="-DGP_PC_NR=4 -DGP_PC_MINW=3"
-               [nr4m4]="-DGP_PC_NR=4 -DGP_PC_MINW=4" [nr2m5]="-DGP_PC_NR=2 -DGP_PC_MINW=5" )
+declare -A V=( [nr2m4]="-DGP_PC_NR=2 -DGP_PC_MINW=4 -DGP_PC_AHEAD=1" [nr4m3]="-DGP_PC_NR=4 -DGP_PC_MINW=3 -DGP_PC_AHEAD=1"
+               [nr4m4]="-DGP_PC_NR=4 -DGP_PC_MINW=4 -DGP_PC_AHEAD=1" [nr2m5]="-DGP_PC_NR=2 -DGP_PC_MINW=5 -DGP_PC_AHEAD=1"
+               [nr2a2]="-DGP_PC_NR=2 -DGP_PC_MINW=4 -DGP_PC_AHEAD=2" [nr4m3a2]="-DGP_PC_NR=4 -DGP_PC_MINW=3 -DGP_PC_AHEAD=2"
+               [nr2a3]="-DGP_PC_NR=2 -DGP_PC_MINW=4 -DGP_PC_AHEAD=3" )
 for v in ${ONLY:-${!V[@]}}; do
   /opt/rocm/bin/hipcc $FLAGS ${V[$v]} -c gossipprotocol_amd/csrc/gp_pscol.hip -o build/ablate/gp_pscol_$v.o &
 done
