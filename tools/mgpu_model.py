@@ -1,0 +1,185 @@
+"""Multi-GPU round-time model from one GPU (experiment tool).
+
+    python tools/mgpu_model.py run   <n> <topology> <algorithm> <W> <rounds>
+    python tools/mgpu_model.py model <trace dir> <n> <topology> <algorithm> <W> <rounds> [out.json]
+
+`run` is the workload: W in-process virtual ranks on one device
+(GP_FLAG_VIRTUAL_RANKS -- the same slab plan, kernels and exchange order as W
+processes over RCCL, with device copies as the transport), advanced to steady
+state (push-sum: every node active), then `rounds` timed rounds.  Run it under
+`rocprofv3 --kernel-trace`.
+
+`model` reads that trace.  Rounds are cut after every group of W
+`k_finalize_post` dispatches (the last kernels of a multi-rank round); inside a
+round the k-th dispatch of a kernel launched once per slab belongs to slab k.
+Per rank: the sum of its kernels (round kernel, pack / unpack or the full
+topology's binning passes, finalize) = what that rank's GPU computes per round
+at world W (each slab ran alone on the whole device, as it would on its own
+GPU).  Device-copy kernels are the virtual transport and are dropped; in their
+place the exchange is modelled from the bytes RCCL moves per round -- the
+fixed-capacity buffers of setup_exchange (restated in tests/test_multigpu_plan.py)
+and the halo planes -- over point-to-point xGMI links (one link per rank pair
+on an 8-GPU node) at the assumed per-direction link rates, plus an assumed
+latency per RCCL group and for the 4 x u64 bookkeeping all-reduce.  Nothing here
+is a measured multi-GPU number.
+"""
+import csv
+import glob
+import json
+import math
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+LINK_GBPS = (64.0, 128.0)   # assumed achieved RCCL send/recv rate per xGMI link and direction
+GROUP_LAT_MS = 0.020        # assumed latency of one grouped send/recv
+ALLREDUCE_LAT_MS = 0.015    # assumed latency of the 4 x u64 all-reduce
+
+
+def run(n, topo, alg, W, rounds):
+    import time
+
+    from gossipprotocol_amd import Simulation
+    s = Simulation(n, topo, alg, virtual_ranks=W)
+    P = s.population
+    pre = 0
+    t = time.perf_counter()
+    if alg == "push-sum":
+        while s.info().active < P and pre < 3000:
+            pre += len(s.step(8))
+    else:
+        pre += len(s.step(40))
+    s.sync()
+    tp = time.perf_counter() - t
+    t = time.perf_counter()
+    got = s.step(rounds)
+    s.sync()
+    wall = time.perf_counter() - t
+    print(json.dumps({"n": n, "topology": topo, "algorithm": alg, "W": W, "P": P, "preroll_rounds": pre,
+                      "preroll_s": tp, "rounds": len(got), "wall_ms_per_round_virtual": wall * 1e3 / max(1, len(got))}),
+          flush=True)
+    s.close()
+
+
+def pair_bytes(n, topo, alg, W):
+    """Bytes rank a sends rank b per round (fixed-capacity buffer incl. its 16-B count
+    header) and the halo bytes per neighbouring pair and direction."""
+    from tests.multirank_emu import full_capacity, resolve, slab_bounds
+    from tests.test_multigpu_plan import cap_of, imp3d_pair_stats
+    P, _, g = resolve(n, topo)
+    push = alg == "push-sum"
+
+    def xbuf(cap):
+        return 0 if cap <= 0 else 16 + ((cap * 4 + 15) & ~15) + (16 * cap if push else 0)
+
+    B = [[0] * W for _ in range(W)]
+    halo = 0
+    if topo == "full":
+        bounds, _ = slab_bounds(P, g, topo, W)
+        for a in range(W):
+            na = bounds[a + 1] - bounds[a]
+            for b in range(W):
+                if b != a:
+                    B[a][b] = xbuf(full_capacity(na, bounds[b + 1] - bounds[b], P))
+    else:
+        bounds, H = slab_bounds(P, g, topo, W)
+        halo = H * (1 + (16 if push else 0))
+        if topo == "Imp3D":
+            _, mu, _ = imp3d_pair_stats(P, g, W)
+            for a in range(W):
+                for b in range(W):
+                    if b != a:
+                        B[a][b] = xbuf(cap_of(mu[a, b]))
+    return P, bounds, B, halo
+
+
+def model(tdir, n, topo, alg, W, rounds, out=None):
+    rows = []
+    for f in glob.glob(tdir + "/**/*kernel_trace.csv", recursive=True):
+        rows += list(csv.DictReader(open(f)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    groups, cur, nfin = [], [], 0
+    for r in rows:
+        name = r["Kernel_Name"]
+        cur.append((name, (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6))
+        if "k_finalize_post" in name:
+            nfin += 1
+            if nfin == W:
+                groups.append(cur)
+                cur, nfin = [], 0
+    groups = groups[-rounds:]
+    if not groups:
+        raise SystemExit("no multi-rank rounds in the trace")
+    short = lambda k: k.split("(")[0].replace("void ", "").replace("gp::", "")  # noqa: E731
+    per_slab, glob_k, copy_ms = {}, {}, []
+    rank_ms = [[] for _ in range(W)]
+    for grp in groups:
+        by = {}
+        for name, ms in grp:
+            by.setdefault(name, []).append(ms)
+        tr = [0.0] * W
+        cp = 0.0
+        for name, v in by.items():
+            if "rocclr_copy" in name:
+                cp += sum(v)
+            elif len(v) == W:
+                per_slab.setdefault(short(name), []).append(v)
+                for k in range(W):
+                    tr[k] += v[k]
+            elif "fill" not in name:  # (memsets: counters, on every rank)
+                glob_k.setdefault(short(name), []).append(sum(v))
+                for k in range(W):
+                    tr[k] += sum(v) / max(1, len(v)) * (len(v) / W)
+            else:
+                for k in range(W):
+                    tr[k] += sum(v) / W
+        copy_ms.append(cp)
+        for k in range(W):
+            rank_ms[k].append(tr[k])
+    P, bounds, B, halo = pair_bytes(n, topo, alg, W)
+    kern = {k: [statistics.mean(x[s] for x in v) for s in range(W)] for k, v in per_slab.items()}
+    comp = [statistics.mean(v) for v in rank_ms]
+    t_comp = max(comp)
+    res = {"workload": f"{alg} {topo} n={n} P={P}", "W": W, "rounds_measured": len(groups),
+           "per_slab_kernel_ms": {k: [round(x, 4) for x in v] for k, v in kern.items()},
+           "global_kernel_ms": {k: round(statistics.mean(v), 4) for k, v in glob_k.items()},
+           "virtual_copy_ms": round(statistics.mean(copy_ms), 4),
+           "rank_compute_ms": [round(x, 4) for x in comp],
+           "pair_bytes_max": max(max(r) for r in B), "bytes_out_per_rank_max": max(sum(r) for r in B),
+           "halo_bytes_per_direction": halo, "assumptions": {
+               "link_gbps_per_direction": LINK_GBPS, "group_latency_ms": GROUP_LAT_MS,
+               "allreduce_latency_ms": ALLREDUCE_LAT_MS, "topology": "one xGMI link per rank pair (8-GPU node)"},
+           "model": []}
+    for bw in LINK_GBPS:
+        # the busiest link: a pair's buffer plus, between slab neighbours, the halo plane
+        link = 0.0
+        for a in range(W):
+            for b in range(W):
+                if a != b:
+                    link = max(link, B[a][b] + (halo if abs(a - b) == 1 else 0))
+        t_x = link / (bw * 1e9) * 1e3 + (GROUP_LAT_MS if link else 0.0)
+        serial = t_comp + t_x + ALLREDUCE_LAT_MS
+        overlap = max(t_comp, t_x) + ALLREDUCE_LAT_MS
+        res["model"].append({"link_gbps": bw, "exchange_ms": round(t_x, 4), "round_ms_serial": round(serial, 4),
+                             "exchange_share_serial": round(t_x / serial, 3), "round_ms_overlapped": round(overlap, 4),
+                             "node_updates_per_s_serial": P / (serial * 1e-3),
+                             "node_updates_per_s_overlapped": P / (overlap * 1e-3)})
+    txt = json.dumps(res, indent=1)
+    print(txt)
+    if out:
+        open(out, "w").write(txt + "\n")
+
+
+def main():
+    if sys.argv[1] == "run":
+        run(int(sys.argv[2]), sys.argv[3], sys.argv[4], int(sys.argv[5]), int(sys.argv[6]))
+    else:
+        model(sys.argv[2], int(sys.argv[3]), sys.argv[4], sys.argv[5], int(sys.argv[6]), int(sys.argv[7]),
+              sys.argv[8] if len(sys.argv) > 8 else None)
+
+
+if __name__ == "__main__":
+    main()
