@@ -131,6 +131,29 @@ GP_HD uint32_t uniform(uint32_t k0, uint32_t k1, uint32_t stream, uint32_t node,
     return uniform_from(x, y, m);
 }
 
+// ---------------------------------------------------------------- push-sum ratio test
+// The stability test of Program.fs:114-123 as SRS v1 states it: did the ratio
+// move, |RN(s2 / w2) - RN(s / w)| > 1e-10 (both quotients and their difference
+// rounded to double)?  Two fp64 divisions are ~30 VALU instructions, a large
+// share of a node's work, so a division-free test decides first whenever it can
+// prove the answer "moved":
+//   N = s2 w - s w2 (b = fma(s2, w, -RN(s w2)), m = RN(w w2)):  |b| > 2^-18 m
+// implies |s2/w2 - s/w| = |N| / (w w2) > 2^-20 + 2^-33 >= 1e-10 (1 + 2^-52) +
+// 2^-53 (|s2/w2| + |s/w|), i.e. even after rounding both quotients (each off by
+// at most 2^-53 of a ratio < 2^32: every ratio is a weighted mean of node ids,
+// ids < 2^32) and their difference, the exact test says "moved".  Margins: the
+// error of b is at most 2^-53 (|N| + s w2 (1 + 2^-53)) <= 2^-53 |N| + 2^-21 w w2,
+// that of m 2^-53 m; the products stay normal (the m and s w2 guards), and s, w
+// are >= 0 / > 0.  Everything else -- slow ratio changes, the converging tail --
+// takes the exact divisions.  Requires -ffp-contract=off (explicit fma only).
+GP_HD bool ratio_moved(double s, double w, double s2, double w2) {
+    const double a = s * w2;
+    const double b = __builtin_fma(s2, w, -a);
+    const double m = w * w2;
+    if (m >= 0x1p-900 && (s == 0.0 || a >= 0x1p-900) && __builtin_fabs(b) > 0x1p-18 * m) return true;
+    return __builtin_fabs(s2 / w2 - s / w) > 1e-10;
+}
+
 // ---------------------------------------------------------------- fast division
 // Exact n / d for 32-bit n and a runtime-constant d (libdivide's u32 scheme).
 struct FastDiv {

@@ -626,10 +626,8 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
             if (p1 > p0) {
                 uint32_t flags = b;
                 if (!(b & B_CONV)) {
-                    const double r_old = sv.x / sv.y;
-                    const double r_new = acc_s / acc_w;
                     uint32_t c = (b >> CNT_SHIFT) & 3u;
-                    c = fabs(r_new - r_old) > 1e-10 ? 0u : c + 1u;
+                    c = ratio_moved(sv.x, sv.y, acc_s, acc_w) ? 0u : c + 1u;
                     flags = (flags & ~(3u << CNT_SHIFT)) | (c << CNT_SHIFT);
                     if (c == 3) {
                         flags |= B_CONV;

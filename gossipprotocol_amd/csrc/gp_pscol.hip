@@ -468,10 +468,8 @@ __device__ __forceinline__ void pscol_item(const PsColArgs& a, uint32_t r, PsCol
                     uint32_t flags = b & (B_ACTIVE | B_CONV | (3u << CNT_SHIFT));
                     if (recv) {
                         if (!(b & B_CONV)) {
-                            const double r_old = sv.x / sv.y;
-                            const double r_new = acc_s / acc_w;
                             uint32_t cnt3 = (b >> CNT_SHIFT) & 3u;
-                            cnt3 = fabs(r_new - r_old) > 1e-10 ? 0u : cnt3 + 1u;
+                            cnt3 = ratio_moved(sv.x, sv.y, acc_s, acc_w) ? 0u : cnt3 + 1u;
                             flags = (flags & ~(3u << CNT_SHIFT)) | (cnt3 << CNT_SHIFT);
                             if (cnt3 == 3) {
                                 flags |= B_CONV;

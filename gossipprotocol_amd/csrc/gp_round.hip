@@ -284,13 +284,14 @@ struct TileWalk {
 __device__ __forceinline__ double2 ld_sw(const double2* p) { return *p; }
 
 // v of another lane of the wave by DPP (CTRL 0x130 wave_shl:1 = lane + 1's,
-// 0x138 wave_shr:1 = lane - 1's; the lane at the wave's end gets 0)
+// 0x138 wave_shr:1 = lane - 1's; the lane at the wave's end gets 0 -- bound_ctrl,
+// so no zeroed destination register is needed)
 template <int CTRL>
 __device__ __forceinline__ double2 dpp_double2(double2 v) {
     auto mv = [](double d) {
         const uint64_t u = __builtin_bit_cast(uint64_t, d);
-        const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xF, 0xF, false);
-        const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)u, CTRL, 0xF, 0xF, true);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, true);
         return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
     };
     return make_double2(mv(v.x), mv(v.y));
@@ -803,10 +804,8 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                         uint32_t flags = b & (B_ACTIVE | B_CONV | (3u << CNT_SHIFT));
                         if (recv) {
                             if (!(b & B_CONV)) {
-                                const double r_old = sv.x / sv.y;
-                                const double r_new = acc_s / acc_w;
                                 uint32_t cnt3 = (b >> CNT_SHIFT) & 3u;
-                                cnt3 = fabs(r_new - r_old) > 1e-10 ? 0u : cnt3 + 1u;
+                                cnt3 = ratio_moved(sv.x, sv.y, acc_s, acc_w) ? 0u : cnt3 + 1u;
                                 flags = (flags & ~(3u << CNT_SHIFT)) | (cnt3 << CNT_SHIFT);
                                 if (cnt3 == 3) {
                                     flags |= B_CONV;

@@ -3,6 +3,7 @@
 // product's Philox/U(m) printed for comparison with the oracle.
 // Built by tests/test_device_math.py with hipcc; runs on the CPU.
 #include <cstdio>
+#include <cmath>
 #include <cstdlib>
 #include <random>
 
@@ -41,5 +42,32 @@ int main() {
     uint32_t x, y;
     gp::philox2(0, 0, 0, 0, 0, x, y);
     std::printf("KAT0 %08x %08x\n", x, y);
+    // ratio_moved (fast division-free decision + exact fallback) == the exact test,
+    // on ratios < 2^32 moved by relative amounts from 0 to the whole range and near the 1e-10 edge
+    {
+        std::uniform_real_distribution<double> U01(0.0, 1.0);
+        long long n = 0, fast = 0, bad = 0;
+        for (int k = 0; k < 4000000; ++k) {
+            const double w = std::ldexp(0.5 + U01(rng), (int)(rng() % 80) - 60);
+            const double q = (k % 7 == 0) ? (double)(rng() % 64) : U01(rng) * std::ldexp(1.0, (int)(rng() % 33));
+            const double s = (k % 11 == 0) ? 0.0 : q * w;
+            const double w2 = w * (0.25 + 1.5 * U01(rng));
+            double q2;
+            switch (k % 4) {
+                case 0: q2 = q + std::ldexp(U01(rng) - 0.5, -(int)(rng() % 60)); break;          // absolute nudges
+                case 1: q2 = q * (1.0 + std::ldexp(U01(rng) - 0.5, -(int)(rng() % 60))); break;  // relative nudges
+                case 2: q2 = q + (U01(rng) < 0.5 ? -1.0 : 1.0) * 1e-10 * (1.0 + std::ldexp(U01(rng) - 0.5, -(int)(rng() % 40))); break;
+                default: q2 = U01(rng) * std::ldexp(1.0, (int)(rng() % 33)); break;
+            }
+            if (q2 < 0.0) q2 = 0.0;
+            const double s2 = q2 * w2;
+            const bool exact = std::fabs(s2 / w2 - s / w) > 1e-10;
+            const double a = s * w2, b = __builtin_fma(s2, w, -a), m = w * w2;
+            fast += (m >= 0x1p-900 && (s == 0.0 || a >= 0x1p-900) && std::fabs(b) > 0x1p-18 * m) ? 1 : 0;
+            bad += gp::ratio_moved(s, w, s2, w2) != exact ? 1 : 0;
+            ++n;
+        }
+        std::printf("ratio_moved %lld cases %lld fast %lld mismatches\n", n, fast, bad);
+    }
     return 0;
 }

@@ -22,7 +22,7 @@ def output(tmp_path_factory):
     if not os.path.exists(hipcc):
         pytest.skip("hipcc not available")
     exe = str(tmp_path_factory.mktemp("dm") / "device_math_check")
-    subprocess.check_call([hipcc, "-O2", "-std=c++17", "-o", exe, os.path.join(HERE, "helpers", "device_math_check.cpp")])
+    subprocess.check_call([hipcc, "-O2", "-std=c++17", "-ffp-contract=off", "-o", exe, os.path.join(HERE, "helpers", "device_math_check.cpp")])
     return subprocess.run([exe], check=True, capture_output=True, text=True).stdout.splitlines()
 
 
@@ -39,3 +39,13 @@ def test_product_philox_matches_oracle(output):
             assert lib().or_uniform(seed, stream, node, rnd, m) == u
             n += 1
     assert n == 200
+
+
+def test_ratio_moved_matches_exact_test(output):
+    """gp_device.hpp ratio_moved: the division-free shortcut never changes the
+    push-sum stability decision (Program.fs:114-123, SRS v1) -- 4e6 cases, ratios
+    < 2^32, moves from 0 to the whole range and around the 1e-10 edge."""
+    line = [l for l in output if l.startswith("ratio_moved")][0].split()
+    cases, fast, bad = int(line[1]), int(line[3]), int(line[5])
+    assert cases == 4000000 and bad == 0
+    assert fast > cases // 4  # the shortcut does decide a large share
