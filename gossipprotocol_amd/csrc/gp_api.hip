@@ -826,6 +826,7 @@ int exchange(gp_sim* s, uint32_t rn) {
             ua.push = push ? 1 : 0;
             for (int p = 0; p < W; ++p) ua.peer[p] = xpeer(sl.xrecv, sl.roff[p], sl.cap_in[p]);
             ua.overflow = sl.overflow;
+            ua.all_active = &sl.S.ctl->all_active;
             HIP_TRY(launch_unpack(ua, rn, std::max(1, s->grid / 8), s->stream));
         }
     }
@@ -908,7 +909,7 @@ void choose_kernel(gp_sim* s, int64_t nloc_max, int& kernel, uint32_t& col_xsegs
     const bool lattice = cfg->topology == GP_3D || cfg->topology == GP_IMP3D;
     const bool push = cfg->algorithm == GP_PUSHSUM;
     // push-sum column kernel: Imp3D senders carry their degree in 2 bits (P <= 2^30)
-    const bool pscol_ok = !s->force_tile && (cfg->topology == GP_3D || s->P <= (1ll << 30));
+    [[maybe_unused]] const bool pscol_ok = !s->force_tile && (cfg->topology == GP_3D || s->P <= (1ll << 30));
     if (lattice && g >= 200 && !push) kernel = KERNEL_COL;
 #ifdef GP_EXPERIMENTS
     if (const char* e = std::getenv("GP_KERNEL")) {

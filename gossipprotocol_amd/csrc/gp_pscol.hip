@@ -203,7 +203,8 @@ __device__ __forceinline__ void pscol_item(const PsColArgs& a, uint32_t r, PsCol
                 for (int m = 0; m < PC_FU; ++m) {
                     const uint32_t q = threadIdx.x + m * BULK_THREADS;
                     const uint32_t di = (raw[m] >> 30) + 4u;
-                    const bool local = !REMOTE || isrc[m] - a.lo < a.nloc;
+                    // every node active: a remote sender's draw decides too (no tag)
+                    const bool local = !REMOTE || all_active || isrc[m] - a.lo < a.nloc;
                     pick[m] = q < cnt && local && uniform_from(x[m], y[m], di) == di - 1u;
                 }
                 if (all_active) {
@@ -229,7 +230,7 @@ __device__ __forceinline__ void pscol_item(const PsColArgs& a, uint32_t r, PsCol
 #pragma unroll
                     for (int m = 0; m < PC_FU; ++m) sent[m] = pick[m] && ((wb_[m] >> zb[m]) & 1ull);
                 }
-                if (REMOTE) {  // sender on another rank: the exchange tagged its message
+                if (REMOTE && !all_active) {  // sender on another rank, activation: the exchange tagged its message
 #pragma unroll
                     for (int m = 0; m < PC_FU; ++m) {
                         const uint32_t q = threadIdx.x + m * BULK_THREADS;

@@ -496,7 +496,9 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
 #pragma unroll
                     for (int m = 0; m < FU; ++m) sent[m] = (wbits[m] >> (isrc[m] & 63)) & 1ull;
                 }
-                if (REMOTE) {  // sender on another rank: the exchange tagged its message
+                // sender on another rank, activation phase: the exchange tagged its message
+                // (every node active: its Philox draw above decides, like a local sender's)
+                if (REMOTE && !all_active) {
 #pragma unroll
                     for (int m = 0; m < FU; ++m) {
                         const uint32_t q = threadIdx.x + m * TPB;
@@ -782,18 +784,16 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                                     const uint32_t i = in_src[e];
                                     bool sent;
                                     double2 mi = make_double2(0.0, 0.0);
-                                    if (REMOTE && i - a.lo >= a.nloc) {
+                                    const bool rem = REMOTE && i - a.lo >= a.nloc;
+                                    if (all_active) {
+                                        const uint32_t di = popc6(present_mask<IMP3D>(i, G)) + 1u;
+                                        sent = uniform(a.k0, a.k1, S_PUSHSUM, i, r, di) == di - 1u;
+                                    } else if (rem) {
                                         sent = a.rtag[e] == r;
-                                        if (sent) mi = a.rmsg[e];
                                     } else {
-                                        if (all_active) {
-                                            const uint32_t di = popc6(present_mask<IMP3D>(i, G)) + 1u;
-                                            sent = uniform(a.k0, a.k1, S_PUSHSUM, i, r, di) == di - 1u;
-                                        } else {
-                                            sent = (rbc[(i >> 6) - (a.lo >> 6)] >> (i & 63)) & 1ull;
-                                        }
-                                        if (sent) mi = ld_sw(swc + i);
+                                        sent = (rbc[(i >> 6) - (a.lo >> 6)] >> (i & 63)) & 1ull;
                                     }
+                                    if (sent) mi = rem ? a.rmsg[e] : ld_sw(swc + i);
                                     if (sent) {
                                         fold(mi);
                                         recv = true;

@@ -35,6 +35,7 @@ struct UnpackArgs {
     int W, me, push;
     XPeer peer[XMAXW];    // receive side
     unsigned int* overflow;  // set when a sender packed more messages than the buffer holds
+    const unsigned int* all_active;  // Ctl::all_active of this rank (push-sum: no tags once set)
 };
 
 struct ZeroArgs {
