@@ -130,6 +130,7 @@ constexpr int FBR_CHUNK = FBR_THREADS * FBR_PER;
 #define GP_FB_RANGE 4
 #endif
 constexpr uint32_t FBR_ITEM = (uint32_t)GP_FB_RANGE * FBR_CHUNK;  // messages per work item
+static_assert(GP_FB_RANGE % 2 == 0, "sweep 1 takes two chunks at a time");
 
 struct FbRangeLds {
     double2 pay[FBR_CHUNK];     // the chunk's payloads in bin order
@@ -236,9 +237,15 @@ __global__ __launch_bounds__(FBR_THREADS, GP_FBR_MINB) void k_fb_send(FullBinArg
     cur.load(a, i0, i1);
     __syncthreads();
     // sweep 1: coarse bin (target >> s1) of every active sender, counted; two
-    // chunks per iteration (one Philox batch of 2 FBR_PER)
+    // chunks per iteration (one Philox batch of 2 FBR_PER).  The bins stay in
+    // registers for sweep 2 (16-bit, two per word), so each message's Philox draw
+    // is computed once per pass
     constexpr int P2 = 2 * FBR_PER;
-    for (uint64_t c0 = i0; c0 < i1; c0 += 2 * FBR_CHUNK) {
+    constexpr int NCH = GP_FB_RANGE;  // chunks per work item
+    uint32_t keys[NCH * FBR_PER / 2];
+#pragma unroll
+    for (int it = 0; it < NCH / 2; ++it) {
+        const uint64_t c0 = i0 + (uint64_t)it * 2 * FBR_CHUNK;
         uint32_t node[P2], x[P2], y[P2];
         uint8_t nbv[P2];
 #pragma unroll
@@ -249,29 +256,37 @@ __global__ __launch_bounds__(FBR_THREADS, GP_FBR_MINB) void k_fb_send(FullBinArg
         }
         philox2_batch<P2>(node, r, S_PUSHSUM, a.k0, a.k1, x, y);
 #pragma unroll
-        for (int k = 0; k < P2; ++k)
-            if ((nbv[k] & B_ACTIVE) && c0 + k * FBR_THREADS + threadIdx.x < i1)  // Program.fs:213-215
-                atomicAdd(&base[full_target(node[k], uniform_from(x[k], y[k], P - 1)) >> a.s1], 1u);
+        for (int k = 0; k < P2; k += 2) {
+            uint32_t kk[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                kk[h] = FB_NONE;
+                if ((nbv[k + h] & B_ACTIVE) && c0 + (k + h) * FBR_THREADS + threadIdx.x < i1) {  // Program.fs:213-215
+                    kk[h] = full_target(node[k + h], uniform_from(x[k + h], y[k + h], P - 1)) >> a.s1;
+                    atomicAdd(&base[kk[h]], 1u);
+                }
+            }
+            keys[(it * P2 + k) / 2] = kk[0] | (kk[1] << 16);
+        }
     }
     fbr_reserve(base, a.nb1, a.cnt1, 0, a.nb1);
     // sweep 2: {sender id | s/2, w/2} into the runs; the next chunk's input is
     // loaded while this one is put in order and written
-    for (uint64_t c0 = i0; c0 < i1; c0 += FBR_CHUNK) {
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+        const uint64_t c0 = i0 + (uint64_t)ch * FBR_CHUNK;
+        if (c0 >= i1) break;
         for (uint32_t b = threadIdx.x; b < a.nb1; b += FBR_THREADS) cnt[b] = 0u;
-        uint32_t node[FBR_PER], x[FBR_PER], y[FBR_PER], key[FBR_PER], rank[FBR_PER];
+        uint32_t node[FBR_PER], key[FBR_PER], rank[FBR_PER];
         double2 pay[FBR_PER];
 #pragma unroll
         for (int k = 0; k < FBR_PER; ++k) node[k] = (uint32_t)(c0 + k * FBR_THREADS + threadIdx.x);
-        philox2_batch<FBR_PER>(node, r, S_PUSHSUM, a.k0, a.k1, x, y);
         lds_barrier();  // counters zeroed
 #pragma unroll
         for (int k = 0; k < FBR_PER; ++k) {
-            key[k] = FB_NONE;
-            rank[k] = 0;
-            if ((cur.nbv[k] & B_ACTIVE) && c0 + k * FBR_THREADS + threadIdx.x < i1) {
-                key[k] = full_target(node[k], uniform_from(x[k], y[k], P - 1)) >> a.s1;
-                rank[k] = atomicAdd(&cnt[key[k]], 1u);
-            }
+            const int m = ch * FBR_PER + k;
+            key[k] = (keys[m / 2] >> (16 * (m & 1))) & 0xFFFFu;
+            rank[k] = key[k] != FB_NONE ? atomicAdd(&cnt[key[k]], 1u) : 0u;
             pay[k] = make_double2(cur.sv[k].x * 0.5, cur.sv[k].y * 0.5);
         }
         cur.load(a, c0 + FBR_CHUNK < i1 ? c0 + FBR_CHUNK : c0, i1);  // (the last chunk reloads itself)
@@ -313,43 +328,52 @@ __global__ __launch_bounds__(FBR_THREADS, GP_FBR_MINB) void k_fb_split(FullBinAr
     cur.load(a, ibase, q0, q1);
     __syncthreads();
     // sweep 1: fine tile of every message (target recomputed from the sender's
-    // draw), two chunks per iteration
+    // draw), two chunks per iteration; the tiles stay in registers for sweep 2
     constexpr int P2 = 2 * FBR_PER;
-    for (uint32_t c0 = q0; c0 < q1; c0 += 2 * FBR_CHUNK) {
+    constexpr int NCH = GP_FB_RANGE;
+    uint32_t keys[NCH * FBR_PER / 2];
+#pragma unroll
+    for (int it = 0; it < NCH / 2; ++it) {
+        const uint32_t c0 = q0 + it * 2 * FBR_CHUNK;
         uint32_t node[P2], x[P2], y[P2];
 #pragma unroll
-        for (int k = 0; k < P2; ++k) {
-            node[k] = a.hdr1[ibase + min(c0 + k * FBR_THREADS + threadIdx.x, q1 - 1)];
-        }
+        for (int k = 0; k < P2; ++k) node[k] = a.hdr1[ibase + min(c0 + k * FBR_THREADS + threadIdx.x, q1 - 1)];
         philox2_batch<P2>(node, r, S_PUSHSUM, a.k0, a.k1, x, y);
 #pragma unroll
-        for (int k = 0; k < P2; ++k)
-            if (c0 + k * FBR_THREADS + threadIdx.x < q1)
-                atomicAdd(
-                    &base[((full_target(node[k], uniform_from(x[k], y[k], a.P - 1)) - a.lo) >> FB_TB) & (nfine - 1u)],
-                    1u);
+        for (int k = 0; k < P2; k += 2) {
+            uint32_t kk[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                kk[h] = FB_NONE;
+                if (c0 + (k + h) * FBR_THREADS + threadIdx.x < q1) {
+                    kk[h] = ((full_target(node[k + h], uniform_from(x[k + h], y[k + h], a.P - 1)) - a.lo) >> FB_TB) &
+                            (nfine - 1u);
+                    atomicAdd(&base[kk[h]], 1u);
+                }
+            }
+            keys[(it * P2 + k) / 2] = kk[0] | (kk[1] << 16);
+        }
     }
     fbr_reserve(base, nfine, a.cnt2, f0, a.nb2);
     // sweep 2: into the fine tiles' runs, the next chunk loaded meanwhile
-    for (uint32_t c0 = q0; c0 < q1; c0 += FBR_CHUNK) {
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+        const uint32_t c0 = q0 + ch * FBR_CHUNK;
+        if (c0 >= q1) break;
         for (uint32_t f = threadIdx.x; f < nfine; f += FBR_THREADS) cnt[f] = 0u;
-        uint32_t node[FBR_PER], x[FBR_PER], y[FBR_PER], key[FBR_PER], rank[FBR_PER];
+        uint32_t node[FBR_PER], key[FBR_PER], rank[FBR_PER];
         double2 pay[FBR_PER];
 #pragma unroll
         for (int k = 0; k < FBR_PER; ++k) {
             node[k] = cur.node[k];
             pay[k] = cur.pv[k];
         }
-        philox2_batch<FBR_PER>(node, r, S_PUSHSUM, a.k0, a.k1, x, y);
         lds_barrier();  // counters zeroed
 #pragma unroll
         for (int k = 0; k < FBR_PER; ++k) {
-            key[k] = FB_NONE;
-            rank[k] = 0;
-            if (c0 + k * FBR_THREADS + threadIdx.x < q1) {
-                key[k] = ((full_target(node[k], uniform_from(x[k], y[k], a.P - 1)) - a.lo) >> FB_TB) & (nfine - 1u);
-                rank[k] = atomicAdd(&cnt[key[k]], 1u);
-            }
+            const int m = ch * FBR_PER + k;
+            key[k] = (keys[m / 2] >> (16 * (m & 1))) & 0xFFFFu;
+            rank[k] = key[k] != FB_NONE ? atomicAdd(&cnt[key[k]], 1u) : 0u;
         }
         cur.load(a, ibase, c0 + FBR_CHUNK < q1 ? c0 + FBR_CHUNK : c0, q1);
         lds_barrier();  // ranks counted
