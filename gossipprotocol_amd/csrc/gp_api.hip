@@ -1279,6 +1279,28 @@ int64_t gp_step(gp_sim* s, int64_t nrounds, int64_t* alerts_out) {
         s->alerts_total = cum;
         s->done = hc.done != 0;
         executed += ex;
+#ifdef GP_EXPERIMENTS
+        if (s->mode != MODE_RCCL && std::getenv("GP_CHECK_CLOSE")) {  // tests: recount the alerts from the state
+            Scratch tmp;
+            unsigned long long* d = nullptr;
+            HIP_TRY(tmp.alloc(&d, 1));
+            HIP_TRY(hipMemsetAsync(d, 0, sizeof(unsigned long long), s->stream));
+            for (Slab& sl : s->slab) {
+                const DevState& S = sl.S;
+                const uint8_t* nb = nullptr;
+                if (S.alg == PUSHSUM) nb = (S.topo == FULL ? S.nb[0] : S.nb[s->rounds_done & 1]) + (S.lo - S.base);
+                HIP_TRY(launch_count_alerted(nb, S.alg == PUSHSUM ? nullptr : S.c, S.nloc, d, s->grid, s->stream));
+            }
+            unsigned long long h = 0;
+            HIP_TRY(hipMemcpyAsync(&h, d, sizeof h, hipMemcpyDeviceToHost, s->stream));
+            HIP_TRY(hipStreamSynchronize(s->stream));
+            if ((int64_t)h != cum) {
+                set_err("round close check: %llu alerted nodes in the state, %lld counted by the round closes", h,
+                        (long long)cum);
+                return GP_ESTATE;
+            }
+        }
+#endif
     }
     return executed;
 }

@@ -318,6 +318,8 @@ hipError_t launch_injector_init(const DevState& S, int grid, hipStream_t st);
 hipError_t launch_bulk(const DevState& S, uint32_t round, int grid, hipStream_t st);
 hipError_t launch_finalize(const DevState& S, uint32_t round_done, uint32_t round_next, hipStream_t st);
 hipError_t launch_finalize_pre(const DevState& S, uint32_t round_next, hipStream_t st);
+hipError_t launch_count_alerted(const uint8_t* nb, const int32_t* c, uint32_t n, unsigned long long* out, int grid,
+                                hipStream_t st);
 hipError_t launch_finalize_post(const DevState& S, uint32_t round_done, uint32_t round_next, hipStream_t st);
 hipError_t launch_full_pushsum_round(const DevState& S, uint32_t round, int grid, hipStream_t st);
 hipError_t launch_iota(uint32_t* v, uint32_t n, int grid, hipStream_t st);

@@ -405,6 +405,28 @@ const char* bulk_kernel_name(const DevState& S) {
     return S.alg == PUSHSUM ? ps[v][S.topo] : go[v][S.topo];
 }
 
+// Experiments build, GP_CHECK_CLOSE=1 (tests): the alert bookkeeping recounted
+// from the node state after a batch, to cross-check the round closes (the fused
+// close orders its shard counts by returning relaxed atomics at the device
+// coherence point, gp_internal.hpp).  Every node alerts once: push-sum when it
+// converges (Program.fs:118-121), gossip on the receipt that takes it past 10
+// rumours (Program.fs:92-94).
+__global__ __launch_bounds__(256) void k_count_alerted(const uint8_t* nb, const int32_t* c, uint32_t n,
+                                                       unsigned long long* out) {
+    uint32_t k = 0;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
+        k += c ? (c[i] > 10 ? 1u : 0u) : ((nb[i] & B_CONV) ? 1u : 0u);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) k += __shfl_xor(k, o, 64);
+    if ((threadIdx.x & 63) == 0 && k) atomicAdd(out, (unsigned long long)k);
+}
+
+hipError_t launch_count_alerted(const uint8_t* nb, const int32_t* c, uint32_t n, unsigned long long* out, int grid,
+                                hipStream_t st) {
+    hipLaunchKernelGGL(k_count_alerted, dim3(grid), dim3(256), 0, st, nb, c, n, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_finalize_pre(const DevState& S, uint32_t round_next, hipStream_t st) {
     const int injector = (S.alg == GOSSIP && S.topo != FULL) ? 1 : 0;
     hipLaunchKernelGGL(k_finalize_pre, dim3(1), dim3(FIN_THREADS), 0, st, S, round_next, injector);

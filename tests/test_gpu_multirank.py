@@ -53,6 +53,7 @@ def test_virtual_ranks_parity(kernel, n, topo, alg, seed, rounds, chk, ranks, mo
     exp = kernel != "default"
     if exp:
         monkeypatch.setenv("GP_KERNEL", kernel)
+        monkeypatch.setenv("GP_CHECK_CLOSE", "1")  # alerts recounted from the state after every batch
     sim = Sim(n, topo, alg, seed=seed, virtual_ranks=ranks, experimental=exp)
     orc = Oracle(n, topo, alg, seed)
     assert sim.info().num_gpus == ranks

@@ -367,8 +367,11 @@ def test_round_close_parity(fuse, n, topo, seed, rounds, chk, monkeypatch):
     GP_FUSE): 0 a separate k_finalize launch, 1 the round kernel's last block via
     one arrival counter, 2 (product default) arrivals sharded over 8 counters whose
     last blocks forward to the global one.  Per-round alerts and full state
-    bit-exact vs the oracle at every checkpoint, through convergence for line."""
+    bit-exact vs the oracle at every checkpoint, through convergence for line.
+    GP_CHECK_CLOSE recounts the alerted nodes from the state after every batch and
+    fails the step if the closes' bookkeeping disagrees."""
     monkeypatch.setenv("GP_FUSE", fuse)
+    monkeypatch.setenv("GP_CHECK_CLOSE", "1")
     sim, orc = Sim(n, topo, "push-sum", seed=seed, experimental=True), Oracle(n, topo, "push-sum", seed)
     done = 0
     while done < rounds and orc.alerts_total < orc.T:
