@@ -11,7 +11,7 @@ every node is active (steady state: every node sends a message each round),
 then W warmup rounds; convergence is never reached inside the timed window.
 
 One JSON line on stdout (rank 0).  `roofline` is measured live: HIP events on
-the library's stream bracket every round kernel (k_ps_col<IMP3D> at this size); its
+the library's stream bracket every round kernel; its
 algorithmic bytes per node-round are DESIGN.md §4's figure.  `traffic` is
 measured in the same run: before the bench, the workload is re-run as a child
 under three rocprofv3 --pmc passes and the round kernel's HBM bytes are read

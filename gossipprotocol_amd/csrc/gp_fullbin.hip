@@ -554,7 +554,7 @@ __global__ __launch_bounds__(FBR_THREADS, GP_FBR_MINB) void k_fbm_coarse(FullBin
 // put in ascending sender order (insertion sort of (sender, LDS position)) and
 // folded from LDS -- no gather of the bin's payloads from global memory.
 #ifndef GP_FBF_THREADS
-#define GP_FBF_THREADS 512
+#define GP_FBF_THREADS 1024
 #endif
 constexpr int FBF_THREADS = GP_FBF_THREADS;
 

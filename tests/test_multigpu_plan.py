@@ -94,8 +94,8 @@ def test_c5_imp3d_pushsum_1e9_world8_plan():
 
 
 def full_bin_plan(nrecv):
-    """gp_fullbin.hip full_bin_plan: coarse bins of 2^s1 receivers, fine tiles of 1024."""
-    fb_tb, cap2 = 10, 1536
+    """gp_fullbin.hip full_bin_plan: coarse bins of 2^s1 receivers, fine tiles of 4096."""
+    fb_tb, cap2 = 12, 4992
     bits = 1
     while bits < 32 and (1 << bits) < nrecv:
         bits += 1
