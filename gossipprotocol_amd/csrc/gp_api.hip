@@ -85,7 +85,7 @@ struct Slab {
     uint8_t* xsend = nullptr;
     uint8_t* xrecv = nullptr;
     uint32_t nedges = 0;
-    std::vector<uint32_t> cap_out, cap_in;
+    std::vector<uint32_t> cap_out, cap_in;           // [h * W + b]: region h of the buffer to / from rank b
     std::vector<size_t> soff, sbytes, roff, rbytes;
     unsigned int* overflow = nullptr;  // device flag
     // full topology over several ranks (gp_full.hip)
@@ -133,6 +133,11 @@ struct gp_sim {
     double kernel_ms = 0.0;
     int64_t launches = 0;
     bool force_tile = false;  // push-sum lattice: the column kernel's capacities were exceeded (build_imp3d)
+    // exchange buffers per rank pair: xhalves regions (2: full-topology push-sum, whose exchange runs
+    // in two halves of each rank's senders on xstream, overlapped with the send / coarse passes)
+    int xhalves = 1;
+    hipStream_t xstream = nullptr;
+    hipEvent_t ev_send[2] = {nullptr, nullptr}, ev_xfer[2] = {nullptr, nullptr};
 };
 
 namespace {
@@ -496,31 +501,38 @@ int build_imp3d(gp_sim* s) {
 int finalize(gp_sim* s, uint32_t round_done, uint32_t round_next);
 
 // Fixed-capacity exchange buffers per rank pair: capacity = expected messages
-// per round + 12 sigma + 64 (never more than the pair's random edges).
+// per round + 12 sigma + 64 (never more than the pair's random edges).  The
+// full-topology push-sum exchange has two regions per pair, one per half of the
+// sender's senders (s->xhalves), moved separately (launch_round_full_multi).
 int setup_exchange(gp_sim* s) {
     const int W = s->world;
     const bool push = s->cfg.algorithm == GP_PUSHSUM;
     const bool full = s->cfg.topology == GP_FULL;
-    std::vector<uint32_t> caps((size_t)W * W, 0);  // caps[a * W + b]: a -> b
+    const int NH = full && push ? 2 : 1;
+    s->xhalves = NH;
+    std::vector<uint32_t> caps((size_t)NH * W * W, 0);  // caps[(h * W + a) * W + b]: a -> b, region h
     Scratch tmp_mem;
     double* mu = nullptr;
     unsigned long long* n = nullptr;
     HIP_TRY(tmp_mem.alloc(&mu, XMAXW));
     HIP_TRY(tmp_mem.alloc(&n, XMAXW));
     if (full) {
-        // every active sender picks a uniform target among P-1: messages a -> b are at
-        // most Binomial(nloc_a, nloc_b / (P-1))
-        for (Slab& sl : s->slab) {
-            const int a = sl.rank;
-            const double na = (double)(s->bounds[a + 1] - s->bounds[a]);
-            for (int b = 0; b < W; ++b) {
-                // push-sum: a rank's messages to itself also pass through a buffer (its
-                // own receive buffer, gp_fullbin.hip k_fbm_send)
-                if (b == a && !push) continue;
-                const double nb = (double)(s->bounds[b + 1] - s->bounds[b]) - (b == a ? 1.0 : 0.0);
-                const double m = na * nb / (double)(s->P - 1);
-                const double c = std::ceil(m + 12.0 * std::sqrt(m) + 64.0);
-                caps[(size_t)a * W + b] = (uint32_t)std::min(c, na);
+        // every active sender picks a uniform target among P-1: messages a -> b from a's half h are
+        // at most Binomial(na_h, nb / (P-1)); a function of the slab bounds only, so every rank
+        // computes the whole table
+        for (int a = 0; a < W; ++a) {
+            const uint32_t na = s->bounds[a + 1] - s->bounds[a];
+            for (int h = 0; h < NH; ++h) {
+                const double nah = (double)(NH == 1 ? na : h == 0 ? na / 2 : na - na / 2);
+                for (int b = 0; b < W; ++b) {
+                    // push-sum: a rank's messages to itself also pass through a buffer (its
+                    // own receive buffer, gp_fullbin.hip k_fbm_send)
+                    if (b == a && !push) continue;
+                    const double nb = (double)(s->bounds[b + 1] - s->bounds[b]) - (b == a ? 1.0 : 0.0);
+                    const double m = nah * nb / (double)(s->P - 1);
+                    const double c = std::ceil(m + 12.0 * std::sqrt(m) + 64.0);
+                    caps[((size_t)h * W + a) * W + b] = (uint32_t)std::min(c, nah);
+                }
             }
         }
     }
@@ -557,7 +569,7 @@ int setup_exchange(gp_sim* s) {
         for (auto& c : caps) c = std::min(c, cap);
     }
 #endif
-    if (s->mode == MODE_RCCL) {
+    if (s->mode == MODE_RCCL && !full) {
         // every rank learns the capacities of the buffers it will receive
         uint32_t* d = nullptr;
         HIP_TRY(tmp_mem.alloc(&d, (size_t)W * W));
@@ -570,49 +582,62 @@ int setup_exchange(gp_sim* s) {
     int rc;
     for (Slab& sl : s->slab) {
         const int a = sl.rank;
-        sl.cap_out.assign(W, 0);
-        sl.cap_in.assign(W, 0);
-        sl.soff.assign(W, 0);
-        sl.sbytes.assign(W, 0);
-        sl.roff.assign(W, 0);
-        sl.rbytes.assign(W, 0);
+        const size_t R = (size_t)NH * W;
+        sl.cap_out.assign(R, 0);
+        sl.cap_in.assign(R, 0);
+        sl.soff.assign(R, 0);
+        sl.sbytes.assign(R, 0);
+        sl.roff.assign(R, 0);
+        sl.rbytes.assign(R, 0);
         size_t so = 0, ro = 0;
-        for (int b = 0; b < W; ++b) {
-            sl.cap_out[b] = caps[(size_t)a * W + b];
-            sl.cap_in[b] = caps[(size_t)b * W + a];
-            sl.soff[b] = so;
-            sl.sbytes[b] = b == a ? 0 : xbuf_bytes(sl.cap_out[b], push);  // own messages: straight to xrecv
-            so += sl.sbytes[b];
-            sl.roff[b] = ro;
-            sl.rbytes[b] = xbuf_bytes(sl.cap_in[b], push);
-            ro += sl.rbytes[b];
-        }
+        for (int h = 0; h < NH; ++h)
+            for (int b = 0; b < W; ++b) {
+                const size_t i = (size_t)h * W + b;
+                sl.cap_out[i] = caps[((size_t)h * W + a) * W + b];
+                sl.cap_in[i] = caps[((size_t)h * W + b) * W + a];
+                sl.soff[i] = so;
+                sl.sbytes[i] = b == a ? 0 : xbuf_bytes(sl.cap_out[i], push);  // own messages: straight to xrecv
+                so += sl.sbytes[i];
+                sl.roff[i] = ro;
+                sl.rbytes[i] = xbuf_bytes(sl.cap_in[i], push);
+                ro += sl.rbytes[i];
+            }
         if ((rc = dev_alloc_t(s, &sl.xsend, so)) || (rc = dev_alloc_t(s, &sl.xrecv, ro))) return rc;
         HIP_TRY(hipMemsetAsync(sl.xsend, 0, so ? so : 16, s->stream));
         HIP_TRY(hipMemsetAsync(sl.xrecv, 0, ro ? ro : 16, s->stream));
         sl.overflow = &sl.S.ctl->overflow;
     }
+    if (NH > 1) {  // the second stream and the events that order it with the compute stream
+        HIP_TRY(hipStreamCreateWithFlags(&s->xstream, hipStreamNonBlocking));
+        for (int h = 0; h < NH; ++h) {
+            HIP_TRY(hipEventCreateWithFlags(&s->ev_send[h], hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&s->ev_xfer[h], hipEventDisableTiming));
+        }
+    }
     return GP_OK;
 }
 
-// Move every rank's exchange buffers to their destinations (device copies for
-// in-process ranks, one RCCL group otherwise).
-int transfer_xbufs(gp_sim* s) {
+// Move region h of every rank's exchange buffers to their destinations on
+// stream st (device copies for in-process ranks, one RCCL group otherwise).
+int transfer_xbufs(gp_sim* s, int h, hipStream_t st) {
     const int W = s->world;
     if (s->mode == MODE_VIRTUAL) {
         for (Slab& a : s->slab)
-            for (Slab& d : s->slab)
-                if (&a != &d && a.sbytes[d.rank])
-                    HIP_TRY(hipMemcpyAsync(d.xrecv + d.roff[a.rank], a.xsend + a.soff[d.rank], a.sbytes[d.rank],
-                                           hipMemcpyDeviceToDevice, s->stream));
+            for (Slab& d : s->slab) {
+                const size_t i = (size_t)h * W + d.rank, j = (size_t)h * W + a.rank;
+                if (&a != &d && a.sbytes[i])
+                    HIP_TRY(hipMemcpyAsync(d.xrecv + d.roff[j], a.xsend + a.soff[i], a.sbytes[i],
+                                           hipMemcpyDeviceToDevice, st));
+            }
         return GP_OK;
     }
     Slab& sl = s->slab[0];
     NCCL_TRY(ncclGroupStart());
     for (int p = 0; p < W; ++p) {
         if (p == sl.rank) continue;
-        if (sl.sbytes[p]) NCCL_TRY(ncclSend(sl.xsend + sl.soff[p], sl.sbytes[p], ncclUint8, p, s->comm, s->stream));
-        if (sl.rbytes[p]) NCCL_TRY(ncclRecv(sl.xrecv + sl.roff[p], sl.rbytes[p], ncclUint8, p, s->comm, s->stream));
+        const size_t i = (size_t)h * W + p;
+        if (sl.sbytes[i]) NCCL_TRY(ncclSend(sl.xsend + sl.soff[i], sl.sbytes[i], ncclUint8, p, s->comm, st));
+        if (sl.rbytes[i]) NCCL_TRY(ncclRecv(sl.xrecv + sl.roff[i], sl.rbytes[i], ncclUint8, p, s->comm, st));
     }
     NCCL_TRY(ncclGroupEnd());
     return GP_OK;
@@ -648,10 +673,10 @@ FullArgs make_full_args(gp_sim* s, Slab& sl, uint32_t round) {
 }
 
 // Push-sum on the full topology, one rank of several (gp_fullbin.hip): this
-// rank's receivers [lo, lo + nloc), node arrays indexed by id - lo, the exchange
-// buffers as the destination-rank bins of k_fbm_send and the sources of
-// k_fbm_coarse.
-FullBinArgs make_fullbin_args(gp_sim* s, Slab& sl, uint32_t round) {
+// rank's receivers [lo, lo + nloc), node arrays indexed by id - lo, region h of
+// the exchange buffers as the destination-rank bins of k_fbm_send (senders of
+// half h) and the sources of k_fbm_coarse.
+FullBinArgs make_fullbin_args(gp_sim* s, Slab& sl, uint32_t round, int h) {
     DevState& S = sl.S;
     const int cur = round & 1;
     const uint32_t d = S.lo - S.base;
@@ -677,54 +702,76 @@ FullBinArgs make_fullbin_args(gp_sim* s, Slab& sl, uint32_t round) {
     a.pay2 = S.fb_pay2;
     a.lo = S.lo;
     a.nloc = S.nloc;
+    const int NH = s->xhalves;
+    a.s_lo = NH == 1 || h == 0 ? 0u : S.nloc / 2;
+    a.s_hi = NH == 1 || h == 1 ? S.nloc : S.nloc / 2;
     a.W = s->world;
     a.me = sl.rank;
     for (int w = 0; w <= s->world; ++w) a.bounds[w] = s->bounds[w];
     const uint32_t item = full_bin_item_messages();
     a.in_item0[0] = 0;
     for (int p = 0; p < s->world; ++p) {
-        a.in[p] = xpeer(sl.xrecv, sl.roff[p], sl.cap_in[p]);
-        a.out[p] = p == sl.rank ? a.in[p] : xpeer(sl.xsend, sl.soff[p], sl.cap_out[p]);
-        a.in_item0[p + 1] = a.in_item0[p] + (item ? (sl.cap_in[p] + item - 1) / item : 0u);
+        const size_t i = (size_t)h * s->world + p;
+        a.in[p] = xpeer(sl.xrecv, sl.roff[i], sl.cap_in[i]);
+        a.out[p] = p == sl.rank ? a.in[p] : xpeer(sl.xsend, sl.soff[i], sl.cap_out[i]);
+        a.in_item0[p + 1] = a.in_item0[p] + (item ? (sl.cap_in[i] + item - 1) / item : 0u);
     }
     return a;
 }
 
 // Full topology on several ranks: one round (push-sum gp_fullbin.hip, gossip gp_full.hip).
+// Push-sum runs as a two-stage pipeline: the senders' first half is binned by
+// destination and handed to the exchange stream (xstream), whose transfer
+// overlaps the second half's binning; the receivers bin half 0's messages by
+// coarse bin while half 1 is in flight, then half 1's, then split and fold.
+// Events order the two streams; every RCCL operation stays serialised in one
+// order on every rank (group half 0, group half 1, then the finalize all-reduce).
 int launch_round_full_multi(gp_sim* s, uint32_t r, hipEvent_t e0, hipEvent_t e1) {
     const bool push = s->cfg.algorithm == GP_PUSHSUM;
     int rc;
     if (e0) HIP_TRY(hipEventRecord(e0, s->stream));
-    for (Slab& sl : s->slab) {
-        if (push) {
-            const FullBinArgs a = make_fullbin_args(s, sl, r);
-            ZeroArgs z{};
-            for (int p = 0; p < s->world; ++p) z.cnt[p] = a.out[p].cnt;
-            z.n = s->world;
-            HIP_TRY(launch_zero_counts(z, s->stream));
-            HIP_TRY(launch_full_bin_send_multi(a, r, s->stream));
-            continue;
+    if (push) {
+        const int NH = s->xhalves;
+        hipStream_t xs = s->xstream ? s->xstream : s->stream;
+        for (int h = 0; h < NH; ++h) {
+            for (Slab& sl : s->slab) {
+                const FullBinArgs a = make_fullbin_args(s, sl, r, h);
+                ZeroArgs z{};
+                for (int p = 0; p < s->world; ++p) z.cnt[p] = a.out[p].cnt;
+                z.n = s->world;
+                HIP_TRY(launch_zero_counts(z, s->stream));
+                HIP_TRY(launch_full_bin_send_multi(a, r, s->stream));
+            }
+            if (xs != s->stream) {
+                HIP_TRY(hipEventRecord(s->ev_send[h], s->stream));
+                HIP_TRY(hipStreamWaitEvent(xs, s->ev_send[h], 0));
+            }
+            if ((rc = transfer_xbufs(s, h, xs))) return rc;
+            if (xs != s->stream) HIP_TRY(hipEventRecord(s->ev_xfer[h], xs));
         }
-        FullArgs a = make_full_args(s, sl, r);
-        {
-            ZeroArgs z{};
-            for (int p = 0; p < s->world; ++p) z.cnt[p] = a.peer[p].cnt;
-            z.n = s->world;
-            HIP_TRY(launch_zero_counts(z, s->stream));
-            HIP_TRY(launch_fullm_gossip_send(a, r, s->grid, s->stream));
+        for (Slab& sl : s->slab) HIP_TRY(launch_full_bin_recv_reset(make_fullbin_args(s, sl, r, 0), s->stream));
+        for (int h = 0; h < NH; ++h) {
+            if (xs != s->stream) HIP_TRY(hipStreamWaitEvent(s->stream, s->ev_xfer[h], 0));
+            for (Slab& sl : s->slab) HIP_TRY(launch_full_bin_coarse(make_fullbin_args(s, sl, r, h), r, s->stream));
         }
+        for (Slab& sl : s->slab)
+            HIP_TRY(launch_full_bin_split_fold(make_fullbin_args(s, sl, r, 0), r, s->grid, s->stream));
+        if (e1) HIP_TRY(hipEventRecord(e1, s->stream));
+        return finalize(s, r, r + 1);
     }
-    if ((rc = transfer_xbufs(s))) return rc;
     for (Slab& sl : s->slab) {
-        if (push) {
-            HIP_TRY(launch_full_bin_recv_multi(make_fullbin_args(s, sl, r), r, s->grid, s->stream));
-            continue;
-        }
         FullArgs a = make_full_args(s, sl, r);
-        {
-            HIP_TRY(launch_fullm_gossip_unpack(a, std::max(1, s->grid / 8), s->stream));
-            HIP_TRY(launch_fullm_gossip_recv(a, s->grid, s->stream));
-        }
+        ZeroArgs z{};
+        for (int p = 0; p < s->world; ++p) z.cnt[p] = a.peer[p].cnt;
+        z.n = s->world;
+        HIP_TRY(launch_zero_counts(z, s->stream));
+        HIP_TRY(launch_fullm_gossip_send(a, r, s->grid, s->stream));
+    }
+    if ((rc = transfer_xbufs(s, 0, s->stream))) return rc;
+    for (Slab& sl : s->slab) {
+        FullArgs a = make_full_args(s, sl, r);
+        HIP_TRY(launch_fullm_gossip_unpack(a, std::max(1, s->grid / 8), s->stream));
+        HIP_TRY(launch_fullm_gossip_recv(a, s->grid, s->stream));
     }
     if (e1) HIP_TRY(hipEventRecord(e1, s->stream));
     return finalize(s, r, r + 1);
@@ -783,7 +830,7 @@ int exchange(gp_sim* s, uint32_t rn) {
             }
         }
         if (imp) {
-            int rc = transfer_xbufs(s);
+            int rc = transfer_xbufs(s, 0, s->stream);
             if (rc) return rc;
         }
     } else {
@@ -1478,11 +1525,17 @@ void gp_destroy(gp_sim* s) {
     if (!s) return;
     (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
+    if (s->xstream) (void)hipStreamSynchronize(s->xstream);
     for (auto& e : s->ev) (void)hipEventDestroy(e);
+    for (int h = 0; h < 2; ++h) {
+        if (s->ev_send[h]) (void)hipEventDestroy(s->ev_send[h]);
+        if (s->ev_xfer[h]) (void)hipEventDestroy(s->ev_xfer[h]);
+    }
     if (s->comm) (void)ncclCommDestroy(s->comm);
     free_all(s);
     if (s->host_ctl) (void)hipHostFree(s->host_ctl);
     if (s->stream) (void)hipStreamDestroy(s->stream);
+    if (s->xstream) (void)hipStreamDestroy(s->xstream);
     delete s;
 }
 

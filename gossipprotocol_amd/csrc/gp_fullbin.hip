@@ -402,9 +402,9 @@ __global__ __launch_bounds__(FBR_THREADS, GP_FBR_MINB) void k_fbm_send(FullBinAr
     if (ld_agent(&a.ctl->done)) return;
     const uint32_t P = a.P;
     const int W = a.W;
-    const uint64_t i0 = (uint64_t)blockIdx.x * FBR_ITEM;
-    if (i0 >= a.nloc || P < 2) return;
-    const uint64_t i1 = std::min<uint64_t>(a.nloc, i0 + FBR_ITEM);
+    const uint64_t i0 = (uint64_t)a.s_lo + (uint64_t)blockIdx.x * FBR_ITEM;
+    if (i0 >= a.s_hi || P < 2) return;
+    const uint64_t i1 = std::min<uint64_t>(a.s_hi, i0 + FBR_ITEM);
     uint32_t* const cnt = fbr_dyn;
     uint32_t* const base = fbr_dyn + W;
     if (threadIdx.x < (uint32_t)W) {
@@ -718,18 +718,25 @@ uint32_t full_bin_item_messages() {
 }
 
 hipError_t launch_full_bin_send_multi(const FullBinArgs& a, uint32_t round, hipStream_t st) {
-    const uint32_t items = (uint32_t)(((uint64_t)a.nloc + FBR_ITEM - 1) / FBR_ITEM);
+    const uint32_t items = (uint32_t)(((uint64_t)(a.s_hi - a.s_lo) + FBR_ITEM - 1) / FBR_ITEM);
     if (items) hipLaunchKernelGGL(k_fbm_send, dim3(items), dim3(FBR_THREADS), 2 * sizeof(uint32_t) * a.W, st, a, round);
     return hipGetLastError();
 }
 
-hipError_t launch_full_bin_recv_multi(const FullBinArgs& a, uint32_t round, int grid, hipStream_t st) {
+hipError_t launch_full_bin_recv_reset(const FullBinArgs& a, hipStream_t st) {
     hipError_t e;
     if ((e = hipMemsetAsync(a.cnt1, 0, sizeof(uint32_t) * a.nb1, st)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(a.cnt2, 0, sizeof(uint32_t) * a.nb2, st)) != hipSuccess) return e;
+    return hipMemsetAsync(a.cnt2, 0, sizeof(uint32_t) * a.nb2, st);
+}
+
+hipError_t launch_full_bin_coarse(const FullBinArgs& a, uint32_t round, hipStream_t st) {
     if (a.in_item0[a.W])
         hipLaunchKernelGGL(k_fbm_coarse, dim3(a.in_item0[a.W]), dim3(FBR_THREADS), 2 * sizeof(uint32_t) * a.nb1, st, a,
                            round);
+    return hipGetLastError();
+}
+
+hipError_t launch_full_bin_split_fold(const FullBinArgs& a, uint32_t round, int grid, hipStream_t st) {
     const uint32_t items_b = a.nb1 * ((a.cap1 + FBR_ITEM - 1) / FBR_ITEM);
     hipLaunchKernelGGL(k_fb_split, dim3(items_b), dim3(FBR_THREADS), 2 * sizeof(uint32_t) * (1u << (a.s1 - FB_TB)), st,
                        a, round);

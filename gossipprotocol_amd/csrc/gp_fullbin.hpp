@@ -39,6 +39,7 @@ struct FullBinArgs {
     // arrays (swc, swn, nb) are indexed by id - lo, coarse bins and fine tiles count
     // from lo
     uint32_t lo, nloc;
+    uint32_t s_lo, s_hi;  // several ranks: k_fbm_send bins the senders lo + [s_lo, s_hi) (a half of the slab)
     // several ranks (k_fbm_send / k_fbm_coarse): senders' messages binned by
     // destination rank into the exchange buffers, then the received ones by coarse bin
     int W, me;
@@ -50,10 +51,14 @@ struct FullBinArgs {
 
 FullBinPlan full_bin_plan(uint32_t nrecv);
 hipError_t launch_full_bin_round(const FullBinArgs& a, uint32_t round, int grid, hipStream_t st);
-// several ranks: messages into the exchange buffers (before the exchange) ...
+// several ranks: messages of the senders [s_lo, s_hi) into the exchange buffers (before the
+// exchange) ...
 hipError_t launch_full_bin_send_multi(const FullBinArgs& a, uint32_t round, hipStream_t st);
-// ... and the received messages binned, split and folded (after it)
-hipError_t launch_full_bin_recv_multi(const FullBinArgs& a, uint32_t round, int grid, hipStream_t st);
+// ... then, per round, the bin counters reset, the received messages of each exchange region
+// binned by coarse bin, and the split and fold
+hipError_t launch_full_bin_recv_reset(const FullBinArgs& a, hipStream_t st);
+hipError_t launch_full_bin_coarse(const FullBinArgs& a, uint32_t round, hipStream_t st);
+hipError_t launch_full_bin_split_fold(const FullBinArgs& a, uint32_t round, int grid, hipStream_t st);
 uint32_t full_bin_item_messages();
 
 }  // namespace gp

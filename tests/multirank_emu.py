@@ -20,8 +20,8 @@ ranks only through the library's exchange plan:
   * full topology: contiguous id slabs, no halo.  Push-sum (gp_fullbin.hip
     k_fbm_send / k_fbm_coarse): every rank bins its messages {sender id, s/2,
     w/2} by destination rank -- its own share included -- into fixed-capacity
-    buffers (expected + 12 sigma + 64, an overflow fails) in no particular
-    order (shuffled here); the receiver recomputes every target from the
+    buffers (expected + 12 sigma + 64, an overflow fails), one region per half
+    of its slab, exchanged separately, in no particular order (shuffled here); the receiver recomputes every target from the
     sender's Philox draw and folds each receiver's messages by ascending sender
     id.  Gossip (gp_full.hip): deliveries are counts added by the owner.
 
@@ -398,25 +398,32 @@ class RankSim:
         return tt[o2], [c[o2] for c in cols]
 
     def _full_pushsum_exchange(self, snd, t, payload):
-        """Push-sum messages -> this rank's receivers (gp_fullbin.hip several ranks):
-        binned by destination rank in arbitrary order, capacity-checked (own share
-        included), targets recomputed by the receiver, each receiver's messages put
-        in ascending sender order.  Returns local receiver ids and payload columns."""
+        """Push-sum messages -> this rank's receivers (gp_fullbin.hip several ranks,
+        gp_api.hip launch_round_full_multi): the senders of each half of the slab
+        ([lo, lo + n/2), [lo + n/2, hi)) are binned by destination rank in arbitrary
+        order into their own fixed-capacity region (own share included) and
+        exchanged separately; the receiver recomputes the targets and puts each
+        receiver's messages in ascending sender order.  Returns local receiver ids
+        and payload columns."""
         owner = np.searchsorted(np.array(self.bounds), t, side="right") - 1
         rng = np.random.default_rng(self.round * 7919 + self.rank)  # buffer order is arbitrary
-        packets = {}
-        for b in range(self.W):
-            sel = np.nonzero(owner == b)[0]
-            nb = self.bounds[b + 1] - self.bounds[b] - (1 if b == self.rank else 0)
-            assert len(sel) <= full_capacity(self.hi - self.lo, nb, self.P), "exchange capacity exceeded"
-            sel = rng.permutation(sel)
-            packets[b] = (snd[sel],) + tuple(p[sel] for p in payload)
-        got = [None] * self.W
-        if self.W > 1:
-            self.dist.all_gather_object(got, packets)
-        else:
-            got = [packets]
-        parts = [got[src][self.rank] for src in range(self.W)]
+        n = self.hi - self.lo
+        cut = self.lo + n // 2
+        parts = []
+        for h, (h_lo, h_hi) in enumerate(((self.lo, cut), (cut, self.hi))):
+            packets = {}
+            for b in range(self.W):
+                sel = np.nonzero((owner == b) & (snd >= h_lo) & (snd < h_hi))[0]
+                nb = self.bounds[b + 1] - self.bounds[b] - (1 if b == self.rank else 0)
+                assert len(sel) <= full_capacity(h_hi - h_lo, nb, self.P), "exchange capacity exceeded"
+                sel = rng.permutation(sel)
+                packets[b] = (snd[sel],) + tuple(p[sel] for p in payload)
+            got = [None] * self.W
+            if self.W > 1:
+                self.dist.all_gather_object(got, packets)
+            else:
+                got = [packets]
+            parts += [got[src][self.rank] for src in range(self.W)]
         src = np.concatenate([p[0] for p in parts]).astype(np.int64)
         cols = [np.concatenate([p[1 + q] for p in parts]) for q in range(len(payload))]
         tt = full_target(src, uniform(self.seed, S_PUSHSUM, src, self.round, self.P - 1)) - self.lo

@@ -112,22 +112,29 @@ def full_bin_plan(nrecv):
 
 def test_c4_full_pushsum_1e8_world8_plan():
     """Several ranks (gp_fullbin.hip k_fbm_send / k_fbm_coarse): every rank's messages to
-    rank b -- itself included -- go through a fixed-capacity buffer, then the receiver bins
-    them by coarse bin and fine tile of its own receivers."""
+    rank b -- itself included -- go through fixed-capacity buffers, one region per half of
+    the sender's slab (the two halves are exchanged separately, gp_api.hip
+    launch_round_full_multi), then the receiver bins them by coarse bin and fine tile of
+    its own receivers."""
     P, T, _ = resolve(10**8, "full")
     W = 8
     bounds, halo = slab_bounds(P, 0, "full", W)
     assert halo == 0 and bounds[-1] == P
+
+    def halves(n):
+        return (n // 2, n - n // 2)
+
     for a in range(W):
         na = bounds[a + 1] - bounds[a]
         caps_in = []
         for b in range(W):
             nb = bounds[b + 1] - bounds[b] - (1 if b == a else 0)  # no message to oneself
-            m = na * nb / (P - 1)
-            sd = math.sqrt(m * (1 - nb / (P - 1)))
-            assert (full_capacity(na, nb, P) - m) / sd >= 12.0
+            for nah in halves(na):
+                m = nah * nb / (P - 1)
+                sd = math.sqrt(m * (1 - nb / (P - 1)))
+                assert (full_capacity(nah, nb, P) - m) / sd >= 12.0
             nsrc = bounds[b + 1] - bounds[b]
-            caps_in.append(full_capacity(nsrc, na - (1 if b == a else 0), P))
+            caps_in += [full_capacity(nsh, na - (1 if b == a else 0), P) for nsh in halves(nsrc)]
         nb1, cap1, nb2, cap2 = full_bin_plan(na)
         assert nb1 < 4096 and nb2 * cap2 < 2**32
         # a coarse bin receives Binomial(sum of senders, 2^s1 / (P - 1)) messages: 12 sigma + 1024

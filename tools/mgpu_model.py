@@ -64,9 +64,10 @@ def run(n, topo, alg, W, rounds):
     s.close()
 
 
-def pair_bytes(n, topo, alg, W):
-    """Bytes rank a sends rank b per round (fixed-capacity buffer incl. its 16-B count
-    header) and the halo bytes per neighbouring pair and direction."""
+def pair_bytes(n, topo, alg, W, halves=1):
+    """Bytes rank a sends rank b per round (fixed-capacity buffers incl. their 16-B count
+    headers; full push-sum: `halves` regions, one per half of a's senders) and the halo
+    bytes per neighbouring pair and direction."""
     from tests.multirank_emu import full_capacity, resolve, slab_bounds
     from tests.test_multigpu_plan import cap_of, imp3d_pair_stats
     P, _, g = resolve(n, topo)
@@ -81,9 +82,10 @@ def pair_bytes(n, topo, alg, W):
         bounds, _ = slab_bounds(P, g, topo, W)
         for a in range(W):
             na = bounds[a + 1] - bounds[a]
+            parts = (na,) if halves == 1 else (na // 2, na - na // 2)
             for b in range(W):
                 if b != a:
-                    B[a][b] = xbuf(full_capacity(na, bounds[b + 1] - bounds[b], P))
+                    B[a][b] = sum(xbuf(full_capacity(nh, bounds[b + 1] - bounds[b], P)) for nh in parts)
     else:
         bounds, H = slab_bounds(P, g, topo, W)
         halo = H * (1 + (16 if push else 0))
@@ -139,10 +141,30 @@ def model(tdir, n, topo, alg, W, rounds, out=None):
         copy_ms.append(cp)
         for k in range(W):
             rank_ms[k].append(tr[k])
-    P, bounds, B, halo = pair_bytes(n, topo, alg, W)
+    # full push-sum runs its exchange in two halves overlapped with the send / coarse
+    # passes (gp_api.hip launch_round_full_multi): those kernels appear twice per slab
+    halves = 2 if topo == "full" and alg == "push-sum" else 1
+    P, bounds, B, halo = pair_bytes(n, topo, alg, W, halves)
     kern = {k: [statistics.mean(x[s] for x in v) for s in range(W)] for k, v in per_slab.items()}
     comp = [statistics.mean(v) for v in rank_ms]
     t_comp = max(comp)
+    piped = None
+    if halves == 2:
+        # per rank: send half 0, half 1; coarse half 0, half 1 (dispatch order), the rest
+        hk = {}
+        for grp in groups:
+            by = {}
+            for name, ms in grp:
+                by.setdefault(short(name), []).append(ms)
+            for nm in ("k_fbm_send", "k_fbm_coarse"):
+                v = by.get(nm, [])
+                if len(v) == 2 * W:
+                    hk.setdefault(nm, []).append(v)
+        if len(hk.get("k_fbm_send", [])) and len(hk.get("k_fbm_coarse", [])):
+            s_h = [[statistics.mean(x[h * W + k] for x in hk["k_fbm_send"]) for k in range(W)] for h in range(2)]
+            c_h = [[statistics.mean(x[h * W + k] for x in hk["k_fbm_coarse"]) for k in range(W)] for h in range(2)]
+            piped = {"send_half_ms": [max(v) for v in s_h], "coarse_half_ms": [max(v) for v in c_h],
+                     "rest_ms": max(comp[k] - s_h[0][k] - s_h[1][k] - c_h[0][k] - c_h[1][k] for k in range(W))}
     res = {"workload": f"{alg} {topo} n={n} P={P}", "W": W, "rounds_measured": len(groups),
            "per_slab_kernel_ms": {k: [round(x, 4) for x in v] for k, v in kern.items()},
            "global_kernel_ms": {k: round(statistics.mean(v), 4) for k, v in glob_k.items()},
@@ -152,7 +174,7 @@ def model(tdir, n, topo, alg, W, rounds, out=None):
            "halo_bytes_per_direction": halo, "assumptions": {
                "link_gbps_per_direction": LINK_GBPS, "group_latency_ms": GROUP_LAT_MS,
                "allreduce_latency_ms": ALLREDUCE_LAT_MS, "topology": "one xGMI link per rank pair (8-GPU node)"},
-           "model": []}
+           "model": [], "pipelined_halves": piped}
     for bw in LINK_GBPS:
         # the busiest link: a pair's buffer plus, between slab neighbours, the halo plane
         link = 0.0
@@ -160,10 +182,19 @@ def model(tdir, n, topo, alg, W, rounds, out=None):
             for b in range(W):
                 if a != b:
                     link = max(link, B[a][b] + (halo if abs(a - b) == 1 else 0))
-        t_x = link / (bw * 1e9) * 1e3 + (GROUP_LAT_MS if link else 0.0)
+        t_x = link / (bw * 1e9) * 1e3 + (GROUP_LAT_MS if link else 0.0) * halves
         serial = t_comp + t_x + ALLREDUCE_LAT_MS
         overlap = max(t_comp, t_x) + ALLREDUCE_LAT_MS
+        if piped:  # as scheduled: x_h after send_h, coarse_h after x_h (one exchange stream)
+            xh = t_x / 2
+            s0, s1 = piped["send_half_ms"]
+            c0, c1 = piped["coarse_half_ms"]
+            x0_end = s0 + xh
+            x1_end = max(x0_end, s0 + s1) + xh
+            c_end = max(max(s0 + s1, x0_end) + c0, x1_end) + c1
+            overlap = c_end + piped["rest_ms"] + ALLREDUCE_LAT_MS
         res["model"].append({"link_gbps": bw, "exchange_ms": round(t_x, 4), "round_ms_serial": round(serial, 4),
+                             "round_ms_as_scheduled": round(overlap, 4) if piped else round(serial, 4),
                              "exchange_share_serial": round(t_x / serial, 3), "round_ms_overlapped": round(overlap, 4),
                              "node_updates_per_s_serial": P / (serial * 1e-3),
                              "node_updates_per_s_overlapped": P / (overlap * 1e-3)})
