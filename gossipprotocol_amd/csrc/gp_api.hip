@@ -132,7 +132,6 @@ struct gp_sim {
     std::vector<hipEvent_t> ev;
     double kernel_ms = 0.0;
     int64_t launches = 0;
-    bool force_tile = false;  // push-sum lattice: the column kernel's capacities were exceeded (build_imp3d)
     // exchange buffers per rank pair: xhalves regions (2: full-topology push-sum, whose exchange runs
     // in two halves of each rank's senders on xstream, overlapped with the send / coarse passes)
     int xhalves = 1;
@@ -335,46 +334,20 @@ int alloc_slab(gp_sim* s, Slab& sl, int r) {
 
 // Imp3D: draw rnd[] for every node (Program.fs:258-260), then a stable sort of
 // (key(rnd[i]), i) by key gives every receiver's senders in ascending id order,
-// and the exclusive scan of the per-key in-degrees the CSR offsets.  The key is
-// the receiver id (tile / gossip kernels: in_off, in_src in id order) or, for
-// the push-sum column kernel, its patch key (gp_pscol.hip: one contiguous edge
-// range per plane of a patch, pc_soff / pc_src / pc_ind4).  Every rank builds
-// the global order (it is deterministic; ranks own consecutive key ranges) and
-// keeps its receivers' slice; with several ranks, each local sender also learns
-// the position of its message in the destination's in-edge array (pos).
-// Returns GP_ERETRY_TILE when the patch-order lists exceed the column kernel's
-// static capacities (a receiver with >= 15 in-edges, or a step with more
-// in-edges than it stages): the caller rebuilds with the tile kernel.
-constexpr int GP_ERETRY_TILE = -100;
+// and the exclusive scan of the per-receiver in-degrees the CSR offsets (in_off,
+// in_src in id order).  Every rank builds the global order (it is
+// deterministic; ranks own consecutive id ranges) and keeps its
+// receivers' slice; with several ranks, each local sender also learns the
+// position of its message in the destination's in-edge array (pos).
 
 int build_imp3d(gp_sim* s) {
     const uint32_t P = (uint32_t)s->P;
     const int W = s->world;
     DevState& S0 = s->slab[0].S;
-    const bool pscol = S0.alg == PUSHSUM && S0.kernel == KERNEL_COL;
     Scratch tmp_mem;  // setup temporaries, freed on every exit path
     uint32_t *rnd_all = nullptr, *iota = nullptr, *keys_sorted = nullptr, *src_sorted = nullptr, *counts = nullptr,
-             *off_all = nullptr, *inv = nullptr, *key_all = nullptr;
-    // key space: receiver ids, or patch keys (planes x patch rows x z-segments x 64)
-    PcKeyPlan kp{};
-    uint64_t nkeys = P;
-    if (pscol) {
-        const uint32_t rows = pscol_patch_rows(), g = (uint32_t)s->g;
-        const uint64_t per_plane = (uint64_t)((g + rows - 1) / rows) * ((g + 63) / 64) * rows * 64;
-        kp.W = W;
-        kp.zs = (g + 63) / 64;
-        uint64_t kb = 0;
-        for (int w = 0; w <= W; ++w) {
-            kp.x_lo[w] = (uint32_t)(s->bounds[w] / (s->g * s->g));
-            kp.kbase[w] = (uint32_t)kb;
-            if (w < W) kb += per_plane * ((s->bounds[w + 1] - s->bounds[w]) / (s->g * s->g));
-        }
-        nkeys = kb;
-        if (nkeys >= 0xFFFFFFFFull) {
-            set_err("internal: patch key space of %llu keys", (unsigned long long)nkeys);
-            return GP_ERETRY_TILE;
-        }
-    }
+             *off_all = nullptr, *inv = nullptr;
+    const uint64_t nkeys = P;
     HIP_TRY(tmp_mem.alloc(&rnd_all, P));
     HIP_TRY(tmp_mem.alloc(&iota, P));
     HIP_TRY(tmp_mem.alloc(&keys_sorted, P));
@@ -383,19 +356,14 @@ int build_imp3d(gp_sim* s) {
     HIP_TRY(tmp_mem.alloc(&off_all, (size_t)nkeys + 1));
     HIP_TRY(launch_topo_rnd_range(S0.k0, S0.k1, P, 0, P, rnd_all, s->grid, s->stream));
     HIP_TRY(launch_iota(iota, P, s->grid, s->stream));
-    key_all = rnd_all;
-    if (pscol) {
-        HIP_TRY(tmp_mem.alloc(&key_all, P));
-        HIP_TRY(launch_pc_keys(rnd_all, P, key_all, S0.G, kp, s->grid, s->stream));
-    }
     const uint32_t bits = bits_for(nkeys > 1 ? nkeys - 1 : 0);
     size_t tmp_bytes = 0;
-    HIP_TRY(sort_pairs(nullptr, tmp_bytes, key_all, keys_sorted, iota, src_sorted, P, bits, s->stream));
+    HIP_TRY(sort_pairs(nullptr, tmp_bytes, rnd_all, keys_sorted, iota, src_sorted, P, bits, s->stream));
     uint8_t* tmp = nullptr;
     HIP_TRY(tmp_mem.alloc(&tmp, tmp_bytes ? tmp_bytes : 4));
-    HIP_TRY(sort_pairs(tmp, tmp_bytes, key_all, keys_sorted, iota, src_sorted, P, bits, s->stream));
+    HIP_TRY(sort_pairs(tmp, tmp_bytes, rnd_all, keys_sorted, iota, src_sorted, P, bits, s->stream));
     HIP_TRY(hipMemsetAsync(counts, 0, sizeof(uint32_t) * ((size_t)nkeys + 1), s->stream));
-    HIP_TRY(launch_histogram(key_all, P, counts, s->grid, s->stream));
+    HIP_TRY(launch_histogram(rnd_all, P, counts, s->grid, s->stream));
     size_t scan_bytes = 0;
     HIP_TRY(exclusive_scan_u32(nullptr, scan_bytes, counts, off_all, (uint32_t)nkeys + 1, s->stream));
     uint8_t* scan_tmp = nullptr;
@@ -408,8 +376,7 @@ int build_imp3d(gp_sim* s) {
     // first global edge of every rank
     std::vector<uint32_t> edge0(W + 1);
     for (int w = 0; w <= W; ++w)
-        HIP_TRY(hipMemcpyAsync(&edge0[w], off_all + (pscol ? kp.kbase[w] : s->bounds[w]), sizeof(uint32_t),
-                               hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(hipMemcpyAsync(&edge0[w], off_all + s->bounds[w], sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
     int rc;
     for (Slab& sl : s->slab) {
@@ -420,44 +387,16 @@ int build_imp3d(gp_sim* s) {
         S.nedges = ne;
         if ((rc = dev_alloc_t(s, &S.rnd, S.nloc))) return rc;
         HIP_TRY(hipMemcpyAsync(S.rnd, rnd_all + S.lo, sizeof(uint32_t) * S.nloc, hipMemcpyDeviceToDevice, s->stream));
-        if (pscol) {
-            // patch-order lists (gp_pscol.hip); the senders carry deg - 4 in bits 30-31
-            const uint32_t nsteps = (uint32_t)((kp.kbase[r + 1] - kp.kbase[r]) / pscol_step_receivers());
-            S.pc_nsteps = nsteps;
-            uint32_t* stat = nullptr;
-            if ((rc = dev_alloc_t(s, &S.pc_src, (size_t)ne + 8)) ||
-                (rc = dev_alloc_t(s, &S.pc_soff, (size_t)nsteps + 2)) ||
-                (rc = dev_alloc_t(s, &S.pc_ind4, (size_t)nsteps * (pscol_step_receivers() / 2) + 64)))
-                return rc;
-            HIP_TRY(tmp_mem.alloc(&stat, 2));
-            HIP_TRY(hipMemsetAsync(stat, 0, sizeof(uint32_t) * 2, s->stream));
-            HIP_TRY(hipMemsetAsync(S.pc_src, 0, sizeof(uint32_t) * ((size_t)ne + 8), s->stream));
-            if (ne) HIP_TRY(launch_pack_src_deg(src_sorted + edge0[r], S.pc_src, ne, S.G, s->grid, s->stream));
-            HIP_TRY(launch_pc_slab(off_all, counts, kp.kbase[r], nsteps, edge0[r], S.pc_soff, S.pc_ind4, stat,
-                                   s->grid, s->stream));
-            uint32_t hs[2] = {0, 0};
-            HIP_TRY(hipMemcpyAsync(hs, stat, sizeof hs, hipMemcpyDeviceToHost, s->stream));
-            HIP_TRY(hipStreamSynchronize(s->stream));
-            uint32_t deg_cap = 14;
-#ifdef GP_EXPERIMENTS
-            if (const char* e = std::getenv("GP_PSCOL_DEGCAP")) deg_cap = (uint32_t)std::atoi(e);  // tests: force the fallback
-#endif
-            if (hs[0] > deg_cap || hs[1] > pscol_step_capacity()) {
-                set_err("push-sum column kernel: in-degree %u / step in-edges %u above its capacity", hs[0], hs[1]);
-                return GP_ERETRY_TILE;
-            }
-        } else {
-            // in-lists padded by 4 words: the tile kernels stage them with 16-byte LDS-DMA
-            if ((rc = dev_alloc_t(s, &S.in_off, (size_t)S.nloc + 1 + 4)) ||
-                (rc = dev_alloc_t(s, &S.in_src, (size_t)ne + 4)))
-                return rc;
-            HIP_TRY(hipMemcpyAsync(S.in_off, off_all + S.lo, sizeof(uint32_t) * ((size_t)S.nloc + 1),
+        // in-lists padded by 4 words: the tile kernels stage them with 16-byte LDS-DMA
+        if ((rc = dev_alloc_t(s, &S.in_off, (size_t)S.nloc + 1 + 4)) ||
+            (rc = dev_alloc_t(s, &S.in_src, (size_t)ne + 4)))
+            return rc;
+        HIP_TRY(hipMemcpyAsync(S.in_off, off_all + S.lo, sizeof(uint32_t) * ((size_t)S.nloc + 1),
+                               hipMemcpyDeviceToDevice, s->stream));
+        HIP_TRY(launch_sub(S.in_off, S.nloc + 1, edge0[r], s->grid, s->stream));
+        if (ne)
+            HIP_TRY(hipMemcpyAsync(S.in_src, src_sorted + edge0[r], sizeof(uint32_t) * ne,
                                    hipMemcpyDeviceToDevice, s->stream));
-            HIP_TRY(launch_sub(S.in_off, S.nloc + 1, edge0[r], s->grid, s->stream));
-            if (ne)
-                HIP_TRY(hipMemcpyAsync(S.in_src, src_sorted + edge0[r], sizeof(uint32_t) * ne,
-                                       hipMemcpyDeviceToDevice, s->stream));
-        }
         S.in_srcd = nullptr;
         bool pack = true;
 #ifdef GP_EXPERIMENTS
@@ -950,33 +889,26 @@ void choose_kernel(gp_sim* s, int64_t nloc_max, int& kernel, uint32_t& col_xsegs
     // 64 workgroups per CU: measured best for the tiled round kernels (tools/ablate.py:
     // 2048 -> 27.5, 8192 -> 22.1, 16384 -> 21.2 ms/round at P = 1e9)
     int64_t cap = (int64_t)prop.multiProcessorCount * 64;
-    // (measured: gossip on a large lattice -> column march, profiles/r01; push-sum on
-    // a large lattice -> column march, profiles/r03; small lattices and line -> tiled)
+    // (measured: gossip on a large lattice -> column march, profiles/r01; push-sum and
+    // small lattices and line -> tiled; the push-sum column march was measured slower,
+    // profiles/r03 and DESIGN.md §5.1)
     kernel = KERNEL_TILE;
     const bool lattice = cfg->topology == GP_3D || cfg->topology == GP_IMP3D;
     const bool push = cfg->algorithm == GP_PUSHSUM;
-    // push-sum column kernel: Imp3D senders carry their degree in 2 bits (P <= 2^30)
-    [[maybe_unused]] const bool pscol_ok = !s->force_tile && (cfg->topology == GP_3D || s->P <= (1ll << 30));
     if (lattice && g >= 200 && !push) kernel = KERNEL_COL;
 #ifdef GP_EXPERIMENTS
     if (const char* e = std::getenv("GP_KERNEL")) {
         if (!std::strcmp(e, "tile")) kernel = KERNEL_TILE;
-        else if (!std::strcmp(e, "col") && lattice && (!push || pscol_ok)) kernel = KERNEL_COL;
+        else if (!std::strcmp(e, "col") && lattice && !push) kernel = KERNEL_COL;
     }
 #endif
     col_xsegs = 1;
     if (cfg->topology != GP_FULL && kernel != KERNEL_TILE) {
-        // gossip: exactly the resident grid (a persistent sweep), a multiple of the 8 XCDs;
-        // push-sum: one block per work item (gp_pscol.hip pscol_grid)
-        const bool remote = s->world > 1 && cfg->topology == GP_IMP3D;
-        const int bpc = push ? pscol_blocks_per_cu(cfg->topology == GP_3D ? GRID3D : IMP3D, remote)
-                             : col_blocks_per_cu(cfg->topology, cfg->algorithm);
-        cap = (int64_t)prop.multiProcessorCount * bpc;
-        // x segments per patch: enough work items for every resident wave (gossip) or
-        // workgroup (push-sum), >= 16 planes each
-        const int64_t rows = push ? pscol_patch_rows() : 4;
-        const int64_t patches = ((g + 63) / 64) * ((g + rows - 1) / rows);
-        const int64_t slots = push ? cap : cap * (BULK_THREADS / 64);
+        // gossip: exactly the resident grid (a persistent sweep), a multiple of the 8 XCDs
+        cap = (int64_t)prop.multiProcessorCount * col_blocks_per_cu(cfg->topology, cfg->algorithm);
+        // x segments per patch: enough work items for every resident wave, >= 16 planes each
+        const int64_t patches = ((g + 63) / 64) * ((g + 3) / 4);
+        const int64_t slots = cap * (BULK_THREADS / 64);
         const int64_t planes = std::max<int64_t>(1, g / s->world);
         int64_t xs = std::max<int64_t>(1, slots / std::max<int64_t>(1, patches));
         xs = std::min<int64_t>(xs, std::max<int64_t>(1, planes / 16));
@@ -1128,28 +1060,7 @@ int create_common(const gp_config* cfg, int mode, int world, int rank, const uin
             return GP_ENCCL;
         }
     }
-    if ((rc = build_sim(s)) == GP_ERETRY_TILE) {
-        // the push-sum column kernel cannot take this topology (build_imp3d): the tile kernel
-        gp_sim* t = new gp_sim();
-        t->cfg = s->cfg;
-        t->device = s->device;
-        t->P = s->P;
-        t->T = s->T;
-        t->g = s->g;
-        t->mode = s->mode;
-        t->world = s->world;
-        t->rank = s->rank;
-        t->timing = s->timing;
-        t->stream = s->stream;
-        t->comm = s->comm;
-        t->force_tile = true;
-        (void)hipStreamSynchronize(s->stream);
-        s->stream = nullptr;
-        s->comm = nullptr;
-        gp_destroy(s);
-        s = t;
-        rc = build_sim(s);
-    }
+    rc = build_sim(s);
     if (rc) {
         const std::string msg = g_err;
         gp_destroy(s);

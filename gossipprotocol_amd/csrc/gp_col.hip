@@ -1,7 +1,7 @@
 // gp_col.hip -- column-march round kernels for the 3D / Imp3D lattice (gfx950).
 //
 // Gossip: one synchronous round of SRS v1 in PULL form with 2.5-D
-// blocking (push-sum: gp_pscol.hip).  A wave owns a patch of 4 y-rows x 64 z-columns (one node per lane
+// blocking (push-sum runs the tile kernel, gp_round.hip).  A wave owns a patch of 4 y-rows x 64 z-columns (one node per lane
 // and row; node id = x*g^2 + y*g + z, lanes = consecutive z, so every row of a
 // patch is one coalesced 64-node segment) and marches it along x through its
 // x-segment.  Planes x and x+1 of the patch stay in registers and plane x+2 is
@@ -387,7 +387,7 @@ int col_blocks_per_cu(int topo, int alg) {
 hipError_t launch_round_col(const WaveArgs& a, int topo, int alg, uint32_t round, int grid, hipStream_t st) {
     const dim3 g(grid), b(BULK_THREADS);
     if (alg == PUSHSUM) {
-        return hipErrorInvalidValue;  // push-sum column kernel: launch_round_pscol (gp_pscol.hip)
+        return hipErrorInvalidValue;  // (push-sum: the tile kernel)
     } else {
         if (topo == GRID3D) {
             hipLaunchKernelGGL(k_gossip_col<GRID3D>, g, b, 0, st, a, round);

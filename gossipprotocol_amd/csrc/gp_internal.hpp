@@ -169,16 +169,6 @@ struct DevState {
     int kernel;  // KERNEL_* below
     // column kernels: x segments per patch (set at create from the resident grid)
     uint32_t col_xsegs;
-    // push-sum column kernel (gp_pscol.hip), Imp3D: in-lists in patch order.  A
-    // step is one plane x of a patch (16 y-rows x 64 z-columns); step
-    // (yb * zsegs + zs) * planes + (x - x_lo) owns the receivers q = (y % 16) * 64
-    // + z % 64 and the edges [pc_soff[step], pc_soff[step + 1]) of pc_src (sender
-    // id | (deg - 4) << 30, ascending sender per receiver); pc_ind4: the
-    // receivers' in-degrees, a nibble each, 512 bytes per step
-    uint32_t* pc_src;
-    uint32_t* pc_soff;
-    uint8_t* pc_ind4;
-    uint32_t pc_nsteps;
     uint32_t tile_walk;  // RoundArgs::walk
     uint32_t tile_wx;    // RoundArgs::wx
     uint32_t tile_stage_cap;  // RoundArgs::stage_cap (experiments build only; default: no limit)
@@ -256,45 +246,6 @@ struct WaveArgs {
 // ---- column-march round kernels (gp_col.hip): 3D / Imp3D
 WaveArgs make_wave_args(const DevState& S, uint32_t round);
 
-// Arguments of the push-sum column kernel (gp_pscol.hip).  Node arrays indexed
-// by global id (pointers offset by the slab's base).
-struct PsColArgs {
-    const double2* swc;
-    double2* swn;
-    const uint8_t* nbc;
-    uint8_t* nbn;
-    const uint64_t* rbc;  // column-layout random-edge bits (activation phase)
-    uint64_t* rbn;
-    const uint32_t* src;   // DevState::pc_src
-    const uint32_t* soff;  // DevState::pc_soff
-    const uint8_t* ind4;   // DevState::pc_ind4
-    const uint32_t* rtag;  // several ranks: per local in-edge (patch order), round of the remote message
-    const double2* rmsg;
-    Ctl* ctl;
-    Geom G;
-    uint32_t k0, k1, lo, nloc, ext_lo, ext_hi;
-    uint32_t x_lo, x_hi, zs, yb, xs_len, nseg, nsteps;
-    uint32_t fuse;
-};
-// Patch keys of the global receiver order (gp_pscol.hip k_pc_keys): rank w owns
-// planes [x_lo[w], x_lo[w + 1]) and keys [kbase[w], kbase[w + 1]).
-struct PcKeyPlan {
-    int W;
-    uint32_t zs;
-    uint32_t x_lo[17];
-    uint32_t kbase[17];
-};
-uint32_t pscol_step_capacity();
-uint32_t pscol_patch_rows();
-uint32_t pscol_step_receivers();
-int pscol_blocks_per_cu(int topo, bool remote);
-PsColArgs make_pscol_args(const DevState& S, uint32_t round);
-uint32_t pscol_grid(const DevState& S);
-hipError_t launch_round_pscol(const DevState& S, uint32_t round, hipStream_t st);
-hipError_t launch_pc_keys(const uint32_t* rnd, uint32_t n, uint32_t* key, const Geom& G, const PcKeyPlan& kp, int grid,
-                          hipStream_t st);
-hipError_t launch_pc_slab(const uint32_t* off_all, const uint32_t* counts, uint32_t kbase, uint32_t nsteps,
-                          uint32_t edge0, uint32_t* soff, uint8_t* ind4, uint32_t* stat, int grid, hipStream_t st);
 hipError_t launch_round_col(const WaveArgs& a, int topo, int alg, uint32_t round, int grid, hipStream_t st);
 int col_blocks_per_cu(int topo, int alg);
 // random-edge bitmap words of the column layout (one 64-bit word per 64-node row segment)

@@ -380,9 +380,7 @@ hipError_t launch_bulk(const DevState& S, uint32_t round, int grid, hipStream_t 
     const dim3 g(grid), b(BULK_THREADS);
     if (S.topo != FULL) {
         if (S.kernel == KERNEL_TILE) return launch_round_tile(S, round, grid, st);
-        if (S.kernel == KERNEL_COL)
-            return S.alg == PUSHSUM ? launch_round_pscol(S, round, st)
-                                    : launch_round_col(make_wave_args(S, round), S.topo, S.alg, round, grid, st);
+        if (S.kernel == KERNEL_COL) return launch_round_col(make_wave_args(S, round), S.topo, S.alg, round, grid, st);
         return hipErrorInvalidValue;
     }
     if (S.alg == PUSHSUM) {

@@ -1,5 +1,5 @@
-// gp_wavecommon.hpp -- helpers shared by the column-march round kernels
-// (gp_col.hip, gp_pscol.hip).  Included by those translation units only.
+// gp_wavecommon.hpp -- helpers of the column-march round kernels (gp_col.hip).
+// Included by that translation unit only.
 #pragma once
 
 #include "gp_internal.hpp"
@@ -12,19 +12,6 @@ constexpr int WPB = BULK_THREADS / 64;  // waves per 256-thread block
 template <typename T>
 __device__ __forceinline__ T ld_agent(const T* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ uint32_t lane_prefix(unsigned long long m) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-
-// LDS written by lanes of this wave and read back by other lanes of it: keep the
-// compiler from moving DS operations across this point (the hardware executes
-// one wave's DS operations in order).
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // Block-wide sum of two per-thread counters, one atomic each (if non-zero).

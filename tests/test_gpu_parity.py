@@ -252,6 +252,8 @@ def test_kernel_variant_parity(kernel, n, topo, alg, seed, rounds, chk, xsegs, m
     """Every round-kernel variant (column march / tiled; experiments build,
     GP_KERNEL) bit-exact vs the oracle, the column march also with its
     x-segmentation forced."""
+    if kernel == "col" and alg == "push-sum":
+        pytest.skip("the column march runs lattice gossip only")
     monkeypatch.setenv("GP_KERNEL", kernel)
     monkeypatch.setenv("GP_XSEGS", xsegs)
     sim, orc = Sim(n, topo, alg, seed=seed, experimental=True), Oracle(n, topo, alg, seed)
