@@ -511,7 +511,11 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                     if (lane == 0) L.bits[m * (TPB / 64) + wv] = bal;
                     if (sent[m]) {
                         const uint32_t q = threadIdx.x + m * TPB;
-                        const double2* src = (REMOTE && isrc[m] - a.lo >= a.nloc) ? a.rmsg + e_lo + q : swc + isrc[m];
+                        // (the edge index opaque: hoisted out of the tile loop, the five per-lane
+                        // rmsg + q addresses were spilled, and each reload waited vmcnt(0))
+                        uint32_t eq = e_lo + q;
+                        if (REMOTE) asm volatile("" : "+v"(eq));
+                        const double2* src = (REMOTE && isrc[m] - a.lo >= a.nloc) ? a.rmsg + eq : swc + isrc[m];
                         __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(L.msg + (m * TPB + wv * 64)), 16,
                                                          0, DMA_ONCE);
                     }
