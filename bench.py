@@ -162,8 +162,14 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    # GP_BENCH_DEVICE pins every rank to one device (multi-process rehearsal on a one-GPU box)
+    # GP_BENCH_DEVICE pins every rank to one device (multi-process rehearsal on a one-GPU box).
+    # RCCL refuses two ranks on one device of one host, so each rank then claims a host id of
+    # its own: the ranks talk over RCCL's socket transport on loopback instead of xGMI.
     device = int(os.environ.get("GP_BENCH_DEVICE", local_rank))
+    if world > 1 and "GP_BENCH_DEVICE" in os.environ:
+        os.environ.setdefault("NCCL_HOSTID", f"gp-rehearsal-{rank}")
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ.setdefault("NCCL_IB_DISABLE", "1")
     sim = Simulation(args.nodes, args.topology, args.algorithm, seed=args.seed, device=device,
                      kernel_timing=True, rank=rank, world=world, dist=dist)
     P = sim.population
