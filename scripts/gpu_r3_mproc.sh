@@ -11,6 +11,6 @@ GP_BENCH_DEVICE=0 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 -
   --nodes ${NODES:-8000000} > $O/bench_w${NPROC:-2}.json 2> $O/bench_w${NPROC:-2}.err || { tail -40 $O/bench_w${NPROC:-2}.err; exit 1; }
 cat $O/bench_w${NPROC:-2}.json
 if [ -n "$FULL" ]; then
-  GP_MPROC_FULL=1 timeout -k 10 1000 python -u -m pytest tests/test_gpu_rccl_multiproc.py -k c5_size -x -v --timeout 950 --timeout-method thread > $O/pytest_c5.log 2>&1 || { tail -60 $O/pytest_c5.log; exit 1; }
-  echo "c5 size: $(tail -1 $O/pytest_c5.log)"
+  GP_MPROC_FULL=1 timeout -k 10 1000 python -u -m pytest tests/test_gpu_rccl_multiproc.py -k baseline_size -x -v --timeout 950 --timeout-method thread > $O/pytest_baseline_sizes.log 2>&1 || { tail -60 $O/pytest_baseline_sizes.log; exit 1; }
+  echo "baseline sizes: $(tail -1 $O/pytest_baseline_sizes.log)"
 fi

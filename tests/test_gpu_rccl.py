@@ -1,7 +1,7 @@
 """GPU: the RCCL transport on the one GPU a test box has -- a one-rank RCCL
 communicator (GP_FORCE_RCCL=1, experiments build) runs the split bookkeeping (pre / all-reduce /
 post) and must match the single-rank path bit for bit.  Multi-rank RCCL runs
-are the driver's multi-GPU bench (bench.py under torch.distributed.run)."""
+as separate processes: test_gpu_rccl_multiproc.py."""
 import os
 
 import numpy as np

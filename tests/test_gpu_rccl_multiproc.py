@@ -71,6 +71,8 @@ CASES = [
     (2, 27000, "Imp3D", "gossip", 4, 300),
     (2, 27000, "3D", "push-sum", 6, 200),
     (2, 2000, "line", "gossip", 7, 300),
+    (4, 64000, "Imp3D", "push-sum", 8, 120),
+    (4, 40000, "full", "push-sum", 9, 30),
 ]
 
 
@@ -97,19 +99,24 @@ def test_rccl_processes_match_single(world, n, topo, alg, seed, rounds):
 
 
 @pytest.mark.skipif(os.environ.get("GP_MPROC_FULL") != "1",
-                    reason="C5 size over the socket transport (minutes; scripts/gpu_r3_mproc.sh sets GP_MPROC_FULL=1)")
-def test_rccl_processes_c5_size():
-    """C5 (Imp3D push-sum, n = 1e9) as two processes past activation into steady state: per-round
-    alerts and an xxh3-128 digest of every rank's slab equal the single-process run's."""
+                    reason="BASELINE sizes over the socket transport (minutes; scripts/gpu_r3_mproc.sh sets GP_MPROC_FULL=1)")
+@pytest.mark.parametrize("world,n,topo,alg,rounds", [
+    (2, 10**9, "Imp3D", "push-sum", 140),   # C5: past activation into steady state
+    (2, 10**8, "full", "push-sum", 60),     # C4: the two-half exchange at its size
+    (2, 10**8, "Imp3D", "gossip", 100),     # C3: delivery pass + halo counters
+])
+def test_rccl_processes_baseline_size(world, n, topo, alg, rounds):
+    """BASELINE configurations as rank processes: per-round alerts and an xxh3-128 digest of every
+    rank's slab equal the single-process run's."""
     sys.path.insert(0, os.path.join(ROOT, "tests", "helpers"))
     from rccl_worker import slab_digest
     from gossipprotocol_amd import Simulation
-    n, rounds = 10**9, int(os.environ.get("GP_MPROC_ROUNDS", "140"))
-    recs = run_ranks(2, n, "Imp3D", "push-sum", 1, rounds, timeout=900)
-    with Simulation(n, "Imp3D", "push-sum", seed=1) as ref:
+    recs = run_ranks(world, n, topo, alg, 1, rounds, timeout=900)
+    with Simulation(n, topo, alg, seed=1) as ref:
         want = ref.step(rounds)
         info = ref.info()
-        assert info.active == info.population, "steady state not reached inside the window"
+        if alg == "push-sum" and topo == "Imp3D":
+            assert info.active == info.population, "steady state not reached inside the window"
         for r, rec in enumerate(recs):
             assert list(rec["alerts"]) == want
             lo, cnt = int(rec["first"]), int(rec["count"])
