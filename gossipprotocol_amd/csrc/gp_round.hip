@@ -53,6 +53,9 @@ namespace gp {
 #ifndef GP_ZDPP
 #define GP_ZDPP 1        // push-sum tile kernel: the j+-1 messages from the neighbour lane's registers (DPP)
 #endif
+#ifndef GP_NG
+#define GP_NG 1          // push-sum tile kernel: node slots whose loads are in flight together
+#endif
 #ifndef GP_MINB
 #define GP_MINB 5  // __launch_bounds__ minimum waves per SIMD (= resident 256-thread blocks per CU):
                    // the LDS tile allows 5, so keep VGPRs <= 96 to not lose the fifth
@@ -614,7 +617,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
             // lattice directions gathered from HBM / L2; with GP_ZDPP the j +- 1 ones
             // (z +- 1, or both line neighbours) are the neighbour lanes' own (s, w)
             constexpr uint32_t NDG = GP_ZDPP ? (TOPO == LINE ? 0u : 4u) : ND;
-            constexpr int NG = 1;  // nodes per slot group (two groups in flight spilled 49 VGPRs)
+            constexpr int NG = GP_NG;  // node slots per group in flight (2 at 5 waves/SIMD spilled 49 VGPRs)
 #pragma unroll
             for (int k0 = 0; k0 < NPT; k0 += NG) {
                 // phase A: node byte, present mask, lattice senders (from the staged
