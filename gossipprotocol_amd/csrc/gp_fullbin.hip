@@ -33,6 +33,7 @@
 // fails the batch in gp_step.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "gp_fullbin.hpp"
 
@@ -701,6 +702,9 @@ FullBinPlan full_bin_plan(uint32_t P) {
     // coarse bins ~ sqrt(P / TILE) so both passes write runs of ~10-20 messages;
     // at most FB_MAXBINS coarse bins and FB_MAXBINS fine tiles per coarse bin
     uint32_t s1 = (bits + FB_TB + 1) / 2;
+#ifdef GP_EXPERIMENTS
+    if (const char* e = std::getenv("GP_FB_S1D")) s1 += (uint32_t)std::atoi(e);  // coarse-bin size sweep
+#endif
     if (s1 < FB_TB) s1 = FB_TB;
     while (((uint64_t)P >> s1) >= FB_MAXBINS) ++s1;
     while (s1 - FB_TB > 12) --s1;
