@@ -18,8 +18,12 @@ under three rocprofv3 --pmc passes and the round kernel's HBM bytes are read
 from the L2's request-size counters (tools/hbm_traffic.py).  `cpu_baseline` times the SRS v1 C oracle on the host cores over a
 bounded sample of the same workload (steady state, smaller lattice).
 
-Multi-GPU (N > 1, launched by torch.distributed.run): one process per GPU,
-contiguous plane-aligned node slabs, RCCL exchange inside libgossip_hip.
+Multi-GPU (N > 1): one process per GPU, contiguous plane-aligned node slabs,
+RCCL exchange inside libgossip_hip.  Under torch.distributed.run the ranks come
+from the environment; `python bench.py --gpus N` without a launcher starts the N
+rank processes itself (launch_ranks) before anything touches a GPU -- it never
+measures fewer GPUs than asked for.  GP_BENCH_DEVICE=d pins every rank to device
+d (the one-GPU rehearsal: RCCL over sockets, recorded as such in the JSON line).
 """
 from __future__ import annotations
 
@@ -112,6 +116,17 @@ def cpu_baseline(args):
     }
 
 
+def launch_ranks(args):
+    """`--gpus N` outside torch.distributed.run: start N rank processes of this
+    script (gossipprotocol_amd/launch.py; device = rank, or GP_BENCH_DEVICE for
+    all), wait for all of them, and return the first failing exit code (the
+    others are stopped) or rank 0's.  This process never touches a GPU; rank 0
+    prints the JSON line."""
+    from gossipprotocol_amd.launch import run_ranks
+    return run_ranks([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], args.gpus,
+                     env_for_rank=lambda r: {"GP_BENCH_LAUNCHED": "1"}, log=log)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -131,11 +146,15 @@ def main():
     ap.add_argument("--traffic-timeout", type=float, default=240.0)
     args = ap.parse_args()
 
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: refusing to measure another GPU count")
     traffic, traffic_note = None, "not measured (multi-GPU run)" if world > 1 else "not measured (--no-traffic)"
     if world == 1 and not args.no_traffic:
         t_tr = time.perf_counter()
@@ -166,10 +185,14 @@ def main():
     # RCCL refuses two ranks on one device of one host, so each rank then claims a host id of
     # its own: the ranks talk over RCCL's socket transport on loopback instead of xGMI.
     device = int(os.environ.get("GP_BENCH_DEVICE", local_rank))
-    if world > 1 and "GP_BENCH_DEVICE" in os.environ:
+    rehearsal = world > 1 and "GP_BENCH_DEVICE" in os.environ
+    if rehearsal:  # every rank on one device: only RCCL's socket transport can connect them
         os.environ.setdefault("NCCL_HOSTID", f"gp-rehearsal-{rank}")
         os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
         os.environ.setdefault("NCCL_IB_DISABLE", "1")
+    transport = ("none (one GPU)" if world == 1 else
+                 f"RCCL sockets on loopback: one-GPU rehearsal, all {world} ranks on device {device} "
+                 "(not a multi-GPU number)" if rehearsal else "RCCL, one process per GPU (xGMI)")
     sim = Simulation(args.nodes, args.topology, args.algorithm, seed=args.seed, device=device,
                      kernel_timing=True, rank=rank, world=world, dist=dist)
     P = sim.population
@@ -213,7 +236,10 @@ def main():
             "workload": f"push-sum rounds, {args.topology} lattice, n={args.nodes} (P={P}), steady state "
                         f"(all nodes active), seed {args.seed}",
             "num_nodes": args.nodes, "population": P, "topology": args.topology, "algorithm": args.algorithm,
-            "parallelism": f"slab{world}", "activation_preroll_rounds": pre,
+            "parallelism": f"slab{world}", "transport": transport,
+            "launcher": ("bench.py --gpus (rank processes)" if os.environ.get("GP_BENCH_LAUNCHED") else
+                         "torch.distributed.run" if world > 1 else "single process"),
+            "activation_preroll_rounds": pre,
         },
         "roofline": {
             "bound": "hbm",
@@ -254,4 +280,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -1,41 +1,62 @@
 """python -m gossipprotocol_amd <num_nodes> <topology> <algorithm> [--seed S] [--max-rounds R]
+                                [--gpus G] [--device D]
 
 Same argv and stdout contract as the reference's `dotnet run` (Program.fs:32-34,
 198/203, 55): prints "Gossip Starts" / "Push Sum Starts", then
-"Convergence Time: %f ms".
+"Convergence Time: %f ms".  --gpus G (or GOSSIP_GPUS=G) runs one rank process per
+GPU (gossipprotocol_amd.launch; rank r on device r, or every rank on --device D
+as the one-GPU rehearsal); rank 0 prints.  Same behaviour as the C++ CLI
+(csrc/gossip_cli.cpp).
 """
 import argparse
+import os
 import sys
 
 from . import _lib as L
-from .sim import Simulation
 
 
 def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
     ap = argparse.ArgumentParser(prog="gossipprotocol_amd")
     ap.add_argument("num_nodes", type=int)
     ap.add_argument("topology")
     ap.add_argument("algorithm")
-    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--seed", type=int, default=int(os.environ.get("GOSSIP_SEED", "1")))
     ap.add_argument("--max-rounds", type=int, default=0)
-    ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--device", type=int, default=None)
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("GOSSIP_GPUS", "1")))
     a = ap.parse_args(argv)
     if a.algorithm not in ("gossip", "push-sum"):
         print("option invalid")  # Program.fs:207
         return 2
+    if a.gpus < 1:
+        print("--gpus / GOSSIP_GPUS must be >= 1", file=sys.stderr)
+        return 2
+    if a.gpus > 1 and not os.environ.get("GOSSIP_LAUNCHED"):
+        from .launch import rehearsal_env, run_ranks
+        extra = (lambda r: rehearsal_env(r)) if a.device is not None else None
+        return run_ranks([sys.executable, "-m", "gossipprotocol_amd"] + argv, a.gpus, env_for_rank=extra,
+                         ok_codes=(0, 3))
+    from .sim import Simulation
+    rank = int(os.environ.get("RANK", "0")) if a.gpus > 1 else 0
+    device = a.device if a.device is not None else rank
     try:
         sim = Simulation(a.num_nodes, a.topology, a.algorithm, seed=a.seed, max_rounds=a.max_rounds,
-                         device=a.device)
+                         device=device, rank=rank, world=a.gpus, rendezvous=os.environ.get("GOSSIP_RDV"))
     except L.GossipError as e:
-        print(e, file=sys.stderr)
+        print(f"[rank {rank}/{a.gpus}] {e}", file=sys.stderr)
         return 2 if e.code == -1 else 1
-    print("Gossip Starts" if a.algorithm == "gossip" else "Push Sum Starts", flush=True)
+    if rank == 0:
+        print("Gossip Starts" if a.algorithm == "gossip" else "Push Sum Starts", flush=True)
     res = sim.run()
     sim.close()
     if res.status == L.GP_STATUS_CONVERGED:
-        print("Convergence Time: %f ms" % res.elapsed_ms)
+        if rank == 0:
+            print("Convergence Time: %f ms" % res.elapsed_ms, flush=True)
         return 0
-    print("Not converged after %d rounds (%d of %d alerts)" % (res.rounds, res.converged, res.threshold))
+    if rank == 0:
+        print("Not converged after %d rounds (%d of %d alerts)" % (res.rounds, res.converged, res.threshold),
+              flush=True)
     return 3
 
 

@@ -54,6 +54,7 @@ SIGNATURES = [
     ("gp_resolve", _i32, [_i64, _i32, C.POINTER(_i64), C.POINTER(_i64), C.POINTER(_i64)]),
     ("gp_create", _i32, [C.POINTER(GpConfig), C.POINTER(_vp)]),
     ("gp_get_unique_id", _i32, [C.c_char_p]),
+    ("gp_rendezvous_id", _i32, [_i32, C.c_char_p, _i32, C.c_char_p]),
     ("gp_create_rank", _i32, [C.POINTER(GpConfig), _i32, _i32, C.c_char_p, C.POINTER(_vp)]),
     ("gp_run", _i32, [_vp, C.POINTER(GpResult)]),
     ("gp_step", _i64, [_vp, _i64, C.POINTER(_i64)]),

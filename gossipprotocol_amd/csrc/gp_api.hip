@@ -22,12 +22,18 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cerrno>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
+
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <rccl/rccl.h>
 
@@ -1135,7 +1141,9 @@ int gp_create(const gp_config* cfg, gp_sim** out) {
     }
     if (cfg->num_gpus > 1) {
         if (cfg->flags & GP_FLAG_VIRTUAL_RANKS) return create_common(cfg, MODE_VIRTUAL, cfg->num_gpus, 0, nullptr, out);
-        set_err("num_gpus > 1: run one process per GPU and use gp_create_rank (or GP_FLAG_VIRTUAL_RANKS)");
+        set_err("num_gpus > 1: one process per GPU -- launch `gossip <n> <topology> <algorithm> --gpus %d` "
+                "(or GOSSIP_GPUS=%d), which joins every rank through gp_rendezvous_id + gp_create_rank; "
+                "GP_FLAG_VIRTUAL_RANKS runs the slabs in this process on one GPU", cfg->num_gpus, cfg->num_gpus);
         return GP_EINVAL;
     }
     return create_common(cfg, MODE_SINGLE, 1, 0, nullptr, out);
@@ -1151,6 +1159,49 @@ int gp_get_unique_id(uint8_t unique_id[128]) {
     NCCL_TRY(ncclGetUniqueId(&id));
     std::memcpy(unique_id, id.internal, NCCL_UNIQUE_ID_BYTES);
     return GP_OK;
+}
+
+int gp_rendezvous_id(int32_t rank, const char* path, int32_t timeout_ms, uint8_t unique_id[128]) {
+    if (!path || !*path || !unique_id || rank < 0) {
+        set_err("gp_rendezvous_id: bad argument");
+        return GP_EINVAL;
+    }
+    const size_t N = 128;
+    if (rank == 0) {  // publish: write a private name, then rename (readers never see a partial id)
+        int rc = gp_get_unique_id(unique_id);
+        if (rc) return rc;
+        const std::string tmp = std::string(path) + ".tmp." + std::to_string((long long)getpid());
+        const int fd = ::open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0600);
+        if (fd < 0) {
+            set_err("gp_rendezvous_id: cannot create '%s': %s", tmp.c_str(), std::strerror(errno));
+            return GP_EINVAL;
+        }
+        const bool ok = ::write(fd, unique_id, N) == (ssize_t)N && ::fsync(fd) == 0;
+        ::close(fd);
+        if (!ok || ::rename(tmp.c_str(), path) != 0) {
+            set_err("gp_rendezvous_id: cannot publish '%s': %s", path, std::strerror(errno));
+            ::unlink(tmp.c_str());
+            return GP_EINVAL;
+        }
+        return GP_OK;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {  // wait for rank 0's file
+        const int fd = ::open(path, O_RDONLY | O_CLOEXEC);
+        if (fd >= 0) {
+            const ssize_t got = ::read(fd, unique_id, N);
+            ::close(fd);
+            if (got == (ssize_t)N) return GP_OK;
+            set_err("gp_rendezvous_id: '%s' holds %zd bytes, expected %zu", path, got, N);
+            return GP_EINVAL;
+        }
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        if (timeout_ms >= 0 && ms >= timeout_ms) {
+            set_err("gp_rendezvous_id: rank %d waited %d ms for rank 0's id at '%s'", rank, timeout_ms, path);
+            return GP_ESTATE;
+        }
+        std::this_thread::sleep_for(std::chrono::milliseconds(5));
+    }
 }
 
 int gp_create_rank(const gp_config* cfg, int32_t rank, int32_t world, const uint8_t unique_id[128], gp_sim** out) {

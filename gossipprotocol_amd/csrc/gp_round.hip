@@ -618,6 +618,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
             // (z +- 1, or both line neighbours) are the neighbour lanes' own (s, w)
             constexpr uint32_t NDG = GP_ZDPP ? (TOPO == LINE ? 0u : 4u) : ND;
             constexpr int NG = GP_NG;  // node slots per group in flight (2 at 5 waves/SIMD spilled 49 VGPRs)
+            static_assert(NPT % NG == 0, "node groups must divide the nodes per thread");
 #pragma unroll
             for (int k0 = 0; k0 < NPT; k0 += NG) {
                 // phase A: node byte, present mask, lattice senders (from the staged

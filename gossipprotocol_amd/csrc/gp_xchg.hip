@@ -39,6 +39,7 @@ __device__ __forceinline__ uint32_t owner_of(uint32_t t, const uint32_t* bounds,
 // and round at world 8, against 2.2 ms for the round kernel.)
 constexpr int PACK_PER = 32;                     // senders per thread
 constexpr uint32_t PACK_RANGE = 256u * PACK_PER;  // senders per block
+static_assert(XMAXW <= 16, "k_pack keeps a destination rank in 4 bits");
 
 __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
     __shared__ uint32_t cnt[XMAXW], off[XMAXW];
@@ -49,7 +50,10 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
     if (threadIdx.x <= (uint32_t)a.W) bnd[threadIdx.x] = a.bounds[threadIdx.x];
     __syncthreads();
     const uint32_t last = a.nloc - 1;
-    uint32_t dst[PACK_PER / 8];  // destination rank per sender, a nibble each (15: no message)
+    // destination rank per sender, a nibble each; `me` means "no message" (a sender never
+    // packs for its own rank, so the value is free for every world size up to XMAXW = 16)
+    const uint32_t none = (uint32_t)a.me;
+    uint32_t dst[PACK_PER / 8];
 #pragma unroll
     for (int g = 0; g < PACK_PER / 8; ++g) {
         uint8_t b[8];
@@ -64,7 +68,7 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
 #pragma unroll
         for (int h = 0; h < 8; ++h) {
             const uint32_t li = r0 + (g * 8 + h) * 256u + threadIdx.x;
-            uint32_t d = 15u;
+            uint32_t d = none;
             if (li < a.nloc && (b[h] & DIR_MASK) == DIR_RANDOM) {
                 const uint32_t own = owner_of(t[h], bnd, a.W);
                 if (own != (uint32_t)a.me) {
@@ -87,7 +91,7 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
 #pragma unroll
         for (int h = 0; h < 8; ++h) {
             const uint32_t d = (dst[g] >> (4 * h)) & 15u;
-            if (d == 15u) continue;
+            if (d == none) continue;
             const uint32_t li = r0 + (g * 8 + h) * 256u + threadIdx.x;
             const uint32_t idx = atomicAdd(&off[d], 1u);
             if (idx < a.peer[d].cap) {

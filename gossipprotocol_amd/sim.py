@@ -42,10 +42,12 @@ class Simulation:
 
     def __init__(self, num_nodes: int, topology: str, algorithm: str, seed: int = 1,
                  max_rounds: int = 0, device: int = 0, kernel_timing: bool = False,
-                 rank: int = 0, world: int = 1, dist=None, virtual_ranks: int = 1, experimental: bool = False):
+                 rank: int = 0, world: int = 1, dist=None, virtual_ranks: int = 1, experimental: bool = False,
+                 rendezvous: str | None = None, rendezvous_timeout_ms: int = 600000):
         """world > 1: this process is rank `rank` of a one-process-per-GPU run
-        (RCCL; `dist` is a torch.distributed group used once to share the RCCL
-        id).  virtual_ranks > 1: that many slabs in this process on `device`,
+        (RCCL; rank 0's RCCL id is shared once, through `dist` -- a
+        torch.distributed group -- or through the file `rendezvous`
+        (gp_rendezvous_id; gossipprotocol_amd.launch sets GOSSIP_RDV)).  virtual_ranks > 1: that many slabs in this process on `device`,
         exchanging through device copies (the multi-GPU path on one GPU).
         experimental: use the experiments build (kernel variants selected by
         GP_* environment variables; tests and tools only)."""
@@ -66,13 +68,16 @@ class Simulation:
             # one process per GPU: rank 0 makes the RCCL id, the caller's process
             # group (gloo is enough) broadcasts it, every rank joins its slab
             uid = C.create_string_buffer(128)
-            if rank == 0:
-                self._chk(self._L.gp_get_unique_id(uid))
-            if dist is None:
-                raise ValueError("world > 1 needs a torch.distributed process group to share the RCCL id")
-            box = [uid.raw if rank == 0 else None]
-            dist.broadcast_object_list(box, src=0)
-            uid = C.create_string_buffer(box[0], 128)
+            if dist is None and rendezvous:
+                self._chk(self._L.gp_rendezvous_id(rank, rendezvous.encode(), rendezvous_timeout_ms, uid))
+            elif dist is None:
+                raise ValueError("world > 1 needs a torch.distributed group or a rendezvous path to share the RCCL id")
+            else:
+                if rank == 0:
+                    self._chk(self._L.gp_get_unique_id(uid))
+                box = [uid.raw if rank == 0 else None]
+                dist.broadcast_object_list(box, src=0)
+                uid = C.create_string_buffer(box[0], 128)
             self._chk(self._L.gp_create_rank(C.byref(cfg), rank, world, uid, C.byref(h)))
         else:
             self._chk(self._L.gp_create(C.byref(cfg), C.byref(h)))

@@ -63,7 +63,8 @@ typedef struct gp_config {
     int32_t topology;    /* GP_LINE .. GP_IMP3D (argv[1], Program.fs:33) */
     int32_t algorithm;   /* GP_GOSSIP | GP_PUSHSUM (argv[2], Program.fs:34) */
     uint64_t seed;       /* Philox key; replaces `new Random()` (Program.fs:86 et al.) */
-    int32_t num_gpus;    /* 1; multi-GPU runs one process per GPU (gp_create_rank), or num_gpus
+    int32_t num_gpus;    /* 1; multi-GPU runs one process per GPU (gp_create_rank; launchers:
+                            `gossip --gpus N` / GOSSIP_GPUS, bench.py --gpus N), or num_gpus
                             in-process slabs with GP_FLAG_VIRTUAL_RANKS */
     int32_t device;      /* HIP device ordinal for num_gpus == 1 */
     int64_t max_rounds;  /* cap; <= 0 means unlimited (the reference blocks forever, Program.fs:282) */
@@ -119,6 +120,16 @@ int gp_create(const gp_config* cfg, gp_sim** out);
 int gp_get_unique_id(uint8_t unique_id[128]);
 int gp_create_rank(const gp_config* cfg, int32_t rank, int32_t world, const uint8_t unique_id[128],
                    gp_sim** out);
+
+/* Launcher rendezvous without a host framework (gossip --gpus N, bench.py
+ * --gpus N, the F# front-end): the launcher starts one process per GPU before
+ * any of them touches a GPU and hands all of them one fresh file path.  Rank 0
+ * calls gp_get_unique_id and publishes the 128 bytes at `path` (written under a
+ * private name, then renamed, so a reader never sees a partial id); every other
+ * rank waits for the file (at most timeout_ms; < 0 waits forever) and reads it.
+ * Then every rank calls gp_create_rank with the same id.  The launcher removes
+ * the file afterwards. */
+int gp_rendezvous_id(int32_t rank, const char* path, int32_t timeout_ms, uint8_t unique_id[128]);
 
 /* Replaces the message loop Program.fs:84-131,141-163 plus the scheduler
  * Program.fs:41-61: runs synchronous rounds until the cumulative alert count

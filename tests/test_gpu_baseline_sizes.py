@@ -15,8 +15,11 @@ progress while it goes; a failing segment stops the run (-x).
   C5  push-sum Imp3D n = 1e8 (g = 465): through activation (every node active)
       and then steady-state rounds, i.e. the headline kernel's all-active path
       (sender Philox redraw, compact in-edge messages) at the 1e8 scale.
-      The 1e9 size itself is covered by tests/test_gpu_parity.py's
-      conservation / determinism check (the oracle would need ~70 GB and ~20 min).
+      The 1e9 size itself is covered by tests/test_gpu_parity.py::
+      test_full_size_imp3d_pushsum_1e9_rounds: four rounds (activation, steady
+      state, the alert peak at round 533, the converged tail at round 700)
+      recomputed by the oracle for ~1.1e6 sampled receivers, bit-exact (a whole
+      oracle run at 1e9 would need ~70 GB and ~20 min).
 """
 import os
 import sys

@@ -99,3 +99,24 @@ def test_exchange_overflow_fails_every_rank(topo, alg, monkeypatch):
         sim.step(200)
     assert e.value.code == -5 and "overflow" in str(e.value)
     sim.close()
+
+
+@pytest.mark.parametrize("topo,alg", [("Imp3D", "push-sum"), ("Imp3D", "gossip"), ("full", "push-sum")])
+def test_virtual_ranks_max_world(topo, alg):
+    """The largest world the exchange supports (XMAXW = 16, gp_xchg.hpp): every rank,
+    rank 15 included, receives its random-edge / full messages (k_pack keeps a
+    destination rank in 4 bits; the "no message" value is the sender's own rank)."""
+    n, seed, rounds = 32768, 11, 400
+    sim = Sim(n, topo, alg, seed=seed, virtual_ranks=16)
+    orc = Oracle(n, topo, alg, seed)
+    assert sim.info().num_gpus == 16
+    done = 0
+    while done < rounds:
+        ga, oa = sim.step(100), orc.step(100)
+        assert ga == oa, f"alerts differ in rounds {done}..{done + 100}"
+        same_state(alg, sim.state(), orc.state())
+        done += 100
+        if len(ga) < 100:
+            break
+    sim.close()
+    orc.close()

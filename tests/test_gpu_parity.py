@@ -188,48 +188,68 @@ def _sample_ids(P, g, rng, n_random=1_000_000):
 
 
 def _check_round_sampled(sim, n, seed, ids):
-    """Round r of the GPU (r = sim.rounds) against or_pushsum_receivers for ids."""
+    """Round r of the GPU (r = sim.rounds) against or_pushsum_receivers for ids.
+    Also: the round's alert count reported by the GPU equals the number of nodes
+    whose converged flag the round set (whole state), and the sampled receivers
+    that converge in it are exactly the ones the oracle says converge."""
     from tests.oracle_ctypes import pushsum_receivers
     P = sim.population
     r = sim.rounds
     s, w, f = _read_all(sim, P)
     tot = (float(np.sum(s)), float(np.sum(w)))
-    so, wo, fo, _ = pushsum_receivers("Imp3D", n, seed, r, s, w, f, ids)
+    so, wo, fo, conv_sampled = pushsum_receivers("Imp3D", n, seed, r, s, w, f, ids)
+    conv0 = int(np.count_nonzero(f & 2))
+    was_conv = (f[ids] & 2) != 0
     del s, w, f
-    sim.step(1)
-    assert sim.rounds == r + 1
+    alerts = sim.step(1)
+    assert sim.rounds == r + 1 and len(alerts) == 1
     s2, w2, f2 = _read_all(sim, P)
     np.testing.assert_array_equal(s2[ids], so, err_msg=f"s differs in round {r}")
     np.testing.assert_array_equal(w2[ids], wo, err_msg=f"w differs in round {r}")
     np.testing.assert_array_equal(f2[ids], fo, err_msg=f"flags differ in round {r}")
-    return tot
+    newly = int(np.count_nonzero(((f2[ids] & 2) != 0) & ~was_conv))
+    assert newly == conv_sampled, f"round {r}: {newly} sampled receivers converged, oracle says {conv_sampled}"
+    assert alerts[0] == int(np.count_nonzero(f2 & 2)) - conv0, f"round {r}: alert count != newly converged nodes"
+    return tot, alerts[0], conv_sampled
 
 
 def test_full_size_imp3d_pushsum_1e9_rounds():
-    """C5 at its real size (P = 1e9), on the kernel bench.py times: one round during
-    activation (round 40) and one in steady state (every node active, 8 rounds
-    later) are recomputed on the host for ~1.1e6 receivers by
-    or_pushsum_receivers from the read-back round-start state -- bit-exact s, w
-    and flags (Program.fs:101-131 via SRS v1 B.4); mass conserved to 1e-12
-    relative; a second run is bit-identical (determinism)."""
+    """C5 at its real size (P = 1e9), on the kernel bench.py times, recomputed on the
+    host for ~1.1e6 receivers by or_pushsum_receivers from the read-back round-start
+    state -- bit-exact s, w and flags (Program.fs:101-131 via SRS v1 B.4) in four
+    rounds: during activation (round 40), in steady state before any alert (every
+    node active, 8 rounds later), at the alert peak (round 533: 1.5e7 of the 1e9
+    nodes converge in that round, the count / converge branch of Program.fs:114-123)
+    and in the tail (round 700: 99 % converged, converged nodes forwarding, D6).
+    Mass conserved to 1e-12 relative; each round's alert count equals the nodes it
+    converged; a second run is bit-identical (determinism)."""
     n, seed = 10**9, 1
     sim = Sim(n, "Imp3D", "push-sum", seed=seed)
     P, g = sim.population, sim.info().grid
     ids = _sample_ids(P, g, np.random.default_rng(7))
-    sim.step(40)
-    tot_s, tot_w = _check_round_sampled(sim, n, seed, ids)
     ref_s = P * (P - 1) / 2
-    assert abs(tot_s - ref_s) <= 1e-12 * ref_s
-    assert abs(tot_w - P) <= 1e-12 * P
+
+    def check():
+        (tot_s, tot_w), a, conv = _check_round_sampled(sim, n, seed, ids)
+        assert abs(tot_s - ref_s) <= 1e-12 * ref_s
+        assert abs(tot_w - P) <= 1e-12 * P
+        return a, conv
+
+    sim.step(40)
+    check()
     h = hashlib.sha256(sim.state(0, 50_000_000)["s"].tobytes()).hexdigest()
     while sim.info().active < P:
         assert sim.rounds < 400, "activation did not complete"
         sim.step(8)
     sim.step(8)
     assert sim.info().active == P
-    tot_s, tot_w = _check_round_sampled(sim, n, seed, ids)
-    assert abs(tot_s - ref_s) <= 1e-12 * ref_s
-    assert abs(tot_w - P) <= 1e-12 * P
+    check()
+    sim.step(533 - sim.rounds)
+    a, conv = check()
+    assert a > 10**7 and conv > 5000, (a, conv)  # the alert peak is exercised
+    sim.step(700 - sim.rounds)
+    a, conv = check()
+    assert a > 10**5 and sim.alerts_total > 0.98 * P, (a, sim.alerts_total)
     sim.close()
     sim2 = Sim(n, "Imp3D", "push-sum", seed=seed)
     sim2.step(41)
