@@ -88,6 +88,7 @@ struct Slab {
     uint32_t hi = 0;  // one past the last owned id
     // Imp3D random-edge exchange (W > 1)
     uint32_t* pos = nullptr;
+    uint8_t* xdst = nullptr;  // owner rank of each local sender's random-edge target (k_pack)
     uint8_t* xsend = nullptr;
     uint8_t* xrecv = nullptr;
     uint32_t nedges = 0;
@@ -252,6 +253,10 @@ int make_bounds(gp_sim* s) {
     return GP_OK;
 }
 
+// Imp3D gossip on the column kernel: random-edge deliveries are counted by their
+// senders (rq) and cross ranks as counts; no bitmap, in-edge tags or slots.
+bool col_gossip_counts(const DevState& S) { return S.topo == IMP3D && S.alg == GOSSIP && S.kernel == KERNEL_COL; }
+
 // Device state of slab `r` (rank r): ids [bounds[r], bounds[r+1]) plus halos.
 int alloc_slab(gp_sim* s, Slab& sl, int r) {
     DevState& S = sl.S;
@@ -318,20 +323,15 @@ int alloc_slab(gp_sim* s, Slab& sl, int r) {
             (rc = dev_alloc_t(s, &S.fb_hdr2, m2)) || (rc = dev_alloc_t(s, &S.fb_pay2, m2)))
             return rc;
     }
-    if (S.topo == IMP3D && S.alg == GOSSIP && S.kernel == KERNEL_COL) {
-        if (W == 1) {  // senders count their random-edge deliveries (k_gossip_col, push form)
-            for (int q = 0; q < 2; ++q) {
-                if ((rc = dev_alloc_t(s, &S.rq[q], (size_t)S.nloc + 64))) return rc;
-                HIP_TRY(hipMemsetAsync(S.rq[q], 0, sizeof(uint32_t) * ((size_t)S.nloc + 64), s->stream));
-            }
-        } else if ((rc = dev_alloc_t(s, &S.rcnt, (size_t)S.nloc + 64))) {  // receivers decide (k_gossip_redges)
-            return rc;
+    if (col_gossip_counts(S)) {  // senders count their random-edge deliveries at the target (k_gossip_col)
+        for (int q = 0; q < 2; ++q) {
+            if ((rc = dev_alloc_t(s, &S.rq[q], (size_t)S.nloc + 64))) return rc;
+            HIP_TRY(hipMemsetAsync(S.rq[q], 0, sizeof(uint32_t) * ((size_t)S.nloc + 64), s->stream));
         }
     }
-    // random-edge bitmaps; not needed by one-rank gossip on the column kernel (push form)
-    if (S.topo == IMP3D && !(S.alg == GOSSIP && S.kernel == KERNEL_COL && W == 1)) {
-        S.rbits_words = S.kernel == KERNEL_COL ? col_rbits_words(S.nloc / S.G.g2, S.G.g)
-                                               : rbits_words_for(S.lo, S.nloc);
+    // random-edge bitmaps of the tile kernels (the column kernel counts deliveries instead)
+    if (S.topo == IMP3D && !col_gossip_counts(S)) {
+        S.rbits_words = rbits_words_for(S.lo, S.nloc);
         if ((rc = dev_alloc_t(s, &S.rbits[0], S.rbits_words)) || (rc = dev_alloc_t(s, &S.rbits[1], S.rbits_words)))
             return rc;
     }
@@ -422,14 +422,18 @@ int build_imp3d(gp_sim* s) {
             HIP_TRY(launch_pack_ind4(S, wide_at, s->grid, s->stream));
         }
         if (W > 1) {
-            if ((rc = dev_alloc_t(s, &sl.pos, S.nloc)) || (rc = dev_alloc_t(s, &S.rtag, ne)) ||
-                (S.alg == PUSHSUM && (rc = dev_alloc_t(s, &S.rmsg, ne))))
+            // counts (gossip column kernel) carry the target's local id: no slots, no tags
+            const bool slots = !col_gossip_counts(S);
+            if ((rc = dev_alloc_t(s, &sl.xdst, (size_t)S.nloc + 64))) return rc;
+            if (slots && ((rc = dev_alloc_t(s, &sl.pos, S.nloc)) || (rc = dev_alloc_t(s, &S.rtag, ne)) ||
+                          (S.alg == PUSHSUM && (rc = dev_alloc_t(s, &S.rmsg, ne)))))
                 return rc;
-            HIP_TRY(hipMemsetAsync(S.rtag, 0xFF, sizeof(uint32_t) * (ne ? ne : 1), s->stream));
+            if (slots) HIP_TRY(hipMemsetAsync(S.rtag, 0xFF, sizeof(uint32_t) * (ne ? ne : 1), s->stream));
             PosArgs pa{};
             pa.rnd = S.rnd;
             pa.inv = inv;
-            pa.pos = sl.pos;
+            pa.pos = slots ? sl.pos : nullptr;
+            pa.xdst = sl.xdst;
             pa.lo = S.lo;
             pa.nloc = S.nloc;
             pa.W = W;
@@ -739,12 +743,14 @@ int exchange(gp_sim* s, uint32_t rn) {
             pa.swn = push ? S.sw[b] : nullptr;
             pa.rnd = S.rnd;
             pa.pos = sl.pos;
+            pa.xdst = sl.xdst;
             pa.lo = S.lo;
             pa.nloc = S.nloc;
             pa.base = S.base;
             pa.W = W;
             pa.me = sl.rank;
             pa.push = push ? 1 : 0;
+            pa.counts = col_gossip_counts(S) ? 1 : 0;
             for (int w = 0; w <= W; ++w) pa.bounds[w] = s->bounds[w];
             for (int p = 0; p < W; ++p) {
                 pa.peer[p] = xpeer(sl.xsend, sl.soff[p], sl.cap_out[p]);
@@ -812,7 +818,8 @@ int exchange(gp_sim* s, uint32_t rn) {
             UnpackArgs ua{};
             ua.rtag = sl.S.rtag;
             ua.rmsg = sl.S.rmsg;
-            ua.nedges = sl.nedges;
+            ua.rq = col_gossip_counts(sl.S) ? sl.S.rq[rn & 1] : nullptr;  // next round's deliveries
+            ua.nedges = ua.rq ? sl.S.nloc : sl.nedges;
             ua.W = W;
             ua.me = sl.rank;
             ua.push = push ? 1 : 0;
@@ -874,12 +881,12 @@ double alg_bytes(const gp_sim* s) {
         return 1.0 + 1.0 + 16.0 + 20.0 + 4.0 + 40.0 + 20.0 + 32.0 + 2.0;
     }
     // gossip: counter r+w 8, direction byte r+w 2; Imp3D:
-    //   one rank, push form (k_gossip_col counts random-edge sends at their targets a
-    //   round ahead): rnd 4 + delivery count read 4, its zeroing where non-zero and the
-    //   senders' atomic increments (~1/7 of nodes each, 4 B) -> 18 + 8/7;
-    //   several ranks (k_gossip_redges + k_gossip_col): in-list 8, per-node count w+r 4;
+    //   column kernel (counts random-edge sends at their targets a round ahead): rnd 4 +
+    //   delivery count read 4, its zeroing where non-zero and the senders' atomic
+    //   increments (~1/7 of nodes each, 4 B) -> 18 + 8/7 (several ranks: the remote 7/8
+    //   of the increments arrive through k_unpack instead);
     //   tile kernel: in-list 8
-    if (S.topo == IMP3D) return S.rq[0] ? 18.0 + 8.0 / 7.0 : S.rcnt ? 22.0 : 18.0;
+    if (S.topo == IMP3D) return S.rq[0] ? 18.0 + 8.0 / 7.0 : 18.0;
     if (S.topo != FULL) return 10.0;
     return 4.0 + 8.0 + 8.0 + 8.0;  // send: c + atomic RMW; recv: inc r+w, c r+w
 }
@@ -1008,8 +1015,7 @@ int build_sim(gp_sim* s) {
         HIP_TRY(hipMemcpyAsync(S.ctl, &init, sizeof(Ctl), hipMemcpyHostToDevice, s->stream));
         HIP_TRY(launch_init(S, s->grid, s->stream));
         if (S.topo == IMP3D)
-            HIP_TRY(S.kernel == KERNEL_COL ? launch_col_rbits_init(S, s->stream)
-                                           : launch_rbits_init(S, s->grid, s->stream));
+            HIP_TRY(col_gossip_counts(S) ? launch_col_seed_init(S, s->stream) : launch_rbits_init(S, s->grid, s->stream));
         if (S.alg == GOSSIP && S.topo != FULL) HIP_TRY(launch_injector_init(S, s->grid, s->stream));
     }
     if ((rc = exchange(s, 0))) return rc;     // halos and random edges of round 0

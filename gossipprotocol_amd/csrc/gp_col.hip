@@ -12,13 +12,13 @@
 // and only the two y-halo rows touch another wave's data.  Per node and round
 // the compulsory stream is the rumour counter + node byte in and out; the
 // lattice costs no HBM traffic of its own.  Imp3D random-edge deliveries are
-// integer counts: counted by their senders a round ahead (one rank) or by the
-// receivers' delivery pass k_gossip_redges (several ranks).
+// integer counts, so their order is free: a sender whose next direction is its
+// random edge counts the rumour at its target a round ahead (rq, an atomic) when
+// the target is on this rank; the exchange carries the others as counts to the
+// target's rank (k_pack / k_unpack, gp_xchg.hip).  No per-edge pass runs.
 //
 // Work items (patch, x-segment) are dealt XCD-contiguously: the waves of one
 // XCD own one y-band of every plane, so y-halo rows come from the XCD's L2.
-// The random-edge bitmap of these kernels has one 64-bit word per row segment:
-// word ((x - x_lo) * g + y) * zsegs + z / 64, bit z % 64 (col_rb_word).
 // Built with -ffp-contract=off: the fold must round exactly like the oracle.
 #include "gp_wavecommon.hpp"
 
@@ -36,28 +36,6 @@ namespace {
 
 using namespace wk;
 constexpr int NR = 4;  // y rows per patch
-
-__device__ __forceinline__ uint32_t col_rb_word(const WaveArgs& a, uint32_t x, uint32_t y, uint32_t z) {
-    return ((x - a.x_lo) * a.G.g + y) * a.zsegs + (z >> 6);
-}
-
-// Did sender i (on this rank) use its random edge in round r?  Its direction
-// draw of round r (counter (i, r), SRS v1 B.2) must pick the random slot -- the
-// last one, deg - 1 -- and, unless every node is active, it must have been
-// active: the bitmap bit (= active and that draw).  Redrawing first reads the
-// bitmap (a random 8-byte load, one 128-byte line) only for the ~1/7 of in-edges
-// whose draw selects the random slot.
-__device__ __forceinline__ bool col_sent_random(const WaveArgs& a, uint32_t i, uint32_t r, bool all_active,
-                                                uint32_t stream) {
-    const Geom& G = a.G;
-    const uint32_t x = fastdiv(i, G.div_g2);
-    const uint32_t rem = i - x * G.g2;
-    const uint32_t y = fastdiv(rem, G.div_g);
-    const uint32_t z = rem - y * G.g;
-    const uint32_t di = popc6(mask_xyz(x, y, z, G.g - 1)) + 1u;
-    if (uniform(a.k0, a.k1, stream, i, r, di) != di - 1u) return false;
-    return all_active || ((a.rbc[col_rb_word(a, x, y, z)] >> (z & 63)) & 1ull);
-}
 
 // XCD-contiguous deal of n work items over the grid's waves (speed only).
 __device__ __forceinline__ void item_range(uint32_t n, uint32_t& it, uint32_t& end, uint32_t& step) {
@@ -89,7 +67,6 @@ __global__ __launch_bounds__(BULK_THREADS, GP_COL_MINW(TOPO)) void k_gossip_col(
     const int lane = threadIdx.x & 63;
     const uint8_t* __restrict__ nbc = a.nbc;
     const uint32_t g = a.G.g, g2 = a.G.g2, base = a.base, lo = a.lo;
-    const bool push = a.rq_cur != nullptr;  // one rank: senders count random-edge deliveries (no k_gossip_redges)
     uint32_t alerts = 0;
 
     uint32_t it, it_end, it_step;
@@ -155,12 +132,8 @@ __global__ __launch_bounds__(BULK_THREADS, GP_COL_MINW(TOPO)) void k_gossip_col(
                 led[k] = nbc[(rv[k] && ledge) ? (lane == 0 ? jl - 1 : jl + 1) : jl];
                 lrc[k] = lrd[k] = 0u;
                 if (TOPO == IMP3D) {
-                    if (push) {
-                        lrc[k] = a.rq_cur[px + yo[k] - lo];
-                        lrd[k] = a.rnd[px + yo[k] - lo];
-                    } else {
-                        lrc[k] = a.rcnt[px + yo[k] - lo];
-                    }
+                    lrc[k] = a.rq_cur[px + yo[k] - lo];
+                    lrd[k] = a.rnd[px + yo[k] - lo];
                 }
             }
             const bool hmv = zv && y0 > 0, hpv = zv && y0 + NR < g;
@@ -212,16 +185,13 @@ __global__ __launch_bounds__(BULK_THREADS, GP_COL_MINW(TOPO)) void k_gossip_col(
                     if (deg > 0) dir = slot_to_dir(mask, uniform(a.k0, a.k1, S_GOSSIP, j, r + 1, deg));
                 }
                 if (rv[k]) a.nbn[j - base] = (uint8_t)dir;
-                if (TOPO == IMP3D && push && rv[k]) {
-                    // one rank, push form: this round's count consumed, and a send on the
-                    // random edge next round counted at its target now (the receiver
-                    // drops it at round start if converged, Program.fs:87)
+                if (TOPO == IMP3D && rv[k]) {
+                    // this round's count consumed, and a send on the random edge next round
+                    // counted at its target now (the receiver drops it at round start if
+                    // converged, Program.fs:87); a target on another rank gets it through
+                    // the exchange (k_pack reads this direction byte)
                     if (lrc[k]) a.rq_cur[j - lo] = 0u;
-                    if (dir == DIR_RANDOM) atomicAdd(&a.rq_next[lrd[k] - lo], 1u);
-                }
-                if (TOPO == IMP3D && !push) {  // several ranks: the delivery pass reads these bits
-                    const unsigned long long bits = __ballot(rv[k] && dir == DIR_RANDOM);
-                    if (lane == 0 && y0 + k < g) a.rbn[col_rb_word(a, x, y0 + k, zs * 64)] = bits;
+                    if (dir == DIR_RANDOM && lrd[k] - lo < a.nloc) atomicAdd(&a.rq_next[lrd[k] - lo], 1u);
                 }
             }
             pb = cb;
@@ -232,149 +202,15 @@ __global__ __launch_bounds__(BULK_THREADS, GP_COL_MINW(TOPO)) void k_gossip_col(
     block_add2(alerts, 0u, &ctl->round_alerts, nullptr);
 }
 
-// Imp3D gossip, before the column kernel: per local receiver, how many of its
-// in-edge senders sent it a rumour on their random edge this round.  Tiles of
-// RE_TILE receivers: the tile's in-edges (receiver-sorted, contiguous) are
-// decided RE_FU per thread -- senders loaded together, their direction draws as
-// one Philox batch, the bitmap read only for the ~1/7 that pick the random slot
-// (col_sent_random), remote senders by the exchange tag -- into a byte per edge
-// in LDS, then every receiver sums its edge range.  Inside the x-march these
-// were three dependent memory round trips per patch step.
-constexpr uint32_t RE_TILE = 1024;
-constexpr int RE_FU = 6;  // staged in-edges per thread: 1536 per tile (mean 1024, 16 sigma)
-
-// Tiles are software-pipelined one step deep: tile t's edge range and senders
-// were loaded during the previous tile of this block, so a tile costs one
-// exposed memory round trip (the bitmap reads of its picks) instead of three
-// (range -> senders -> bitmap).  Loads are unconditional where possible
-// (clamped indices) and the barriers wait for LDS only, so the next tile's
-// loads stay in flight across them.
-__device__ __forceinline__ void redges_src(const WaveArgs& a, uint32_t e_lo, uint32_t e_hi, uint32_t (&src)[RE_FU]) {
-    const uint32_t cnt = e_hi - e_lo;
-#pragma unroll
-    for (int m = 0; m < RE_FU; ++m) {
-        const uint32_t q = threadIdx.x + m * BULK_THREADS;
-        src[m] = a.in_src[cnt ? e_lo + min(q, cnt - 1u) : 0u];  // lanes with q >= cnt: never used
-    }
-}
-
-__device__ __forceinline__ void lds_barrier_only() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-#ifndef GP_RE_MINW
-#define GP_RE_MINW 5  // delivery pass: waves per SIMD (5: 96 VGPRs, no spills; 4 measured slower, profiles/r02/c3_redges/minw.txt)
-#endif
-__global__ __launch_bounds__(BULK_THREADS, GP_RE_MINW) void k_gossip_redges(WaveArgs a, uint32_t r) {
-    __shared__ uint8_t sent[BULK_THREADS * RE_FU];
-    if (ld_agent(&a.ctl->done)) return;
-    const uint32_t lo = a.lo, nloc = a.nloc;
-    const Geom& G = a.G;
-    constexpr int NPT = RE_TILE / BULK_THREADS;
-    const uint32_t ntl = (nloc + RE_TILE - 1) / RE_TILE;
-    uint32_t t = blockIdx.x;
-    if (t >= ntl) return;
-    uint32_t e_lo = a.in_off[t * RE_TILE], e_hi = a.in_off[min(nloc, t * RE_TILE + RE_TILE)];
-    uint32_t src[RE_FU];
-    redges_src(a, e_lo, e_hi, src);
-    for (;;) {
-        const uint32_t j0 = t * RE_TILE, j1 = min(nloc, j0 + RE_TILE);  // local receiver ids
-        const uint32_t tn = t + gridDim.x;
-        const bool more = tn < ntl;  // block-uniform
-        const uint32_t cnt = e_hi - e_lo;
-        const bool staged = cnt <= (uint32_t)(BULK_THREADS * RE_FU);
-        uint32_t eb[NPT], ee[NPT];
-#pragma unroll
-        for (int k = 0; k < NPT; ++k) {
-            const uint32_t jl = min(j0 + k * BULK_THREADS + threadIdx.x, j1 - 1u);
-            eb[k] = a.in_off[jl];
-            ee[k] = a.in_off[jl + 1];
-        }
-        uint32_t n_lo = 0, n_hi = 0;
-        if (more) {
-            n_lo = a.in_off[tn * RE_TILE];
-            n_hi = a.in_off[min(nloc, tn * RE_TILE + RE_TILE)];
-        }
-        if (staged) {
-            uint32_t di[RE_FU], wrd[RE_FU], zb[RE_FU], X[RE_FU], Y[RE_FU];
-#pragma unroll
-            for (int m = 0; m < RE_FU; ++m) {
-                const uint32_t i = src[m];
-                const uint32_t x = fastdiv(i, G.div_g2);
-                const uint32_t rem = i - x * G.g2;
-                const uint32_t y = fastdiv(rem, G.div_g);
-                const uint32_t z = rem - y * G.g;
-                di[m] = popc6(mask_xyz(x, y, z, G.g - 1)) + 1u;
-                wrd[m] = i - lo < nloc ? col_rb_word(a, x, y, z) : 0u;
-                zb[m] = z & 63u;
-            }
-            philox2_batch<RE_FU>(src, r, S_GOSSIP, a.k0, a.k1, X, Y);
-            unsigned long long w[RE_FU];
-#pragma unroll
-            for (int m = 0; m < RE_FU; ++m) {
-                const uint32_t q = threadIdx.x + m * BULK_THREADS;
-                const uint32_t i = src[m];
-                w[m] = 0ull;
-                if (q < cnt) {
-                    if (i - lo >= nloc) w[m] = a.rtag[e_lo + q] == r ? ~0ull : 0ull;  // sender on another rank
-                    else if (uniform_from(X[m], Y[m], di[m]) == di[m] - 1u) w[m] = a.rbc[wrd[m]];
-                }
-            }
-            // the next tile's senders, behind this tile's bitmap reads (issued on every
-            // path -- the last tile reloads its own -- so the wait below counts them)
-            redges_src(a, more ? n_lo : e_lo, more ? n_hi : e_hi, src);
-#pragma unroll
-            for (int m = 0; m < RE_FU; ++m) sent[threadIdx.x + m * BULK_THREADS] = (uint8_t)((w[m] >> zb[m]) & 1ull);
-        } else {
-            redges_src(a, more ? n_lo : e_lo, more ? n_hi : e_hi, src);
-        }
-        lds_barrier_only();
-#pragma unroll
-        for (int k = 0; k < NPT; ++k) {
-            const uint32_t jl = j0 + k * BULK_THREADS + threadIdx.x;
-            if (jl >= j1) continue;
-            uint32_t n = 0;
-            if (staged) {
-                for (uint32_t e = eb[k]; e < ee[k]; ++e) n += sent[e - e_lo];
-            } else {  // rare: tile in-degree above the staging capacity
-                for (uint32_t e = eb[k]; e < ee[k]; ++e) {
-                    const uint32_t i = a.in_src[e];
-                    if (i - lo >= nloc) n += a.rtag[e] == r ? 1u : 0u;
-                    else n += col_sent_random(a, i, r, false, S_GOSSIP) ? 1u : 0u;
-                }
-            }
-            a.rcnt[jl] = (uint16_t)n;
-        }
-        if (!more) break;
-        lds_barrier_only();
-        t = tn;
-        e_lo = n_lo;
-        e_hi = n_hi;
-    }
-}
-
-// Random-edge bits of round 0 in the column layout (only the seed can be sending).
-// Every word is written exactly once (the seed's word with its bit), so no
-// store can race the seed's bit away.
-__global__ __launch_bounds__(BULK_THREADS) void k_col_rbits_init(WaveArgs a, const uint8_t* nb0, uint32_t words) {
+// Imp3D gossip, round 0: the seed's send on its random edge (only the seed can be
+// sending), counted at its target when the target is on this rank (otherwise the
+// exchange of round 0 carries it).
+__global__ void k_col_seed_init(WaveArgs a, const uint8_t* nb0) {
     const uint32_t i = a.seed_node;
-    uint32_t sw = 0xFFFFFFFFu;
-    unsigned long long sbit = 0ull;
-    if (i - a.lo < a.nloc && (nb0[i - a.base] & DIR_MASK) == DIR_RANDOM) {
-        const Geom& G = a.G;
-        const uint32_t x = fastdiv(i, G.div_g2);
-        const uint32_t rem = i - x * G.g2;
-        const uint32_t y = fastdiv(rem, G.div_g);
-        const uint32_t z = rem - y * G.g;
-        sw = col_rb_word(a, x, y, z);
-        sbit = 1ull << (z & 63);
-    }
-    if (a.rbn)  // (gossip, one rank, push form: no bitmap)
-        for (uint32_t w = blockIdx.x * BULK_THREADS + threadIdx.x; w < words; w += gridDim.x * BULK_THREADS)
-            a.rbn[w] = w == sw ? sbit : 0ull;
-    // one rank, push form: the seed's round-0 send on its random edge, counted at the target
-    if (a.rq_cur && sbit && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&a.rq_cur[a.rnd[i - a.lo] - a.lo], 1u);
+    if (i - a.lo >= a.nloc || (nb0[i - a.base] & DIR_MASK) != DIR_RANDOM) return;
+    const uint32_t t = a.rnd[i - a.lo] - a.lo;
+    if (t < a.nloc) atomicAdd(&a.rq_cur[t], 1u);
 }
-
-uint32_t col_rbits_words(uint32_t planes, uint32_t g) { return planes * g * ((g + 63) / 64) + 16u; }
 
 int col_blocks_per_cu(int topo, int alg) {
     (void)alg;
@@ -392,21 +228,17 @@ hipError_t launch_round_col(const WaveArgs& a, int topo, int alg, uint32_t round
         if (topo == GRID3D) {
             hipLaunchKernelGGL(k_gossip_col<GRID3D>, g, b, 0, st, a, round);
         } else {
-            if (!a.rq_cur) {  // several ranks: receivers decide their in-edges (exchange tags for remote senders)
-                if (!a.rcnt) return hipErrorInvalidValue;
-                const uint32_t ge = std::min<uint32_t>((a.nloc + RE_TILE - 1) / RE_TILE, 256u * 16u);
-                hipLaunchKernelGGL(k_gossip_redges, dim3(std::max(1u, ge)), b, 0, st, a, round);
-            }
+            if (!a.rq_cur || !a.rq_next || !a.rnd) return hipErrorInvalidValue;
             hipLaunchKernelGGL(k_gossip_col<IMP3D>, g, b, 0, st, a, round);
         }
     }
     return hipGetLastError();
 }
 
-hipError_t launch_col_rbits_init(const DevState& S, hipStream_t st) {
+hipError_t launch_col_seed_init(const DevState& S, hipStream_t st) {
+    if (S.topo != IMP3D) return hipSuccess;
     WaveArgs a = make_wave_args(S, 0);
-    a.rbn = S.rbits[0];  // the bits of round 0's sends
-    hipLaunchKernelGGL(k_col_rbits_init, dim3(256), dim3(BULK_THREADS), 0, st, a, S.nb[0], S.rbits_words);
+    hipLaunchKernelGGL(k_col_seed_init, dim3(1), dim3(1), 0, st, a, S.nb[0]);
     return hipGetLastError();
 }
 
@@ -424,7 +256,6 @@ WaveArgs make_wave_args(const DevState& S, uint32_t round) {
     a.rtag = S.rtag;
     a.rmsg = S.rmsg;
     a.c = S.c;
-    a.rcnt = S.rcnt;
     a.rq_cur = S.rq[round & 1];
     a.rq_next = S.rq[(round + 1) & 1];
     a.rnd = S.rnd;

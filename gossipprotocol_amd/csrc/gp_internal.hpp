@@ -131,10 +131,11 @@ struct DevState {
     uint8_t* nb[2];
     // gossip: rumour counters (in place), direction byte double buffered (nb)
     int32_t* c;
-    // gossip, Imp3D, column kernel: random-edge rumours each local node receives
-    // this round (k_gossip_redges, before the round kernel), indexed from lo
-    uint16_t* rcnt;
-    uint32_t* rq[2];      // gossip Imp3D column kernel, one rank: random-edge deliveries per node, by round parity
+    // gossip, Imp3D, column kernel: random-edge rumours each local node receives, by
+    // round parity, indexed from lo -- counted a round ahead by the senders (atomics
+    // from local senders in k_gossip_col, the exchange's counts from remote ones in
+    // k_unpack) and read (then zeroed) by the receiver
+    uint32_t* rq[2];
     // Imp3D: bit i of rbits[b] = node i sends on its random edge in the round
     // of buffer b (ballot-packed by the round kernel)
     uint64_t* rbits[2];
@@ -230,9 +231,8 @@ struct WaveArgs {
     const uint32_t* rtag;
     const double2* rmsg;
     int32_t* c;
-    uint16_t* rcnt;          // gossip Imp3D (column kernel): random-edge deliveries per local node
-    uint32_t* rq_cur;        // one rank: this round's random-edge deliveries per node (read, then zeroed)
-    uint32_t* rq_next;       // one rank: next round's, counted by their senders with atomics
+    uint32_t* rq_cur;        // Imp3D gossip: this round's random-edge deliveries per local node (read, then zeroed)
+    uint32_t* rq_next;       // next round's, counted by local senders with atomics (remote ones: k_unpack)
     const uint32_t* rnd;     // random edge of each local sender (id - lo)
     Ctl* ctl;
     Geom G;
@@ -248,9 +248,8 @@ WaveArgs make_wave_args(const DevState& S, uint32_t round);
 
 hipError_t launch_round_col(const WaveArgs& a, int topo, int alg, uint32_t round, int grid, hipStream_t st);
 int col_blocks_per_cu(int topo, int alg);
-// random-edge bitmap words of the column layout (one 64-bit word per 64-node row segment)
-uint32_t col_rbits_words(uint32_t planes, uint32_t g);
-hipError_t launch_col_rbits_init(const DevState& S, hipStream_t st);
+// Imp3D gossip: count the seed's round-0 random-edge send at its target (rq)
+hipError_t launch_col_seed_init(const DevState& S, hipStream_t st);
 
 // ---- tiled round kernels (gp_round.hip)
 uint32_t rbits_words_for(uint32_t lo, uint32_t nloc);

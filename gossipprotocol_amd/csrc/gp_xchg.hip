@@ -6,7 +6,9 @@
 // packs, per destination rank, the messages of its senders that chose their
 // random edge for round r+1 (dir byte == DIR_RANDOM, written by the round
 // kernel): {slot, (s, w)} where `slot` is the message's in-edge position in the
-// destination's receiver-sorted CSR (static, precomputed).  Buffers have a
+// destination's receiver-sorted CSR (static, precomputed) -- or, for gossip on the
+// column kernel, {target's local id}: a rumour count the receiver adds to its
+// next-round delivery counter (integer, so order-free).  Buffers have a
 // fixed capacity per rank pair (expected count + 12 sigma), so
 // RCCL moves fixed sizes on the stream with no host synchronisation; the
 // in-band count says how many entries are real, and an overflow is recorded
@@ -16,6 +18,8 @@
 // node is active a push-sum sender's draw alone decides, remote or not).  Entry
 // order inside a buffer does not matter: every
 // message carries its slot, so results are independent of the atomics' order.
+#include <algorithm>
+
 #include "gp_xchg.hpp"
 
 namespace gp {
@@ -31,7 +35,8 @@ __device__ __forceinline__ uint32_t owner_of(uint32_t t, const uint32_t* bounds,
 
 // Range binning: a block owns PACK_RANGE consecutive senders.  Sweep 1 finds
 // every sender's destination rank (its next direction is the random edge and
-// the edge's target lives elsewhere), kept as a nibble per sender in registers,
+// the edge's target lives elsewhere: xdst, a byte per sender precomputed at
+// create, instead of the 4-byte edge), kept as a nibble per sender in registers,
 // and counts them per rank in LDS; one global reservation per (block, rank)
 // on the buffer's in-band counter; sweep 2 writes each message at the block's
 // run offset (an LDS counter per rank).  (The previous form reserved per wave
@@ -49,6 +54,7 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
     if (threadIdx.x < XMAXW) cnt[threadIdx.x] = 0u;
     if (threadIdx.x <= (uint32_t)a.W) bnd[threadIdx.x] = a.bounds[threadIdx.x];
     __syncthreads();
+    const uint32_t me = (uint32_t)a.me;
     const uint32_t last = a.nloc - 1;
     // destination rank per sender, a nibble each; `me` means "no message" (a sender never
     // packs for its own rank, so the value is free for every world size up to XMAXW = 16)
@@ -56,25 +62,21 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
     uint32_t dst[PACK_PER / 8];
 #pragma unroll
     for (int g = 0; g < PACK_PER / 8; ++g) {
-        uint8_t b[8];
-        uint32_t t[8];
+        uint8_t b[8], t[8];
 #pragma unroll
         for (int h = 0; h < 8; ++h) {  // unconditional loads (clamped), all in flight
             const uint32_t li = min(r0 + (g * 8 + h) * 256u + threadIdx.x, last);
             b[h] = a.nbn[a.lo + li - a.base];
-            t[h] = a.rnd[li];
+            t[h] = a.xdst[li];
         }
         uint32_t w = 0;
 #pragma unroll
         for (int h = 0; h < 8; ++h) {
             const uint32_t li = r0 + (g * 8 + h) * 256u + threadIdx.x;
             uint32_t d = none;
-            if (li < a.nloc && (b[h] & DIR_MASK) == DIR_RANDOM) {
-                const uint32_t own = owner_of(t[h], bnd, a.W);
-                if (own != (uint32_t)a.me) {
-                    d = own;
-                    atomicAdd(&cnt[own], 1u);
-                }
+            if (li < a.nloc && (b[h] & DIR_MASK) == DIR_RANDOM && t[h] != me) {
+                d = t[h];
+                atomicAdd(&cnt[d], 1u);
             }
             w |= d << (4 * h);
         }
@@ -95,7 +97,7 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
             const uint32_t li = r0 + (g * 8 + h) * 256u + threadIdx.x;
             const uint32_t idx = atomicAdd(&off[d], 1u);
             if (idx < a.peer[d].cap) {
-                a.peer[d].slots[idx] = a.pos[li];
+                a.peer[d].slots[idx] = a.counts ? a.rnd[li] - bnd[d] : a.pos[li];
                 if (a.push) a.peer[d].vals[idx] = a.swn[a.lo + li - a.base];
             } else {
                 atomicOr(a.overflow, 1u);
@@ -104,22 +106,42 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
     }
 }
 
-// blockIdx.y = source rank.
+// blockIdx.y = source rank.  A thread owns UNP entries UNP_STRIDE apart: their
+// slots and payloads are loaded together (all in flight), then the scatters.  The
+// grid covers the largest buffer's capacity (launch_unpack), so no thread loops.
+constexpr int UNP = 4;
+constexpr uint32_t UNP_BLOCK = 256u * UNP;
 __global__ __launch_bounds__(256) void k_unpack(UnpackArgs a, uint32_t round) {
     const int p = blockIdx.y;
     if (p == a.me || !a.peer[p].cnt) return;
     const uint32_t sent = *a.peer[p].cnt;
     if (sent > a.peer[p].cap && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.overflow, 1u);
     const uint32_t n = min(sent, a.peer[p].cap);
+    const uint32_t k0 = blockIdx.x * UNP_BLOCK + threadIdx.x;
+    if (k0 >= n) return;
     // push-sum with every node active: the round kernels decide remote senders by their
     // Philox draw and read no tag (all_active only ever goes 0 -> 1, and a round kernel
     // reads it after this unpack); gossip and the activation phase need the tags
     const bool tags = !a.push || __hip_atomic_load(a.all_active, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
-    for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < n; k += gridDim.x * 256) {
-        const uint32_t slot = a.peer[p].slots[k];
-        if (slot >= a.nedges) continue;  // never: slots are in-edge positions of this rank
-        if (tags) a.rtag[slot] = round;
-        if (a.push) a.rmsg[slot] = a.peer[p].vals[k];
+    uint32_t slot[UNP];
+    double2 v[UNP];
+#pragma unroll
+    for (int u = 0; u < UNP; ++u) {  // clamped: every load unconditional
+        const uint32_t k = min(k0 + u * 256u, n - 1u);
+        slot[u] = a.peer[p].slots[k];
+        if (a.push) v[u] = a.peer[p].vals[k];
+    }
+#pragma unroll
+    for (int u = 0; u < UNP; ++u) {
+        if (k0 + u * 256u >= n) break;
+        const uint32_t e = slot[u];
+        if (e >= a.nedges) continue;  // never: slots are in-edge positions (or nodes) of this rank
+        if (a.rq) {  // gossip column kernel: a rumour for local node `e` next round (integer count)
+            atomicAdd(&a.rq[e], 1u);
+            continue;
+        }
+        if (tags) a.rtag[e] = round;
+        if (a.push) a.rmsg[e] = v[u];
     }
 }
 
@@ -153,12 +175,14 @@ __global__ __launch_bounds__(256) void k_sub(uint32_t* v, uint32_t n, uint32_t d
     for (uint32_t q = blockIdx.x * 256 + threadIdx.x; q < n; q += gridDim.x * 256) v[q] -= d;
 }
 
-// pos[li] = position of sender lo+li in its target owner's local in-edge array
-// (global sorted position minus the owner's first edge); ~0 for local targets.
+// xdst[li] = owner rank of sender lo+li's random-edge target; pos[li] = position
+// of the sender in that owner's local in-edge array (global sorted position minus
+// the owner's first edge), ~0 for local targets.
 __global__ __launch_bounds__(256) void k_make_pos(PosArgs a) {
     for (uint32_t li = blockIdx.x * 256 + threadIdx.x; li < a.nloc; li += gridDim.x * 256) {
         const uint32_t own = owner_of(a.rnd[li], a.bounds, a.W);
-        a.pos[li] = own == (uint32_t)a.me ? 0xFFFFFFFFu : a.inv[a.lo + li] - a.edge0[own];
+        a.xdst[li] = (uint8_t)own;
+        if (a.pos) a.pos[li] = own == (uint32_t)a.me ? 0xFFFFFFFFu : a.inv[a.lo + li] - a.edge0[own];
     }
 }
 
@@ -194,7 +218,12 @@ hipError_t launch_pack(const PackArgs& a, int grid, hipStream_t st) {
     return hipGetLastError();
 }
 hipError_t launch_unpack(const UnpackArgs& a, uint32_t round, int grid, hipStream_t st) {
-    hipLaunchKernelGGL(k_unpack, dim3(grid, a.W), dim3(256), 0, st, a, round);
+    (void)grid;
+    uint32_t cap = 0;
+    for (int p = 0; p < a.W; ++p)
+        if (p != a.me) cap = std::max(cap, a.peer[p].cap);
+    const uint32_t blocks = (cap + UNP_BLOCK - 1) / UNP_BLOCK;
+    if (blocks) hipLaunchKernelGGL(k_unpack, dim3(blocks, a.W), dim3(256), 0, st, a, round);
     return hipGetLastError();
 }
 hipError_t launch_zero_counts(const ZeroArgs& z, hipStream_t st) {

@@ -20,9 +20,12 @@ struct PackArgs {
     const uint8_t* nbn;   // node bytes of the round being prepared (local array, id - base)
     const double2* swn;   // (s, w) of that round (local array, id - base)
     const uint32_t* rnd;  // random edge of each local sender (id - lo)
-    const uint32_t* pos;  // its slot in the destination's in-edge array (id - lo)
+    const uint8_t* xdst;  // owner rank of that edge's target (id - lo)
+    const uint32_t* pos;  // its slot in the destination's in-edge array (id - lo; null in counts mode)
     uint32_t lo, nloc, base;
     int W, me, push;
+    int counts;           // gossip column kernel: the entry is the target's local id at its owner
+                          // (a delivery count, k_unpack adds it to rq), not an in-edge slot
     uint32_t bounds[XMAXW + 1];
     XPeer peer[XMAXW];    // send side
     unsigned int* overflow;
@@ -31,7 +34,8 @@ struct PackArgs {
 struct UnpackArgs {
     uint32_t* rtag;
     double2* rmsg;
-    uint32_t nedges;
+    uint32_t* rq;         // counts mode (gossip column kernel): next round's deliveries per local node
+    uint32_t nedges;      // entries must be below this bound (in-edges; counts mode: local nodes)
     int W, me, push;
     XPeer peer[XMAXW];    // receive side
     unsigned int* overflow;  // set when a sender packed more messages than the buffer holds
@@ -51,7 +55,8 @@ struct SumArgs {
 struct PosArgs {
     const uint32_t* rnd;  // local senders' random edges
     const uint32_t* inv;  // global sorted position of every sender
-    uint32_t* pos;
+    uint32_t* pos;        // may be null (counts mode)
+    uint8_t* xdst;
     uint32_t lo, nloc;
     int W, me;
     uint32_t bounds[XMAXW + 1];

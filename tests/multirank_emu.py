@@ -10,10 +10,13 @@ ranks only through the library's exchange plan:
     bytes -- here the direction / active fields -- and (s, w) goes to the
     neighbouring rank (gp_api.hip exchange, halo part);
   * random-edge messages: every sender whose next direction is its random edge
-    and whose target lives on another rank sends {slot, s, w} with `slot` =
-    the message's position in the destination's receiver-sorted in-edge array,
-    computed from the global stable sort exactly like build_imp3d / k_make_pos;
-    the receiver tags rtag[slot] = round (gp_xchg.hip k_pack / k_unpack);
+    and whose target lives on another rank sends, for push-sum, {slot, s, w}
+    with `slot` = the message's position in the destination's receiver-sorted
+    in-edge array, computed from the global stable sort exactly like
+    build_imp3d / k_make_pos (the receiver tags rtag[slot] = round, gp_xchg.hip
+    k_pack / k_unpack); for gossip (the column kernel's counts mode) {target's
+    local id}, a rumour the receiver counts for the next round -- local senders
+    count theirs at the target directly (k_gossip_col);
   * bookkeeping: {alerts, newly active, injector pick converged} summed over
     ranks (k_finalize_pre / all-reduce / k_finalize_post); the gossip
     injector's live list is replicated on every rank;
@@ -233,6 +236,12 @@ class RankSim:
                         f[hi_l:hi_l + H] = v.astype(f.dtype)
             if self.alg == "push-sum":
                 self.active = fields[3].astype(bool)
+        if self.topo == "Imp3D" and self.alg == "gossip":
+            # counts for round rn: local random-edge sends at their targets (k_gossip_col)
+            mydir = self.dir[self._local(self.ids)]
+            self.rq = np.zeros(self.hi - self.lo, dtype=np.int64)
+            mine = (mydir == DIR_RANDOM) & (self.owner == self.rank)
+            np.add.at(self.rq, self.rnd[mine] - self.lo, 1)
         if self.topo == "Imp3D" and self.W > 1:
             mydir = self.dir[self._local(self.ids)]
             send = (mydir == DIR_RANDOM) & (self.owner != self.rank)
@@ -242,18 +251,20 @@ class RankSim:
                 if self.alg == "push-sum":
                     li = self._local(self.ids[sel])
                     packets[p] = (self.pos[sel], self.s[li], self.w[li])
-                else:
-                    packets[p] = (self.pos[sel],)
+                else:  # counts: the target's id local to its owner
+                    packets[p] = (self.rnd[sel] - self.bounds[p],)
             got = [None] * self.W
             d.all_gather_object(got, packets)
             for src, pk in enumerate(got):
                 if src == self.rank:
                     continue
                 msg = pk[self.rank]
-                self.rtag[msg[0]] = rn
                 if self.alg == "push-sum":
+                    self.rtag[msg[0]] = rn
                     self.rmsg[msg[0], 0] = msg[1]
                     self.rmsg[msg[0], 1] = msg[2]
+                else:
+                    np.add.at(self.rq, msg[0], 1)
         _ = torch  # gloo transport via torch.distributed
 
     def _allreduce(self, vals):
@@ -348,13 +359,8 @@ class RankSim:
             ok = n >= 0
             ln = self._local(np.where(ok, n, self.lo))
             inc += ok & (self.dir[ln] == (d ^ 1))
-        if self.topo == "Imp3D":
-            sent, _ = self._random_in(r)
-            indeg = np.diff(self.in_off)
-            for k in range(int(indeg.max()) if len(indeg) else 0):
-                has = indeg > k
-                e = np.where(has, self.in_off[:-1] + k, 0)
-                inc += has & sent[e]
+        if self.topo == "Imp3D":  # random-edge rumours, counted a round ahead (local + exchanged)
+            inc += self.rq
         if self.lo <= self.inj < self.hi:
             inc[self.inj - self.lo] += 1
         inc[conv] = 0                                   # dropped at converged receivers (Program.fs:87)

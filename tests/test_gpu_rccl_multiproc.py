@@ -73,6 +73,8 @@ CASES = [
     (2, 2000, "line", "gossip", 7, 300),
     (4, 64000, "Imp3D", "push-sum", 8, 120),
     (4, 40000, "full", "push-sum", 9, 30),
+    (2, 200**3, "Imp3D", "gossip", 4, 150),  # g = 200: the column kernel, random-edge counts through the exchange
+    (3, 200**3, "Imp3D", "gossip", 6, 120),
 ]
 
 
