@@ -69,7 +69,17 @@ int run(const Args& a, int rank, int world, const char* rdv) {
         if ((rc = gp_rendezvous_id(rank, rdv, 600000, uid)) == 0) {
             cfg.num_gpus = world;
             if (!a.device_set) cfg.device = rank;
+            // RCCL prints its version line on stdout when the communicator starts: keep
+            // stdout for the reference's contract (the line goes to stderr)
+            std::fflush(stdout);
+            const int saved = dup(1);
+            if (saved >= 0) dup2(2, 1);
             rc = gp_create_rank(&cfg, rank, world, uid, &sim);
+            std::fflush(stdout);
+            if (saved >= 0) {
+                dup2(saved, 1);
+                close(saved);
+            }
         }
     }
     if (rc) {

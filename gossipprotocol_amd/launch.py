@@ -16,6 +16,8 @@ fresh file path for gp_rendezvous_id (rank 0's RCCL id).
 """
 from __future__ import annotations
 
+import contextlib
+import ctypes
 import os
 import shutil
 import signal
@@ -24,6 +26,25 @@ import subprocess
 import sys
 import tempfile
 import time
+
+
+@contextlib.contextmanager
+def stdout_to_stderr():
+    """Route file descriptor 1 to stderr for the duration (RCCL prints its version
+    line on stdout when a communicator starts; stdout is the reference's contract
+    / bench.py's one JSON line).  C stdio is flushed on both edges."""
+    libc = ctypes.CDLL(None)
+    sys.stdout.flush()
+    libc.fflush(None)
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        yield
+    finally:
+        sys.stdout.flush()
+        libc.fflush(None)
+        os.dup2(saved, 1)
+        os.close(saved)
 
 
 def free_port() -> int:

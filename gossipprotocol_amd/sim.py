@@ -78,7 +78,10 @@ class Simulation:
                 box = [uid.raw if rank == 0 else None]
                 dist.broadcast_object_list(box, src=0)
                 uid = C.create_string_buffer(box[0], 128)
-            self._chk(self._L.gp_create_rank(C.byref(cfg), rank, world, uid, C.byref(h)))
+            from .launch import stdout_to_stderr
+            with stdout_to_stderr():  # (RCCL's version line)
+                rc = self._L.gp_create_rank(C.byref(cfg), rank, world, uid, C.byref(h))
+            self._chk(rc)
         else:
             self._chk(self._L.gp_create(C.byref(cfg), C.byref(h)))
         self._h = h
