@@ -127,6 +127,27 @@ def launch_ranks(args):
                      env_for_rank=lambda r: {"GP_BENCH_LAUNCHED": "1"}, log=log)
 
 
+def akka_baseline():
+    """north_star's "original Akka reference timed on the box's host cores": needs a
+    .NET SDK (and the reference tree, which the GPU box does not have); recorded as
+    unavailable with the host's core count and CPU model (tools/akka_timing.py runs
+    it where dotnet exists)."""
+    import shutil
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
+    except OSError:
+        pass
+    rec = {"nproc": os.cpu_count(), "cpu_model": model,
+           "sched_cores": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None}
+    if shutil.which("dotnet") is None:
+        rec["status"] = "unavailable (no dotnet)"
+    else:
+        rec["status"] = "unavailable (dotnet present; run tools/akka_timing.py where the reference tree is)"
+    return rec
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -268,6 +289,7 @@ def main():
         out["roofline"]["traffic_detail"] = {"method": traffic_note}
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args)
+    out["akka_baseline"] = akka_baseline()
     if rank == 0 and world == 1 and args.converge:
         with Simulation(args.nodes, args.topology, args.algorithm, seed=args.seed, device=device) as s2:
             res = s2.run()

@@ -32,7 +32,9 @@ def main():
     alerts, kms, active_round = [], [], None
     t0 = time.perf_counter()
     while True:
-        a = sim.step(64 if active_round is None and alg == "push-sum" else 1024)
+        # 8-round steps until every node is active, so the activation round is exact to 8
+        # (bench.py's pre-roll does the same); then 1024-round batches
+        a = sim.step(8 if active_round is None and alg == "push-sum" else 1024)
         ms, k, name = sim.kernel_stats(reset=True)
         alerts += a
         kms.append((len(a), ms))
@@ -40,6 +42,8 @@ def main():
             active_round = sim.rounds
         if not a or sim.alerts_total >= T:
             break
+        if len(a) == 8 and active_round is None:
+            continue
         print(f"[converge] round {sim.rounds}: alerts {sim.alerts_total} of {T} "
               f"({time.perf_counter() - t0:.1f} s)", file=sys.stderr, flush=True)
     wall = time.perf_counter() - t0
