@@ -18,7 +18,7 @@ print('fds after load:', [f for f in fds if 'kfd' in f or 'dri' in f])
 " > $O/kfd_on_load.txt 2>&1; cat $O/kfd_on_load.txt
 timeout -k 10 700 python3 -u -m pytest -x -v --timeout 400 --timeout-method thread --durations=30 \
   tests/test_gpu_launcher.py tests/test_gpu_multirank.py::test_virtual_ranks_max_world \
-  "tests/test_gpu_multirank.py::test_virtual_ranks_parity" -k "col or max_world or launcher or rccl_processes or full_size" \
+  "tests/test_gpu_multirank.py::test_virtual_ranks_parity" -k "col or max_world or launcher or rccl_processes or full_size_1e9" \
   "tests/test_gpu_rccl_multiproc.py::test_rccl_processes_match_single" \
-  "tests/test_gpu_parity.py::test_full_size_imp3d_pushsum_1e9_rounds" > $O/pytest.log 2>&1
+  "tests/test_gpu_parity.py" > $O/pytest.log 2>&1
 rc=$?; tail -45 $O/pytest.log; exit $rc

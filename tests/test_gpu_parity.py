@@ -213,47 +213,74 @@ def _check_round_sampled(sim, n, seed, ids):
     return tot, alerts[0], conv_sampled
 
 
-def test_full_size_imp3d_pushsum_1e9_rounds():
-    """C5 at its real size (P = 1e9), on the kernel bench.py times, recomputed on the
-    host for ~1.1e6 receivers by or_pushsum_receivers from the read-back round-start
-    state -- bit-exact s, w and flags (Program.fs:101-131 via SRS v1 B.4) in four
-    rounds: during activation (round 40), in steady state before any alert (every
-    node active, 8 rounds later), at the alert peak (round 533: 1.5e7 of the 1e9
-    nodes converge in that round, the count / converge branch of Program.fs:114-123)
-    and in the tail (round 700: 99 % converged, converged nodes forwarding, D6).
-    Mass conserved to 1e-12 relative; each round's alert count equals the nodes it
-    converged; a second run is bit-identical (determinism)."""
+class _C5:
+    """The one P = 1e9 run the full-size tests below share (module fixture), so each
+    segment reports as it finishes."""
     n, seed = 10**9, 1
-    sim = Sim(n, "Imp3D", "push-sum", seed=seed)
-    P, g = sim.population, sim.info().grid
-    ids = _sample_ids(P, g, np.random.default_rng(7))
-    ref_s = P * (P - 1) / 2
 
-    def check():
-        (tot_s, tot_w), a, conv = _check_round_sampled(sim, n, seed, ids)
-        assert abs(tot_s - ref_s) <= 1e-12 * ref_s
-        assert abs(tot_w - P) <= 1e-12 * P
-        return a, conv
 
-    sim.step(40)
-    check()
-    h = hashlib.sha256(sim.state(0, 50_000_000)["s"].tobytes()).hexdigest()
-    while sim.info().active < P:
-        assert sim.rounds < 400, "activation did not complete"
-        sim.step(8)
-    sim.step(8)
-    assert sim.info().active == P
-    check()
-    sim.step(533 - sim.rounds)
-    a, conv = check()
+@pytest.fixture(scope="module")
+def c5():
+    st = _C5()
+    st.sim = Sim(st.n, "Imp3D", "push-sum", seed=st.seed)
+    st.P, g = st.sim.population, st.sim.info().grid
+    st.ids = _sample_ids(st.P, g, np.random.default_rng(7))
+    st.ref_s = st.P * (st.P - 1) / 2
+    st.hash41 = None
+    yield st
+    st.sim.close()
+
+
+def _c5_check(st):
+    (tot_s, tot_w), a, conv = _check_round_sampled(st.sim, st.n, st.seed, st.ids)
+    assert abs(tot_s - st.ref_s) <= 1e-12 * st.ref_s  # mass conserved
+    assert abs(tot_w - st.P) <= 1e-12 * st.P
+    return a, conv
+
+
+# C5 at its real size (P = 1e9), on the kernel bench.py times: rounds recomputed on
+# the host for ~1.1e6 receivers by or_pushsum_receivers from the read-back
+# round-start state -- bit-exact s, w and flags (Program.fs:101-131 via SRS v1
+# B.4) -- during activation (round 40), in steady state before any alert (every
+# node active, 8 rounds later), at the alert peak (round 533: 1.5e7 of the 1e9
+# nodes converge in that round, the count / converge branch of Program.fs:114-123)
+# and in the tail (round 700: 99 % converged, converged nodes forwarding, D6); mass
+# conserved to 1e-12 relative; each round's alert count equals the nodes it
+# converged; a second run is bit-identical (determinism).
+def test_full_size_1e9_activation_round(c5):
+    c5.sim.step(40)
+    _c5_check(c5)
+    c5.hash41 = hashlib.sha256(c5.sim.state(0, 50_000_000)["s"].tobytes()).hexdigest()
+
+
+def test_full_size_1e9_steady_round(c5):
+    assert c5.sim.rounds == 41
+    while c5.sim.info().active < c5.P:
+        assert c5.sim.rounds < 400, "activation did not complete"
+        c5.sim.step(8)
+    c5.sim.step(8)
+    assert c5.sim.info().active == c5.P
+    _c5_check(c5)
+
+
+def test_full_size_1e9_alert_peak_round(c5):
+    c5.sim.step(533 - c5.sim.rounds)
+    a, conv = _c5_check(c5)
     assert a > 10**7 and conv > 5000, (a, conv)  # the alert peak is exercised
-    sim.step(700 - sim.rounds)
-    a, conv = check()
-    assert a > 10**5 and sim.alerts_total > 0.98 * P, (a, sim.alerts_total)
-    sim.close()
-    sim2 = Sim(n, "Imp3D", "push-sum", seed=seed)
+
+
+def test_full_size_1e9_tail_round(c5):
+    c5.sim.step(700 - c5.sim.rounds)
+    a, conv = _c5_check(c5)
+    assert a > 10**5 and c5.sim.alerts_total > 0.98 * c5.P, (a, c5.sim.alerts_total)
+
+
+def test_full_size_1e9_determinism(c5):
+    assert c5.hash41 is not None
+    c5.sim.close()
+    sim2 = Sim(c5.n, "Imp3D", "push-sum", seed=c5.seed)
     sim2.step(41)
-    assert hashlib.sha256(sim2.state(0, 50_000_000)["s"].tobytes()).hexdigest() == h
+    assert hashlib.sha256(sim2.state(0, 50_000_000)["s"].tobytes()).hexdigest() == c5.hash41
     sim2.close()
 
 
@@ -342,9 +369,10 @@ def test_nibble_wide_tile_fallback_parity(wide_at, monkeypatch):
 @pytest.mark.parametrize("kernel", ["col", "tile"])
 def test_seed_random_edge_round0(kernel, monkeypatch):
     """Many seeds, so that several seed nodes send their round-0 rumour on the random
-    edge: the round-0 random-edge bitmap (k_col_rbits_init / k_rbits_init) must carry
-    that send.  Regression: k_col_rbits_init once raced its own zeroing loop against
-    the seed's bit (lost about one time in four)."""
+    edge: the column kernel's round-0 delivery count (k_col_seed_init) / the tile
+    kernel's round-0 random-edge bitmap (k_rbits_init) must carry that send.
+    Regression: the column layout's bitmap init once raced its own zeroing loop
+    against the seed's bit (lost about one time in four)."""
     monkeypatch.setenv("GP_KERNEL", kernel)
     for seed in range(1, 25):
         sim, orc = Sim(27000, "Imp3D", "gossip", seed=seed, experimental=True), Oracle(27000, "Imp3D", "gossip", seed)
@@ -373,6 +401,35 @@ def test_tile_unstaged_path_parity(cap, monkeypatch):
         done += k
     sim.close()
 
+
+INBOX_CASES = [  # (num_nodes, seed, rounds, checkpoint, staging cap)
+    (512000, 4, 90, 45, None),        # activation into steady state
+    (64000, 5, 3000, 500, None),      # through convergence
+    (343000, 6, 120, 60, "1000"),     # a mix of tiles on the unstaged path
+    (27000, 3, 60, 30, "0"),          # every tile unstaged
+]
+
+
+@pytest.mark.parametrize("n,seed,rounds,chk,cap", INBOX_CASES, ids=lambda v: str(v))
+def test_inbox_mode_parity(n, seed, rounds, chk, cap, monkeypatch):
+    """Imp3D push-sum with the in-edge pass as a kernel of its own (GP_INBOX=1,
+    experiments build: k_ps_gather writes each tile's used-in-edge bitmap and the
+    used messages compacted in edge order; k_ps_tile<INBOX> folds them by rank) --
+    bit-exact vs the oracle, with GP_STAGE_CAP forcing the flagged-tile path."""
+    monkeypatch.setenv("GP_INBOX", "1")
+    if cap is not None:
+        monkeypatch.setenv("GP_STAGE_CAP", cap)
+    sim, orc = Sim(n, "Imp3D", "push-sum", seed=seed, experimental=True), Oracle(n, "Imp3D", "push-sum", seed)
+    done = 0
+    while done < rounds and orc.alerts_total < orc.T:
+        k = min(chk, rounds - done)
+        ga, oa = sim.step(k), orc.step(k)
+        assert ga == oa, f"alerts differ in rounds {done}..{done + k}"
+        assert_same_state("push-sum", sim.state(), orc.state())
+        done += k
+    assert sim.rounds == orc.rounds
+    sim.close()
+    orc.close()
 
 
 CLOSE_CASES = [  # (num_nodes, topology, seed, rounds, checkpoint): push-sum, one rank
