@@ -42,6 +42,15 @@ extern int gp_parse_algorithm(string s)
 [<DllImport(Lib, CallingConvention = CallingConvention.Cdecl)>]
 extern int gp_create(GpConfig& cfg, nativeint& sim)
 
+/// Multi-GPU, one process per GPU: rank 0 publishes its RCCL id at `path`, the
+/// other ranks read it (include/gossip_hip.h gp_rendezvous_id); then every rank
+/// joins with gp_create_rank.
+[<DllImport(Lib, CallingConvention = CallingConvention.Cdecl)>]
+extern int gp_rendezvous_id(int rank, string path, int timeoutMs, byte[] uniqueId)
+
+[<DllImport(Lib, CallingConvention = CallingConvention.Cdecl)>]
+extern int gp_create_rank(GpConfig& cfg, int rank, int world, byte[] uniqueId, nativeint& sim)
+
 [<DllImport(Lib, CallingConvention = CallingConvention.Cdecl)>]
 extern int gp_run(nativeint sim, GpResult& result)
 
