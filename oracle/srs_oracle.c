@@ -647,7 +647,7 @@ int64_t or_pushsum_receivers(int topology, int64_t num_nodes, uint64_t seed, uin
     or_sim c;
     memset(&c, 0, sizeof c);
     int64_t P, T, g;
-    if (topology == OR_FULL || or_resolve(num_nodes, topology, &P, &T, &g)) return -1;
+    if (or_resolve(num_nodes, topology, &P, &T, &g)) return -1;
     c.topo = topology; c.alg = OR_PUSHSUM; c.threads = threads; c.seed = seed;
     c.P = P; c.T = T; c.g = g;
     const int nt = nthreads(&c);
@@ -662,16 +662,33 @@ int64_t or_pushsum_receivers(int topology, int64_t num_nodes, uint64_t seed, uin
         if (ids[q] < 0 || ids[q] >= P || pos[ids[q]] >= 0) { free(pos); free(roff); free(rcur); return -1; }
         pos[ids[q]] = (int32_t)q;
     }
-    if (topology == OR_IMP3D) {
+    if (topology == OR_FULL) {
+        /* full topology (Program.fs:209-216): every active sender's round-r target,
+         * t = U(P-1) mapped past i (as pushsum_round_full); senders of the sampled
+         * receivers grouped per receiver, then sorted below */
+        c.rnd = (uint32_t*)malloc(sizeof(uint32_t) * P);
+        if (!c.rnd) { free(pos); free(roff); free(rcur); return -1; }
+        #pragma omp parallel for num_threads(nt) schedule(static)
+        for (int64_t i = 0; i < P; ++i) {
+            uint32_t t = NONE_U32;
+            if ((flags[i] & 1) && P > 1) {
+                const uint32_t k = or_uniform(seed, OR_STREAM_PUSHSUM, (uint64_t)i, round, (uint32_t)(P - 1));
+                t = (int64_t)k < i ? k : (uint32_t)(k + 1);
+            }
+            c.rnd[i] = t;
+        }
+    } else if (topology == OR_IMP3D) {
         c.rnd = (uint32_t*)malloc(sizeof(uint32_t) * P);
         if (!c.rnd) { free(pos); free(roff); free(rcur); return -1; }
         #pragma omp parallel for num_threads(nt) schedule(static)
         for (int64_t i = 0; i < P; ++i)
             c.rnd[i] = or_uniform(seed, OR_STREAM_TOPO, (uint64_t)i, 0, (uint32_t)(P - 1));
+    }
+    if (topology == OR_IMP3D || topology == OR_FULL) {
         /* random in-senders of the sampled receivers, grouped per receiver */
         #pragma omp parallel for num_threads(nt) schedule(static)
         for (int64_t i = 0; i < P; ++i) {
-            int32_t q = pos[c.rnd[i]];
+            int32_t q = c.rnd[i] == NONE_U32 ? -1 : pos[c.rnd[i]];
             if (q >= 0) {
                 #pragma omp atomic
                 roff[q + 1] += 1;
@@ -683,7 +700,7 @@ int64_t or_pushsum_receivers(int topology, int64_t num_nodes, uint64_t seed, uin
         if (!rsrc) { free(c.rnd); free(pos); free(roff); free(rcur); return -1; }
         #pragma omp parallel for num_threads(nt) schedule(static)
         for (int64_t i = 0; i < P; ++i) {
-            int32_t q = pos[c.rnd[i]];
+            int32_t q = c.rnd[i] == NONE_U32 ? -1 : pos[c.rnd[i]];
             if (q >= 0) {
                 int64_t at;
                 #pragma omp atomic capture
@@ -702,9 +719,9 @@ int64_t or_pushsum_receivers(int topology, int64_t num_nodes, uint64_t seed, uin
         double acc_s = halve ? sv[j] * 0.5 : sv[j];
         double acc_w = halve ? wv[j] * 0.5 : wv[j];
         int recv = 0;
-        /* lattice senders in j's slot order */
+        /* lattice senders in j's slot order (none on the full topology) */
         int64_t nb[7];
-        const int d = topology == OR_LINE ? line_nbrs(P, j, nb) : lattice_nbrs(g, j, nb);
+        const int d = topology == OR_FULL ? 0 : topology == OR_LINE ? line_nbrs(P, j, nb) : lattice_nbrs(g, j, nb);
         for (int k = 0; k < d; ++k) {
             const int64_t n = nb[k];
             if (!(flags[n] & 1)) continue;
@@ -717,8 +734,8 @@ int64_t or_pushsum_receivers(int topology, int64_t num_nodes, uint64_t seed, uin
             acc_w = acc_w + wv[n] * 0.5;
             recv = 1;
         }
-        /* random in-senders by ascending id */
-        if (topology == OR_IMP3D) {
+        /* random in-senders (full: every sender) by ascending id */
+        if (topology == OR_IMP3D || topology == OR_FULL) {
             const int64_t b = roff[q], e = roff[q + 1];
             for (int64_t p = b + 1; p < e; ++p) { /* insertion sort: a handful per receiver */
                 uint32_t v = rsrc[p];
@@ -729,9 +746,11 @@ int64_t or_pushsum_receivers(int topology, int64_t num_nodes, uint64_t seed, uin
             for (int64_t p = b; p < e; ++p) {
                 const int64_t i = rsrc[p];
                 if (!(flags[i] & 1)) continue;
-                const int64_t di = degree(&c, i);
-                const uint32_t kk = or_uniform(seed, OR_STREAM_PUSHSUM, (uint64_t)i, round, (uint32_t)di);
-                if (kk != (uint32_t)(di - 1)) continue; /* the random slot is the last one */
+                if (topology == OR_IMP3D) {
+                    const int64_t di = degree(&c, i);
+                    const uint32_t kk = or_uniform(seed, OR_STREAM_PUSHSUM, (uint64_t)i, round, (uint32_t)di);
+                    if (kk != (uint32_t)(di - 1)) continue; /* the random slot is the last one */
+                } /* (full: rsrc holds exactly this round's senders to j) */
                 acc_s = acc_s + sv[i] * 0.5;
                 acc_w = acc_w + wv[i] * 0.5;
                 recv = 1;

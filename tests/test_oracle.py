@@ -151,25 +151,30 @@ def test_gossip_invariants(topo):
         prev = c
 
 
-@pytest.mark.parametrize("n,topo,seed", [(27000, "Imp3D", 3), (64000, "Imp3D", 11), (8000, "3D", 5), (3000, "line", 2)])
-def test_pushsum_receivers_matches_whole_network_round(n, topo, seed):
+@pytest.mark.parametrize("n,topo,seed,warms", [(27000, "Imp3D", 3, (3, 25, 150)), (64000, "Imp3D", 11, (3, 25, 150)),
+                                                (8000, "3D", 5, (3, 25, 150)), (3000, "line", 2, (3, 25, 150)),
+                                                (20000, "full", 4, (3, 20, 60, 108, 111, 116))])
+def test_pushsum_receivers_matches_whole_network_round(n, topo, seed, warms):
     """or_pushsum_receivers (one round for sampled receivers, pulled from a full
-    round-start state -- the checker of the P = 1e9 GPU round) equals the whole-
-    network oracle's round, bit for bit, during activation and in steady state."""
+    round-start state -- the checker of the P = 1e9 GPU round and of the full
+    topology's alert phase at P = 1e8) equals the whole-network oracle's round, bit
+    for bit, during activation, in steady state and (full) while nodes converge;
+    its return value counts the sampled receivers that converge in the round."""
     from tests.oracle_ctypes import pushsum_receivers
     orc = Oracle(n, topo, "push-sum", seed)
     P = orc.P
     rng = np.random.default_rng(seed)
-    for warm in (3, 25, 150):
+    for warm in warms:
         orc.step(warm - orc.rounds) if warm > orc.rounds else None
         st = orc.state()
         r = orc.rounds
         ids = np.unique(np.concatenate([rng.choice(P, size=min(P, 2000), replace=False),
                                         np.arange(min(P, 300)), np.arange(P - 300, P)]))
-        so, wo, fo, _ = pushsum_receivers(topo, n, seed, r, st["s"], st["w"], st["flags"], ids)
-        orc.step(1)
+        so, wo, fo, conv = pushsum_receivers(topo, n, seed, r, st["s"], st["w"], st["flags"], ids)
+        assert len(orc.step(1)) == 1
         nx = orc.state()
         np.testing.assert_array_equal(so, nx["s"][ids])
         np.testing.assert_array_equal(wo, nx["w"][ids])
         np.testing.assert_array_equal(fo, nx["flags"][ids])
+        assert conv == int(np.count_nonzero((nx["flags"][ids] & 2) & ~(st["flags"][ids] & 2)))
     orc.close()
