@@ -62,12 +62,15 @@ def test_cli_gossip_gpus_env():
 
 
 def test_cli_gpus_beyond_visible_fails_loudly():
-    """--gpus 2 without --device on a one-GPU box: rank 1 has no device 1, so the
-    launcher stops rank 0 and fails -- it never runs on fewer GPUs than asked."""
-    r = subprocess.run([EXE, "27000", "Imp3D", "push-sum", "--gpus", "2"], capture_output=True, text=True, timeout=300)
+    """--gpus (visible + 1) without --device: the last rank has no device, so the
+    launcher stops the others and fails -- it never runs on fewer GPUs than asked."""
+    import torch  # device_count() does not initialise the GPU on this image
+    n = max(1, torch.cuda.device_count())
+    r = subprocess.run([EXE, "27000", "Imp3D", "push-sum", "--gpus", str(n + 1)], capture_output=True, text=True,
+                       timeout=300)
     assert r.returncode != 0
     assert "Convergence Time" not in r.stdout
-    assert "rank 1" in r.stderr
+    assert f"rank {n}" in r.stderr
 
 
 def test_python_cli_gpus_matches_one_gpu():
