@@ -187,7 +187,7 @@ def _sample_ids(P, g, rng, n_random=1_000_000):
     return np.unique(np.concatenate(ids).astype(np.int64))
 
 
-def _check_round_sampled(sim, n, seed, ids):
+def _check_round_sampled(sim, n, seed, ids, topology="Imp3D"):
     """Round r of the GPU (r = sim.rounds) against or_pushsum_receivers for ids.
     Also: the round's alert count reported by the GPU equals the number of nodes
     whose converged flag the round set (whole state), and the sampled receivers
@@ -197,7 +197,7 @@ def _check_round_sampled(sim, n, seed, ids):
     r = sim.rounds
     s, w, f = _read_all(sim, P)
     tot = (float(np.sum(s)), float(np.sum(w)))
-    so, wo, fo, conv_sampled = pushsum_receivers("Imp3D", n, seed, r, s, w, f, ids)
+    so, wo, fo, conv_sampled = pushsum_receivers(topology, n, seed, r, s, w, f, ids)
     conv0 = int(np.count_nonzero(f & 2))
     was_conv = (f[ids] & 2) != 0
     del s, w, f
@@ -282,6 +282,32 @@ def test_full_size_1e9_determinism(c5):
     sim2.step(41)
     assert hashlib.sha256(sim2.state(0, 50_000_000)["s"].tobytes()).hexdigest() == c5.hash41
     sim2.close()
+
+
+def test_full_pushsum_1e8_alert_phase_sampled():
+    """C4 (full push-sum, P = 100,000,001) in its alert phase: the round in which the
+    cumulative alerts first pass 10 % of T and the one in which they pass 99 % are
+    recomputed on the host for ~1e6 sampled receivers (or_pushsum_receivers, full
+    topology: every active sender's Philox target, folded by ascending sender id,
+    Program.fs:209-216,101-131) -- bit-exact s, w, flags; the round's alert count
+    equals the nodes it converged; mass conserved.  (The whole-network comparison
+    through convergence is tests/test_gpu_baseline_sizes.py's C4 run.)"""
+    n, seed = 10**8, 1
+    sim = Sim(n, "full", "push-sum", seed=seed)
+    P, T = sim.population, sim.threshold
+    rng = np.random.default_rng(5)
+    ids = np.unique(np.concatenate([rng.choice(P, size=1_000_000, replace=False), np.arange(2000),
+                                    np.arange(P - 2000, P)]).astype(np.int64))
+    ref_s = P * (P - 1) / 2
+    checked = []
+    for frac in (0.10, 0.99):
+        while sim.alerts_total < frac * T:
+            assert sim.rounds < 2000 and len(sim.step(1)) == 1
+        (tot_s, tot_w), a, conv = _check_round_sampled(sim, n, seed, ids, topology="full")
+        assert abs(tot_s - ref_s) <= 1e-12 * ref_s and abs(tot_w - P) <= 1e-12 * P
+        checked.append((sim.rounds - 1, a, conv))
+    assert all(a > 0 for _, a, _ in checked), checked
+    sim.close()
 
 
 KERNEL_CASES = [  # (num_nodes, topology, algorithm, seed, rounds, checkpoint, x-segments)
