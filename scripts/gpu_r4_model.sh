@@ -12,3 +12,8 @@ for cfg in "1000000000 Imp3D push-sum 8" "100000000 Imp3D gossip 8"; do
 done
 timeout -k 10 600 python3 tools/xchg_traffic.py 1000000000 Imp3D push-sum 8 4 k_pack k_unpack k_ps_tile > $O/xt_c5_w8.txt 2>&1 || { tail -20 $O/xt_c5_w8.txt; exit 1; }
 cat $O/xt_c5_w8.txt | grep -v '^{'
+# rejected headline variant (in-edge pass as its own kernel): HBM bytes of both kernels
+timeout -k 10 600 python3 tools/traffic_probe.py 1000000000 Imp3D push-sum k_ps_gather "GP_INBOX=1,GP_EXP=1" > $O/inbox_gather_traffic.txt 2>&1 || { tail -5 $O/inbox_gather_traffic.txt; exit 1; }
+cat $O/inbox_gather_traffic.txt
+timeout -k 10 600 python3 tools/traffic_probe.py 1000000000 Imp3D push-sum "k_ps_tile<3, false, true>" "GP_INBOX=1,GP_EXP=1" > $O/inbox_tile_traffic.txt 2>&1 || { tail -5 $O/inbox_tile_traffic.txt; exit 1; }
+cat $O/inbox_tile_traffic.txt
