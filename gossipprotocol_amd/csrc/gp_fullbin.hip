@@ -131,12 +131,6 @@ constexpr int FBR_CHUNK = FBR_THREADS * FBR_PER;
 #define GP_FB_RANGE 4
 #endif
 constexpr uint32_t FBR_ITEM = (uint32_t)GP_FB_RANGE * FBR_CHUNK;  // messages per work item
-// B's work items dealt by coarse bin to XCDs (blocks b and b + 8 share an XCD): all
-// ranges of a coarse bin run on one XCD, so the partial 128-byte lines at the ends of
-// adjacent runs of a fine tile are written through one L2 (and can merge there)
-#ifndef GP_FB_XCDMAP
-#define GP_FB_XCDMAP 0
-#endif
 static_assert(GP_FB_RANGE % 2 == 0, "sweep 1 takes two chunks at a time");
 
 struct FbRangeLds {
@@ -321,13 +315,7 @@ __global__ __launch_bounds__(FBR_THREADS, GP_FBR_MINB) void k_fb_split(FullBinAr
     __shared__ FbRangeLds L;
     if (ld_agent(&a.ctl->done)) return;
     const uint32_t per_bin = (a.cap1 + FBR_ITEM - 1) / FBR_ITEM;
-#if GP_FB_XCDMAP
-    const uint32_t kx = blockIdx.x >> 3;
-    const uint32_t b = (blockIdx.x & 7u) + 8u * (kx / per_bin), c = kx % per_bin;
-    if (b >= a.nb1) return;
-#else
     const uint32_t b = blockIdx.x / per_bin, c = blockIdx.x % per_bin;
-#endif
     const uint32_t n_bin = min(ld_agent(&a.cnt1[b]), a.cap1);
     const uint32_t q0 = c * FBR_ITEM;
     if (q0 >= n_bin) return;
@@ -752,11 +740,8 @@ hipError_t launch_full_bin_coarse(const FullBinArgs& a, uint32_t round, hipStrea
     return hipGetLastError();
 }
 
-// B's grid (GP_FB_XCDMAP: whole coarse bins per XCD, 8-aligned)
-static uint32_t split_items(const FullBinArgs& a) {
-    const uint32_t per_bin = (a.cap1 + FBR_ITEM - 1) / FBR_ITEM;
-    return (GP_FB_XCDMAP ? (a.nb1 + 7u) / 8u * 8u : a.nb1) * per_bin;
-}
+// B's grid: every coarse bin's ranges
+static uint32_t split_items(const FullBinArgs& a) { return a.nb1 * ((a.cap1 + FBR_ITEM - 1) / FBR_ITEM); }
 
 hipError_t launch_full_bin_split_fold(const FullBinArgs& a, uint32_t round, int grid, hipStream_t st) {
     const uint32_t items_b = split_items(a);
