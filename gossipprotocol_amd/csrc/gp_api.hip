@@ -144,9 +144,6 @@ struct gp_sim {
     int xhalves = 1;
     hipStream_t xstream = nullptr;
     hipEvent_t ev_send[2] = {nullptr, nullptr}, ev_xfer[2] = {nullptr, nullptr};
-    // Imp3D push-sum on one rank: the in-edge pass as a kernel of its own (k_ps_gather)
-    // writing per-tile inboxes
-    bool inbox = false;
 };
 
 namespace {
@@ -948,14 +945,9 @@ void choose_kernel(gp_sim* s, int64_t nloc_max, int& kernel, uint32_t& col_xsegs
     if (const char* e = std::getenv("GP_WALK")) walk = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("GP_WX")) wx = (uint32_t)std::max(1, std::atoi(e));
 #endif
-    s->inbox = false;
-#ifdef GP_EXPERIMENTS
-    if (const char* e = std::getenv("GP_INBOX"))
-        s->inbox = e[0] == '1' && kernel == KERNEL_TILE && cfg->topology == GP_IMP3D && push && s->world == 1;
-#endif
     if (walk == 3) {
         const int topo = cfg->topology == GP_LINE ? LINE : cfg->topology == GP_3D ? GRID3D : IMP3D;
-        const int64_t res = ps_tile_resident_blocks(topo, s->world > 1 && topo == IMP3D, s->inbox, s->device) / 8 * 8;
+        const int64_t res = ps_tile_resident_blocks(topo, s->world > 1 && topo == IMP3D, s->device) / 8 * 8;
         if (res >= 8) s->grid = (int)std::min<int64_t>(s->grid, res);
         else walk = 2;
     }
@@ -1006,12 +998,6 @@ int build_sim(gp_sim* s) {
         }
     }
     if (s->cfg.topology == GP_IMP3D && (rc = build_imp3d(s))) return rc;
-    if (s->inbox) {  // per tile: header (bitmap, word prefixes, count, flag) + compacted messages
-        DevState& S = s->slab[0].S;
-        const size_t nt = tiles_of_slab(S.lo, S.nloc);
-        if ((rc = dev_alloc_t(s, &S.ib_hdr, nt * IB_HW)) || (rc = dev_alloc_t(s, &S.ib_msg, nt * IB_CAP))) return rc;
-        HIP_TRY(hipMemsetAsync(S.ib_hdr, 0, sizeof(uint32_t) * nt * IB_HW, s->stream));
-    }
     if ((s->cfg.topology == GP_IMP3D || s->cfg.topology == GP_FULL) && s->world > 1 && (rc = setup_exchange(s)))
         return rc;
     if (hipHostMalloc((void**)&s->host_ctl, sizeof(Ctl), hipHostMallocDefault) != hipSuccess) {

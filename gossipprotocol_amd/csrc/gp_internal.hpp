@@ -183,15 +183,8 @@ struct DevState {
     // items at [woff[c], woff[c + 1])
     uint32_t* wtiles;
     uint32_t woff[9];
-    // Imp3D push-sum, one rank, inbox mode (k_ps_gather + k_ps_tile<INBOX>): per tile
-    // the used-in-edge bitmap + word prefixes (IB_HW words) and the used in-edges'
-    // messages in edge order, compacted (IB_CAP each)
-    uint32_t* ib_hdr;
-    double2* ib_msg;
 };
 constexpr int TQ_STRIDE = 64;
-constexpr int IB_HW = 64;     // inbox header words per tile: bits [0, 40), word prefixes [40, 60), total 60, flag 61
-constexpr int IB_CAP = 192;   // inbox messages per tile (mean ~146 at TILE = 1024, sigma ~11)
 
 // Arguments of the tiled round kernels (gp_round.hip): only what they read.
 struct RoundArgs {
@@ -221,8 +214,6 @@ struct RoundArgs {
     uint32_t wo[9];
     uint32_t* tq;        // walk 3: this round's 8 per-XCD tile-item counters (TQ_STRIDE apart)
     uint32_t* tq_next;   // walk 3: the next round's counters, zeroed by block 0 this round
-    uint32_t* ib_hdr;    // inbox mode (DevState::ib_hdr / ib_msg), by tile relative to lo / TILE
-    double2* ib_msg;
 };
 
 enum KernelVariant : int { KERNEL_TILE = 1, KERNEL_COL = 2 };
@@ -263,8 +254,7 @@ hipError_t launch_col_seed_init(const DevState& S, hipStream_t st);
 // ---- tiled round kernels (gp_round.hip)
 uint32_t rbits_words_for(uint32_t lo, uint32_t nloc);
 hipError_t launch_round_tile(const DevState& S, uint32_t round, int grid, hipStream_t st);
-int ps_tile_resident_blocks(int topo, bool remote, bool inbox, int device);
-uint32_t tiles_of_slab(uint32_t lo, uint32_t nloc);
+int ps_tile_resident_blocks(int topo, bool remote, int device);
 bool build_walk_list(const DevState& S, std::vector<uint32_t>& list, uint32_t woff[9]);
 hipError_t launch_rbits_init(const DevState& S, int grid, hipStream_t st);
 uint32_t ind4_bytes_for(uint32_t lo, uint32_t nloc);

@@ -110,25 +110,6 @@ struct TileLdsP {
     double2 zb[TPB / 64][NPT][2];     // GP_ZDPP: (s, w) across each wave's ends, slot k: [0] node - 1, [1] node + 64
 };
 
-// Inbox mode (k_ps_gather + k_ps_tile<..., INBOX>): the in-edge pass runs in a
-// kernel of its own, which writes per tile the used-in-edge bitmap and the used
-// edges' messages, compacted in edge order; the round kernel stages the header
-// and the messages by LDS-DMA.  A tile with more than IB_CAP used edges (mean
-// ~146, sigma ~11: ~3e-5 of tiles) is flagged and takes the unstaged path.
-constexpr int IB_DMA = IB_CAP;
-struct TileLdsI {
-    uint32_t rows[W_ROWS + DMA_SLACK];
-    uint32_t xm[W_PLANE + DMA_SLACK];
-    uint32_t xp[W_PLANE + DMA_SLACK];
-    uint32_t ind[TILE / 8 + DMA_SLACK];
-    uint32_t ibh[IB_HW + DMA_SLACK];  // the tile's inbox header (bits, word prefixes, total, flag)
-    double2 msg[IB_DMA];              // the tile's first IB_DMA used messages, in edge order
-    uint32_t out[TILE / 4];
-    uint32_t red[2][TPB / 64];
-    uint32_t qn[2];
-    double2 zb[TPB / 64][NPT][2];
-};
-
 // set bits of m below this lane
 __device__ __forceinline__ uint32_t mbcnt64(unsigned long long m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -359,10 +340,9 @@ __device__ __forceinline__ void st_stream(uint32_t* p, uint32_t v) {
 //      test (Program.fs:114-123);
 //   4. next-round directions of the thread's NPT nodes as one Philox batch;
 //      node bytes out as words, random-edge bits as one ballot per wave.
-template <int TOPO, bool REMOTE, bool INBOX, class Lds>
-__device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, Lds& L, bool all_active, uint32_t& alerts,
+template <int TOPO, bool REMOTE>
+__device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLdsP& L, bool all_active, uint32_t& alerts,
                                          uint32_t& newly, bool& tiny) {
-    static_assert(!INBOX || (TOPO == IMP3D && !REMOTE), "inbox mode: Imp3D, one rank");
     const double2* __restrict__ swc = a.swc;
     double2* __restrict__ swn = a.swn;
     const uint64_t* __restrict__ rbc = a.rbc;
@@ -442,11 +422,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, Lds& L,
                 pf_tile = nti;
             }
         }
-        if constexpr (INBOX) {
-            // the tile's inbox (k_ps_gather): header and the first IB_DMA messages
-            dma_copy<DMA_ONCE>(L.ibh, reinterpret_cast<const char*>(a.ib_hdr + (size_t)ti * IB_HW), IB_HW * 4);
-            dma_copy<DMA_ONCE>(L.msg, reinterpret_cast<const char*>(a.ib_msg + (size_t)ti * IB_CAP), IB_DMA * 16);
-        } else if constexpr (TOPO == IMP3D) {
+        if constexpr (TOPO == IMP3D) {
             if (staged) {
                 // in-edge q = m * TPB + wave * 64 + lane is bit `lane` of bitmap word
                 // m * 4 + wave; its message (if used) lands in slot q
@@ -575,10 +551,6 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, Lds& L,
         if (dyn && threadIdx.x == 0) L.qn[it & 1] = claim;
         __syncthreads();  // staging copies, in-edge bitmap and gathered messages retired
         GP_STAMP(t3);
-        // inbox mode: the gather kernel marks tiles it did not stage (in-degree above
-        // the staging capacity, or more used edges than the inbox holds)
-        bool use_bits = staged;
-        if constexpr (INBOX) use_bits = staged && L.ibh[61] == 0u;
         // Imp3D: node jl's in-edges are [e_lo + pre(jl), + d(jl)), pre = exclusive
         // prefix of the nibble in-degrees.  Every wave sums all 16 64-node chunks
         // (lane L: nodes 16L..16L+15) and keeps the prefixes of its own chunks
@@ -797,36 +769,20 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, Lds& L,
                                 e_b = a.in_off[j];
                                 e_e = a.in_off[j + 1];
                             }
-                            if (use_bits) {
+                            if (staged) {
                                 // the node's used in-edges: its window of the tile bitmap, 32 bits
                                 // at a time (funnel shift of two LDS words), walked set bit by set
                                 // bit (ascending sender = canonical order); edge q's message is at
-                                // slot q (inbox mode: at its rank among the tile's used edges)
-                                const uint32_t* bw;
-                                if constexpr (INBOX) bw = L.ibh;
-                                else bw = reinterpret_cast<const uint32_t*>(L.bits);
+                                // slot q
+                                const uint32_t* bw = reinterpret_cast<const uint32_t*>(L.bits);
                                 const uint32_t qe = e_e - e_lo;
-                                uint32_t rk = 0;
-                                if constexpr (INBOX) {
-                                    const uint32_t qb = e_b - e_lo, wq = qb >> 6;
-                                    if (qb < qe) {
-                                        const unsigned long long wd =
-                                            ((unsigned long long)bw[2 * wq + 1] << 32) | bw[2 * wq];
-                                        rk = L.ibh[40 + wq] + (uint32_t)__popcll(wd & ((1ull << (qb & 63u)) - 1ull));
-                                    }
-                                }
                                 for (uint32_t q0 = e_b - e_lo; q0 < qe; q0 += 32u) {
                                     uint32_t win = __builtin_amdgcn_alignbit(bw[(q0 >> 5) + 1], bw[q0 >> 5], q0 & 31u);
                                     if (qe - q0 < 32u) win &= (1u << (qe - q0)) - 1u;
                                     while (win) {
                                         const uint32_t q = q0 + (uint32_t)__builtin_ctz(win);
                                         win &= win - 1u;
-                                        if constexpr (INBOX) {
-                                            fold(L.msg[rk]);  // (rk < IB_CAP: more used edges flag the tile)
-                                            ++rk;
-                                        } else {
-                                            fold(L.msg[q]);
-                                        }
+                                        fold(L.msg[q]);
                                         recv = true;
                                     }
                                 }
@@ -972,18 +928,15 @@ __device__ __forceinline__ void add_round_counts(Ctl* ctl, uint32_t x, uint32_t 
     __builtin_amdgcn_s_waitcnt(0);
 }
 
-#ifndef GP_IMINB
-#define GP_IMINB 5  // inbox-mode round kernel: minimum waves per SIMD
-#endif
-template <int TOPO, bool REMOTE, bool INBOX = false>
-__global__ __launch_bounds__(TPB, INBOX ? GP_IMINB : GP_MINB) void k_ps_tile(RoundArgs a, uint32_t r) {
-    __shared__ typename std::conditional<INBOX, TileLdsI, TileLdsP>::type L;
+template <int TOPO, bool REMOTE>
+__global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t r) {
+    __shared__ TileLdsP L;
     Ctl* ctl = a.ctl;
     if (ld_agent(&ctl->done)) return;
     const bool all_active = ld_agent(&ctl->all_active) != 0;
     uint32_t alerts = 0, newly = 0;
     bool tiny = false;
-    ps_tiles<TOPO, REMOTE, INBOX>(a, r, L, all_active, alerts, newly, tiny);
+    ps_tiles<TOPO, REMOTE>(a, r, L, all_active, alerts, newly, tiny);
     if (__ballot(tiny) && (threadIdx.x & 63u) == 0) atomicOr(&ctl->tiny, 1u);
     block_counts(L.red, alerts, newly);
     if (threadIdx.x == 0) {
@@ -996,116 +949,6 @@ __global__ __launch_bounds__(TPB, INBOX ? GP_IMINB : GP_MINB) void k_ps_tile(Rou
             if (alerts) atomicAdd(&ctl->round_alerts, (unsigned long long)alerts);
             if (newly) atomicAdd(&ctl->round_active, (unsigned long long)newly);
         }
-    }
-}
-
-// Inbox mode, before k_ps_tile<IMP3D, false, true>: the in-edge pass of every
-// tile as a kernel of its own (few registers, little LDS, so many waves keep
-// the random message gathers in flight).  Per tile: did each in-edge's sender use
-// its random edge this round (every node active: the sender's Philox draw;
-// activation: the draw, then the ballot bitmap) -> bitmap in edge order, the
-// prefix of its 64-bit words, and the used edges' (s, w) gathered and written
-// compacted in edge order (the round kernel folds them by rank).
-#ifndef GP_GMINB
-#define GP_GMINB 8
-#endif
-__global__ __launch_bounds__(TPB, GP_GMINB) void k_ps_gather(RoundArgs a, uint32_t r) {
-    constexpr int FU = SLOT_FU;
-    constexpr int NW = FU * (TPB / 64);  // bitmap words per tile
-    static_assert(2 * NW <= 40 && 40 + NW <= 60, "inbox header layout");
-    __shared__ uint32_t wcnt[NW];
-    Ctl* ctl = a.ctl;
-    if (ld_agent(&ctl->done)) return;
-    const bool all_active = ld_agent(&ctl->all_active) != 0;
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    const uint32_t cap = min((uint32_t)SLOTS, a.stage_cap);
-    const bool packed = a.in_srcd != nullptr;
-    const uint32_t* __restrict__ srcp = packed ? a.in_srcd : a.in_src;
-    const double2* __restrict__ swc = a.swc;
-    const Geom G = a.G;
-    for (uint32_t ti = blockIdx.x; ti < a.ntiles; ti += gridDim.x) {
-        const uint32_t T = (a.lo / TILE + ti) * TILE;
-        const uint32_t j0 = max(a.lo, T), j1 = min(a.lo + a.nloc, T + TILE);
-        const uint32_t e_lo = a.in_off[j0], e_hi = a.in_off[j1];
-        const uint32_t cnt = e_hi - e_lo;
-        uint32_t* hdr = a.ib_hdr + (size_t)ti * IB_HW;
-        if (cnt > cap) {  // block-uniform: the round kernel takes its unstaged path
-            if (threadIdx.x == 0) hdr[61] = 1u;
-            continue;
-        }
-        uint32_t raw[FU], isrc[FU];
-        bool sent[FU];
-#pragma unroll
-        for (int m = 0; m < FU; ++m) {
-            const uint32_t q = threadIdx.x + m * TPB;
-            raw[m] = q < cnt ? __builtin_nontemporal_load(srcp + e_lo + q) : 0u;
-            isrc[m] = packed ? raw[m] & 0x3FFFFFFFu : raw[m];
-        }
-        {
-            uint32_t x[FU], y[FU];
-            philox2_batch<FU>(isrc, r, S_PUSHSUM, a.k0, a.k1, x, y);
-            bool pick[FU];
-#pragma unroll
-            for (int m = 0; m < FU; ++m) {
-                const uint32_t q = threadIdx.x + m * TPB;
-                const uint32_t di = packed ? (raw[m] >> 30) + 4u : popc6(present_mask<IMP3D>(isrc[m], G)) + 1u;
-                pick[m] = q < cnt && uniform_from(x[m], y[m], di) == di - 1u;
-            }
-            if (all_active) {
-#pragma unroll
-                for (int m = 0; m < FU; ++m) sent[m] = pick[m];
-            } else {  // activation: the pick's bitmap bit (active and the draw), loads batched
-                unsigned long long wbits[FU];
-#pragma unroll
-                for (int m = 0; m < FU; ++m) wbits[m] = a.rbc[pick[m] ? (isrc[m] >> 6) - (a.lo >> 6) : 0u];
-#pragma unroll
-                for (int m = 0; m < FU; ++m) asm volatile("" : "+v"(wbits[m])::"memory");
-#pragma unroll
-                for (int m = 0; m < FU; ++m) sent[m] = pick[m] && ((wbits[m] >> (isrc[m] & 63)) & 1ull);
-            }
-        }
-        // the used edges' messages: unconditional loads (a non-sender reads the tile's
-        // first node, one shared line), all in flight
-        double2 v[FU];
-#pragma unroll
-        for (int m = 0; m < FU; ++m) v[m] = swc[sent[m] ? isrc[m] : j0];
-        unsigned long long bal[FU];
-#pragma unroll
-        for (int m = 0; m < FU; ++m) {
-            bal[m] = __ballot(sent[m]);
-            if (lane == 0) {
-                wcnt[m * (TPB / 64) + wv] = (uint32_t)__popcll(bal[m]);
-                reinterpret_cast<unsigned long long*>(hdr)[m * (TPB / 64) + wv] = bal[m];
-            }
-        }
-        __syncthreads();
-        uint32_t pre[FU];
-#pragma unroll
-        for (int m = 0; m < FU; ++m) pre[m] = 0u;
-        uint32_t total = 0;
-        for (int w = 0; w < NW; ++w) {
-            const uint32_t c = wcnt[w];
-#pragma unroll
-            for (int m = 0; m < FU; ++m) pre[m] += w < m * (TPB / 64) + (int)wv ? c : 0u;
-            if (threadIdx.x == (uint32_t)w) hdr[40 + w] = total;
-            total += c;
-        }
-#pragma unroll
-        for (int m = 0; m < FU; ++m) asm volatile("" : "+v"(v[m].x), "+v"(v[m].y));
-#pragma unroll
-        for (int m = 0; m < FU; ++m) {
-            const uint32_t pos = pre[m] + mbcnt64(bal[m]);
-            if (sent[m] && pos < (uint32_t)IB_CAP) {
-                double2* d = a.ib_msg + (size_t)ti * IB_CAP + pos;
-                __builtin_nontemporal_store(v[m].x, &d->x);
-                __builtin_nontemporal_store(v[m].y, &d->y);
-            }
-        }
-        if (threadIdx.x == 0) {
-            hdr[60] = total;
-            hdr[61] = total > (uint32_t)IB_CAP ? 1u : 0u;
-        }
-        __syncthreads();  // wcnt is rewritten by the next tile
     }
 }
 
@@ -1286,7 +1129,6 @@ __global__ __launch_bounds__(TPB) void k_rbits_init(const uint8_t* nb, uint64_t*
 static uint32_t tiles_for(uint32_t lo, uint32_t nloc) {
     return (uint32_t)(((uint64_t)lo + nloc + TILE - 1) / TILE - lo / TILE);
 }
-uint32_t tiles_of_slab(uint32_t lo, uint32_t nloc) { return tiles_for(lo, nloc); }
 // 64-bit words the ballot stores of one round touch (whole tiles) plus slack.
 uint32_t rbits_words_for(uint32_t lo, uint32_t nloc) { return tiles_for(lo, nloc) * (TILE / 64) + 16u; }
 
@@ -1325,8 +1167,6 @@ RoundArgs make_round_args(const DevState& S, uint32_t round) {
     for (int c = 0; c <= 8; ++c) a.wo[c] = S.woff[c];
     a.tq = S.tq + (round & 1) * 8 * TQ_STRIDE;
     a.tq_next = S.tq + ((round + 1) & 1) * 8 * TQ_STRIDE;
-    a.ib_hdr = S.ib_hdr;
-    a.ib_msg = S.ib_msg;
     return a;
 }
 
@@ -1365,11 +1205,10 @@ bool build_walk_list(const DevState& S, std::vector<uint32_t>& list, uint32_t wo
 
 // Resident 256-thread blocks of the push-sum tile kernel on this device (walk 3
 // runs exactly that grid); 0 if unknown.
-int ps_tile_resident_blocks(int topo, bool remote, bool inbox, int device) {
+int ps_tile_resident_blocks(int topo, bool remote, int device) {
     const void* f = topo == LINE     ? reinterpret_cast<const void*>(&k_ps_tile<LINE, false>)
                     : topo == GRID3D ? reinterpret_cast<const void*>(&k_ps_tile<GRID3D, false>)
                     : remote         ? reinterpret_cast<const void*>(&k_ps_tile<IMP3D, true>)
-                    : inbox          ? reinterpret_cast<const void*>(&k_ps_tile<IMP3D, false, true>)
                                      : reinterpret_cast<const void*>(&k_ps_tile<IMP3D, false>);
     int per_cu = 0, cus = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, TPB, 0) != hipSuccess) return 0;
@@ -1387,21 +1226,8 @@ hipError_t launch_round_tile(const DevState& S, uint32_t round, int grid, hipStr
             case LINE: hipLaunchKernelGGL((k_ps_tile<LINE, false>), g, b, 0, st, a, round); break;
             case GRID3D: hipLaunchKernelGGL((k_ps_tile<GRID3D, false>), g, b, 0, st, a, round); break;
             default:
-                if (remote) {
-                    hipLaunchKernelGGL((k_ps_tile<IMP3D, true>), g, b, 0, st, a, round);
-                } else if (S.ib_hdr) {  // inbox mode: the in-edge pass as its own kernel first
-                    int per_cu = 0, cus = 0;
-                    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_ps_gather),
-                                                                       TPB, 0);
-                    int dev = 0;
-                    (void)hipGetDevice(&dev);
-                    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-                    const uint32_t gg = std::max(8u, (uint32_t)std::max(1, per_cu * cus));
-                    hipLaunchKernelGGL(k_ps_gather, dim3(std::min(gg, a.ntiles)), b, 0, st, a, round);
-                    hipLaunchKernelGGL((k_ps_tile<IMP3D, false, true>), g, b, 0, st, a, round);
-                } else {
-                    hipLaunchKernelGGL((k_ps_tile<IMP3D, false>), g, b, 0, st, a, round);
-                }
+                if (remote) hipLaunchKernelGGL((k_ps_tile<IMP3D, true>), g, b, 0, st, a, round);
+                else hipLaunchKernelGGL((k_ps_tile<IMP3D, false>), g, b, 0, st, a, round);
                 break;
         }
     } else {

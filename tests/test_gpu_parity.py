@@ -428,36 +428,6 @@ def test_tile_unstaged_path_parity(cap, monkeypatch):
     sim.close()
 
 
-INBOX_CASES = [  # (num_nodes, seed, rounds, checkpoint, staging cap)
-    (512000, 4, 90, 45, None),        # activation into steady state
-    (64000, 5, 3000, 500, None),      # through convergence
-    (343000, 6, 120, 60, "1000"),     # a mix of tiles on the unstaged path
-    (27000, 3, 60, 30, "0"),          # every tile unstaged
-]
-
-
-@pytest.mark.parametrize("n,seed,rounds,chk,cap", INBOX_CASES, ids=lambda v: str(v))
-def test_inbox_mode_parity(n, seed, rounds, chk, cap, monkeypatch):
-    """Imp3D push-sum with the in-edge pass as a kernel of its own (GP_INBOX=1,
-    experiments build: k_ps_gather writes each tile's used-in-edge bitmap and the
-    used messages compacted in edge order; k_ps_tile<INBOX> folds them by rank) --
-    bit-exact vs the oracle, with GP_STAGE_CAP forcing the flagged-tile path."""
-    monkeypatch.setenv("GP_INBOX", "1")
-    if cap is not None:
-        monkeypatch.setenv("GP_STAGE_CAP", cap)
-    sim, orc = Sim(n, "Imp3D", "push-sum", seed=seed, experimental=True), Oracle(n, "Imp3D", "push-sum", seed)
-    done = 0
-    while done < rounds and orc.alerts_total < orc.T:
-        k = min(chk, rounds - done)
-        ga, oa = sim.step(k), orc.step(k)
-        assert ga == oa, f"alerts differ in rounds {done}..{done + k}"
-        assert_same_state("push-sum", sim.state(), orc.state())
-        done += k
-    assert sim.rounds == orc.rounds
-    sim.close()
-    orc.close()
-
-
 CLOSE_CASES = [  # (num_nodes, topology, seed, rounds, checkpoint): push-sum, one rank
     (2000000, "3D", 3, 120, 60),      # ~2000 blocks: uneven shard sizes (blockIdx % 8)
     (343000, "Imp3D", 6, 300, 100),
