@@ -324,6 +324,10 @@ int alloc_slab(gp_sim* s, Slab& sl, int r) {
             return rc;
     }
     if (col_gossip_counts(S)) {  // senders count their random-edge deliveries at the target (k_gossip_col)
+        S.rq8 = 0;
+#ifdef GP_EXPERIMENTS
+        if (const char* e = std::getenv("GP_RQ8")) S.rq8 = e[0] == '1' ? 1u : 0u;
+#endif
         for (int q = 0; q < 2; ++q) {
             if ((rc = dev_alloc_t(s, &S.rq[q], (size_t)S.nloc + 64))) return rc;
             HIP_TRY(hipMemsetAsync(S.rq[q], 0, sizeof(uint32_t) * ((size_t)S.nloc + 64), s->stream));
@@ -819,6 +823,7 @@ int exchange(gp_sim* s, uint32_t rn) {
             ua.rtag = sl.S.rtag;
             ua.rmsg = sl.S.rmsg;
             ua.rq = col_gossip_counts(sl.S) ? sl.S.rq[rn & 1] : nullptr;  // next round's deliveries
+            ua.rq8 = sl.S.rq8;
             ua.nedges = ua.rq ? sl.S.nloc : sl.nedges;
             ua.W = W;
             ua.me = sl.rank;

@@ -132,7 +132,8 @@ __global__ __launch_bounds__(BULK_THREADS, GP_COL_MINW(TOPO)) void k_gossip_col(
                 led[k] = nbc[(rv[k] && ledge) ? (lane == 0 ? jl - 1 : jl + 1) : jl];
                 lrc[k] = lrd[k] = 0u;
                 if (TOPO == IMP3D) {
-                    lrc[k] = a.rq_cur[px + yo[k] - lo];
+                    lrc[k] = a.rq8 ? (uint32_t)reinterpret_cast<const uint8_t*>(a.rq_cur)[px + yo[k] - lo]
+                                   : a.rq_cur[px + yo[k] - lo];
                     lrd[k] = a.rnd[px + yo[k] - lo];
                 }
             }
@@ -190,8 +191,11 @@ __global__ __launch_bounds__(BULK_THREADS, GP_COL_MINW(TOPO)) void k_gossip_col(
                     // counted at its target now (the receiver drops it at round start if
                     // converged, Program.fs:87); a target on another rank gets it through
                     // the exchange (k_pack reads this direction byte)
-                    if (lrc[k]) a.rq_cur[j - lo] = 0u;
-                    if (dir == DIR_RANDOM && lrd[k] - lo < a.nloc) atomicAdd(&a.rq_next[lrd[k] - lo], 1u);
+                    if (lrc[k]) {
+                        if (a.rq8) reinterpret_cast<uint8_t*>(a.rq_cur)[j - lo] = 0u;
+                        else a.rq_cur[j - lo] = 0u;
+                    }
+                    if (dir == DIR_RANDOM && lrd[k] - lo < a.nloc) rq_add(a.rq_next, a.rq8, lrd[k] - lo);
                 }
             }
             pb = cb;
@@ -209,7 +213,7 @@ __global__ void k_col_seed_init(WaveArgs a, const uint8_t* nb0) {
     const uint32_t i = a.seed_node;
     if (i - a.lo >= a.nloc || (nb0[i - a.base] & DIR_MASK) != DIR_RANDOM) return;
     const uint32_t t = a.rnd[i - a.lo] - a.lo;
-    if (t < a.nloc) atomicAdd(&a.rq_cur[t], 1u);
+    if (t < a.nloc) rq_add(a.rq_cur, a.rq8, t);
 }
 
 int col_blocks_per_cu(int topo, int alg) {
@@ -258,6 +262,7 @@ WaveArgs make_wave_args(const DevState& S, uint32_t round) {
     a.c = S.c;
     a.rq_cur = S.rq[round & 1];
     a.rq_next = S.rq[(round + 1) & 1];
+    a.rq8 = S.rq8;
     a.rnd = S.rnd;
     a.ctl = S.ctl;
     a.G = S.G;

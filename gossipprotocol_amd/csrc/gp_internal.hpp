@@ -119,6 +119,15 @@ __device__ inline void block_done_close_sharded(Ctl* ctl, uint32_t P, uint32_t T
     close_round_ctl(ctl, P, T, round, ga, gna);
 }
 
+// One more random-edge rumour for local node t next round (gossip column kernel):
+// rq holds a word per node, or (rq8) a byte per node packed four to a word -- a
+// node's count in one round is at most its random in-degree (Poisson(1): never
+// near 256).
+__device__ inline void rq_add(uint32_t* rq, uint32_t rq8, uint32_t t) {
+    if (rq8) atomicAdd(&rq[t >> 2], 1u << (8u * (t & 3u)));
+    else atomicAdd(&rq[t], 1u);
+}
+
 // Node state in HBM (structure of arrays, single GPU / one slab).
 struct DevState {
     Geom G;
@@ -136,6 +145,7 @@ struct DevState {
     // from local senders in k_gossip_col, the exchange's counts from remote ones in
     // k_unpack) and read (then zeroed) by the receiver
     uint32_t* rq[2];
+    uint32_t rq8;         // rq holds one byte per node (four per word) instead of one word
     // Imp3D: bit i of rbits[b] = node i sends on its random edge in the round
     // of buffer b (ballot-packed by the round kernel)
     uint64_t* rbits[2];
@@ -233,6 +243,7 @@ struct WaveArgs {
     int32_t* c;
     uint32_t* rq_cur;        // Imp3D gossip: this round's random-edge deliveries per local node (read, then zeroed)
     uint32_t* rq_next;       // next round's, counted by local senders with atomics (remote ones: k_unpack)
+    uint32_t rq8;            // byte counters (DevState::rq8)
     const uint32_t* rnd;     // random edge of each local sender (id - lo)
     Ctl* ctl;
     Geom G;

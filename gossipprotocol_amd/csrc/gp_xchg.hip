@@ -137,7 +137,7 @@ __global__ __launch_bounds__(256) void k_unpack(UnpackArgs a, uint32_t round) {
         const uint32_t e = slot[u];
         if (e >= a.nedges) continue;  // never: slots are in-edge positions (or nodes) of this rank
         if (a.rq) {  // gossip column kernel: a rumour for local node `e` next round (integer count)
-            atomicAdd(&a.rq[e], 1u);
+            rq_add(a.rq, a.rq8, e);
             continue;
         }
         if (tags) a.rtag[e] = round;

@@ -35,6 +35,7 @@ struct UnpackArgs {
     uint32_t* rtag;
     double2* rmsg;
     uint32_t* rq;         // counts mode (gossip column kernel): next round's deliveries per local node
+    uint32_t rq8;         // (byte counters, DevState::rq8)
     uint32_t nedges;      // entries must be below this bound (in-edges; counts mode: local nodes)
     int W, me, push;
     XPeer peer[XMAXW];    // receive side

@@ -120,3 +120,22 @@ def test_virtual_ranks_max_world(topo, alg):
             break
     sim.close()
     orc.close()
+
+
+@pytest.mark.parametrize("ranks", [1, 3])
+def test_col_gossip_byte_counters(ranks, monkeypatch):
+    """Imp3D gossip on the column kernel with the random-edge delivery counts held
+    as bytes, four per word (GP_RQ8=1, experiments build): local senders' atomics,
+    the exchange's counts and the seed's round-0 send all add into byte lanes --
+    bit-exact vs the oracle on one and on three ranks."""
+    monkeypatch.setenv("GP_KERNEL", "col")
+    monkeypatch.setenv("GP_RQ8", "1")
+    n, seed = 125000, 12
+    sim = Sim(n, "Imp3D", "gossip", seed=seed, virtual_ranks=ranks, experimental=True)
+    orc = Oracle(n, "Imp3D", "gossip", seed)
+    for _ in range(3):
+        ga, oa = sim.step(100), orc.step(100)
+        assert ga == oa
+        same_state("gossip", sim.state(), orc.state())
+    sim.close()
+    orc.close()
