@@ -14,3 +14,9 @@ for rep in 1 2; do
 done
 timeout -k 10 600 python3 tools/traffic_probe.py 100000000 Imp3D gossip k_gossip_col "GP_EXP=1,GP_RQ8=0" "GP_EXP=1,GP_RQ8=1" > $O/traffic.txt 2>&1 || { tail -5 $O/traffic.txt; exit 1; }
 cat $O/traffic.txt
+# C2 (3D push-sum, 1e6: launch / latency bound): tile-shape variants of the round kernel, wall per round
+for v in base t1024m8 npt2 n2m6 t512m6; do
+  GOSSIP_HIP_LIB_EXPERIMENT=build/ablate/lib_$v.so timeout -k 10 120 python3 tools/variant_parity.py 64000 3D push-sum 300 3 > $O/c2_parity_$v.log 2>&1 || { tail -5 $O/c2_parity_$v.log; exit 1; }
+  GOSSIP_HIP_LIB_EXPERIMENT=build/ablate/lib_$v.so GP_EXP=1 timeout -k 10 120 python3 tools/perf_round.py 1000000 3D push-sum 2000 > $O/c2_perf_$v.log 2>&1 || { tail -5 $O/c2_perf_$v.log; exit 1; }
+  echo "C2 $v: $(grep -o 'no events: wall [0-9.]* ms/round' $O/c2_perf_$v.log) $(tail -1 $O/c2_parity_$v.log | cut -c1-40)"
+done
