@@ -324,7 +324,9 @@ int alloc_slab(gp_sim* s, Slab& sl, int r) {
             return rc;
     }
     if (col_gossip_counts(S)) {  // senders count their random-edge deliveries at the target (k_gossip_col)
-        S.rq8 = 0;
+        // byte counters, four per word (C3: 0.632 -> 0.600 ms per round, reads 16.5 -> 11.7 and
+        // writes 11.2 -> 9.8 B/node; profiles/r04/c3_byte_counters.txt)
+        S.rq8 = 1;
 #ifdef GP_EXPERIMENTS
         if (const char* e = std::getenv("GP_RQ8")) S.rq8 = e[0] == '1' ? 1u : 0u;
 #endif
@@ -898,7 +900,8 @@ double alg_bytes(const gp_sim* s) {
 
 // Kernel variant and grid for this run (measured defaults, GP_KERNEL / GP_GRID /
 // GP_XSEGS / GP_WALK override for experiments).
-void choose_kernel(gp_sim* s, int64_t nloc_max, int& kernel, uint32_t& col_xsegs, uint32_t& walk, uint32_t& wx) {
+void choose_kernel(gp_sim* s, int64_t nloc_max, int& kernel, uint32_t& col_xsegs, uint32_t& walk, uint32_t& wx,
+                   uint32_t& wide) {
     hipDeviceProp_t prop;
     (void)hipGetDeviceProperties(&prop, s->device);
     const gp_config* cfg = &s->cfg;
@@ -950,9 +953,26 @@ void choose_kernel(gp_sim* s, int64_t nloc_max, int& kernel, uint32_t& col_xsegs
     if (const char* e = std::getenv("GP_WALK")) walk = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("GP_WX")) wx = (uint32_t)std::max(1, std::atoi(e));
 #endif
+    // size class of the tiled kernels: a slab with at most two tiles per resident block of the
+    // 4-nodes-per-thread kernel (~2500 tiles, P <~ 2.6e6 per slab) runs the 1024-thread, one-node-
+    // per-thread build (gp_round_wide.hip): its node phase is one memory round trip per tile
+    // instead of four, which is what bounds a round with few tiles per block (C2, P = 1e6: 26.4 ->
+    // 21.0 us per round; profiles/r04/c2_tile_shape.txt)
+    wide = 0;
+    if (kernel == KERNEL_TILE) {
+        const int topo = cfg->topology == GP_LINE ? LINE : cfg->topology == GP_3D ? GRID3D : IMP3D;
+        const int64_t tiles = (nloc_max + 1023) / 1024 + 1;
+        const int64_t res4 = ps_tile_resident_blocks(topo, s->world > 1 && topo == IMP3D, s->device);
+        wide = res4 > 0 && tiles <= 2 * res4 ? 1u : 0u;
+#ifdef GP_EXPERIMENTS
+        if (const char* e = std::getenv("GP_WIDE")) wide = e[0] == '1' ? 1u : 0u;
+#endif
+    }
     if (walk == 3) {
         const int topo = cfg->topology == GP_LINE ? LINE : cfg->topology == GP_3D ? GRID3D : IMP3D;
-        const int64_t res = ps_tile_resident_blocks(topo, s->world > 1 && topo == IMP3D, s->device) / 8 * 8;
+        const bool rem = s->world > 1 && topo == IMP3D;
+        const int64_t res = (wide ? wide::ps_tile_resident_blocks(topo, rem, s->device)
+                                  : ps_tile_resident_blocks(topo, rem, s->device)) / 8 * 8;
         if (res >= 8) s->grid = (int)std::min<int64_t>(s->grid, res);
         else walk = 2;
     }
@@ -965,8 +985,8 @@ int build_sim(gp_sim* s) {
     int64_t nloc_max = 0;
     for (int w = 0; w < s->world; ++w) nloc_max = std::max<int64_t>(nloc_max, s->bounds[w + 1] - s->bounds[w]);
     int kernel;
-    uint32_t col_xsegs, walk, wx;
-    choose_kernel(s, nloc_max, kernel, col_xsegs, walk, wx);
+    uint32_t col_xsegs, walk, wx, wide;
+    choose_kernel(s, nloc_max, kernel, col_xsegs, walk, wx, wide);
     if (s->mode == MODE_VIRTUAL) {
         s->slab.resize(s->world);
         for (int w = 0; w < s->world; ++w) s->slab[w].rank = w;
@@ -976,6 +996,7 @@ int build_sim(gp_sim* s) {
     }
     for (Slab& sl : s->slab) {
         sl.S.kernel = kernel;
+        sl.S.tile_wide = wide;
         sl.S.col_xsegs = col_xsegs;
         sl.S.tile_walk = walk;
         sl.S.tile_wx = wx;

@@ -184,6 +184,7 @@ struct DevState {
     uint32_t tile_wx;    // RoundArgs::wx
     uint32_t tile_stage_cap;  // RoundArgs::stage_cap (experiments build only; default: no limit)
     uint32_t fuse_finalize;   // the round kernel closes its own round (single rank push-sum)
+    uint32_t tile_wide;       // KERNEL_TILE: the 1024-thread size class (gp_round_wide.hip)
     // Imp3D: the rank's in-edge count
     uint32_t nedges;
     // walk 3 (dynamic tile queue): per round parity, 8 per-XCD item counters,
@@ -272,6 +273,12 @@ uint32_t ind4_bytes_for(uint32_t lo, uint32_t nloc);
 hipError_t launch_pack_ind4(const DevState& S, uint32_t wide_at, int grid, hipStream_t st);
 hipError_t launch_pack_src_deg(const uint32_t* src, uint32_t* out, uint32_t n, const Geom& G, int grid,
                                hipStream_t st);
+
+// ---- the same tiled kernels as the small-population size class (gp_round_wide.hip)
+namespace wide {
+hipError_t launch_round_tile(const DevState& S, uint32_t round, int grid, hipStream_t st);
+int ps_tile_resident_blocks(int topo, bool remote, int device);
+}  // namespace wide
 
 // ---- kernels (gp_kernels.hip)
 hipError_t launch_init(const DevState& S, int grid, hipStream_t st);

@@ -379,7 +379,8 @@ hipError_t launch_histogram(const uint32_t* keys, uint32_t n, uint32_t* counts, 
 hipError_t launch_bulk(const DevState& S, uint32_t round, int grid, hipStream_t st) {
     const dim3 g(grid), b(BULK_THREADS);
     if (S.topo != FULL) {
-        if (S.kernel == KERNEL_TILE) return launch_round_tile(S, round, grid, st);
+        if (S.kernel == KERNEL_TILE)
+            return S.tile_wide ? wide::launch_round_tile(S, round, grid, st) : launch_round_tile(S, round, grid, st);
         if (S.kernel == KERNEL_COL) return launch_round_col(make_wave_args(S, round), S.topo, S.alg, round, grid, st);
         return hipErrorInvalidValue;
     }
@@ -400,6 +401,12 @@ const char* bulk_kernel_name(const DevState& S) {
                                    {"k_gossip_tile<LINE>", "k_full_gossip_send+recv", "k_gossip_col<GRID3D>",
                                     "k_gossip_col<IMP3D>"}};
     const int v = S.kernel == KERNEL_COL ? 1 : 0;
+    if (v == 0 && S.tile_wide && S.topo != FULL) {  // the 1024-thread size class (gp_round_wide.hip)
+        static const char* w[2][4] = {{"wide::k_gossip_tile<LINE>", "", "wide::k_gossip_tile<GRID3D>",
+                                       "wide::k_gossip_tile<IMP3D>"},
+                                      {"wide::k_ps_tile<LINE>", "", "wide::k_ps_tile<GRID3D>", "wide::k_ps_tile<IMP3D>"}};
+        return w[S.alg == PUSHSUM ? 1 : 0][S.topo];
+    }
     return S.alg == PUSHSUM ? ps[v][S.topo] : go[v][S.topo];
 }
 

@@ -27,6 +27,11 @@
 #include "gp_internal.hpp"
 
 namespace gp {
+#ifdef GP_ROUND_WIDE
+// gp_round_wide.hip: this file again with 1024-thread tiles of one node per
+// thread (the small-population size class), its host entry points in gp::wide
+namespace wide {
+#endif
 
 // Experiment knobs (tools/ablate.py); the product build uses the defaults.
 #ifndef GP_TPB
@@ -1296,6 +1301,9 @@ hipError_t launch_rbits_init(const DevState& S, int grid, hipStream_t st) {
     return hipGetLastError();
 }
 
+#ifdef GP_ROUND_WIDE
+}  // namespace wide
+#endif
 }  // namespace gp
 
 #if GP_STAMPS

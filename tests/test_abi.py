@@ -108,6 +108,6 @@ def test_product_library_has_no_environment_switches():
     prod = open(L.LIB_PATH, "rb").read()
     exp = open(os.path.join(os.path.dirname(L.LIB_PATH), "libgossip_hip_exp.so"), "rb").read()
     for knob in (b"GP_KERNEL", b"GP_GRID", b"GP_XSEGS", b"GP_WALK", b"GP_WX", b"GP_STAGE_CAP", b"GP_NO_PACK",
-                 b"GP_FORCE_RCCL", b"GP_XCAP"):
+                 b"GP_FORCE_RCCL", b"GP_XCAP", b"GP_WIDE", b"GP_RQ8"):
         assert knob not in prod, knob
         assert knob in exp, knob

@@ -319,15 +319,19 @@ KERNEL_CASES = [  # (num_nodes, topology, algorithm, seed, rounds, checkpoint, x
 ]
 
 
-@pytest.mark.parametrize("kernel", ["col", "tile"])
+@pytest.mark.parametrize("kernel", ["col", "tile", "tile4", "tile1"])
 @pytest.mark.parametrize("n,topo,alg,seed,rounds,chk,xsegs", KERNEL_CASES, ids=lambda v: str(v))
 def test_kernel_variant_parity(kernel, n, topo, alg, seed, rounds, chk, xsegs, monkeypatch):
     """Every round-kernel variant (column march / tiled; experiments build,
     GP_KERNEL) bit-exact vs the oracle, the column march also with its
-    x-segmentation forced."""
+    x-segmentation forced; the tiled kernel in the size class its population
+    selects (tile), forced to 256 threads x 4 nodes (tile4, GP_WIDE=0) and to the
+    1024-thread x 1 node build (tile1, GP_WIDE=1, gp_round_wide.hip)."""
     if kernel == "col" and alg == "push-sum":
         pytest.skip("the column march runs lattice gossip only")
-    monkeypatch.setenv("GP_KERNEL", kernel)
+    monkeypatch.setenv("GP_KERNEL", "tile" if kernel.startswith("tile") else kernel)
+    if kernel in ("tile4", "tile1"):
+        monkeypatch.setenv("GP_WIDE", "1" if kernel == "tile1" else "0")
     monkeypatch.setenv("GP_XSEGS", xsegs)
     sim, orc = Sim(n, topo, alg, seed=seed, experimental=True), Oracle(n, topo, alg, seed)
     done = 0
@@ -358,6 +362,7 @@ def test_tile_walk_and_sender_packing_parity(n, topo, seed, rounds, chk, walk, p
     if topo != "Imp3D" and pack == "0":
         pytest.skip("sender packing is Imp3D only")
     monkeypatch.setenv("GP_KERNEL", "tile")
+    monkeypatch.setenv("GP_WIDE", "0")  # the 256 x 4 kernel (the 1e9 one); its walks
     monkeypatch.setenv("GP_WALK", walk)
     monkeypatch.setenv("GP_WX", "3")
     monkeypatch.setenv("GP_NO_PACK", "0" if pack == "1" else "1")
@@ -382,6 +387,7 @@ def test_nibble_wide_tile_fallback_parity(wide_at, monkeypatch):
     most (2) or some (4) tiles take the path; bit-exact vs the oracle through
     activation into steady state."""
     monkeypatch.setenv("GP_IND4_WIDE", wide_at)
+    monkeypatch.setenv("GP_WIDE", "0")
     n, topo = 512000, "Imp3D"
     sim, orc = Sim(n, topo, "push-sum", seed=7, experimental=True), Oracle(n, topo, "push-sum", 7)
     for _ in range(2):
@@ -408,13 +414,15 @@ def test_seed_random_edge_round0(kernel, monkeypatch):
         orc.close()
 
 
+@pytest.mark.parametrize("wide", ["0", "1"])
 @pytest.mark.parametrize("cap", ["0", "1000", "1024"])
-def test_tile_unstaged_path_parity(cap, monkeypatch):
+def test_tile_unstaged_path_parity(cap, wide, monkeypatch):
     """Push-sum Imp3D tile kernel with the staging cap lowered (GP_STAGE_CAP): tiles
     with more in-edges than the cap take the unstaged path (per-edge decisions and
     gathers from HBM) -- all of them at 0, a mix at 1000 / 1024 (mean in-degree
     1024 per tile).  At the default cap (1216) that path runs for ~1e-9 of tiles."""
     monkeypatch.setenv("GP_KERNEL", "tile")
+    monkeypatch.setenv("GP_WIDE", wide)
     monkeypatch.setenv("GP_STAGE_CAP", cap)
     n, seed, rounds, chk = 512000, 4, 90, 45
     sim, orc = Sim(n, "Imp3D", "push-sum", seed=seed, experimental=True), Oracle(n, "Imp3D", "push-sum", seed)
