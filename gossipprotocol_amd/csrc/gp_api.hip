@@ -456,14 +456,19 @@ int build_imp3d(gp_sim* s) {
 int finalize(gp_sim* s, uint32_t round_done, uint32_t round_next);
 
 // Fixed-capacity exchange buffers per rank pair: capacity = expected messages
-// per round + 12 sigma + 64 (never more than the pair's random edges).  The
-// full-topology push-sum exchange has two regions per pair, one per half of the
-// sender's senders (s->xhalves), moved separately (launch_round_full_multi).
+// per round + 12 sigma + 64 (never more than the pair's random edges).  Push-sum
+// exchanges have two regions per pair, one per half of the sender's senders
+// (s->xhalves), moved separately on the exchange stream so that one half's
+// transfer overlaps the other half's packing / unpacking (full topology:
+// launch_round_full_multi; Imp3D: exchange).
 int setup_exchange(gp_sim* s) {
     const int W = s->world;
     const bool push = s->cfg.algorithm == GP_PUSHSUM;
     const bool full = s->cfg.topology == GP_FULL;
-    const int NH = full && push ? 2 : 1;
+    int NH = push ? 2 : 1;
+#ifdef GP_EXPERIMENTS
+    if (const char* e = std::getenv("GP_XHALVES")) NH = std::max(1, std::min(2, std::atoi(e)));
+#endif
     s->xhalves = NH;
     std::vector<uint32_t> caps((size_t)NH * W * W, 0);  // caps[(h * W + a) * W + b]: a -> b, region h
     Scratch tmp_mem;
@@ -494,28 +499,32 @@ int setup_exchange(gp_sim* s) {
     for (Slab& sl : s->slab) {
         if (full) break;
         DevState& S = sl.S;
-        HIP_TRY(hipMemsetAsync(mu, 0, sizeof(double) * XMAXW, s->stream));
-        HIP_TRY(hipMemsetAsync(n, 0, sizeof(unsigned long long) * XMAXW, s->stream));
-        ExpectArgs ea{};
-        ea.rnd = S.rnd;
-        ea.lo = S.lo;
-        ea.nloc = S.nloc;
-        ea.W = W;
-        ea.me = sl.rank;
-        for (int w = 0; w <= W; ++w) ea.bounds[w] = s->bounds[w];
-        ea.G = S.G;
-        ea.mu = mu;
-        ea.n = n;
-        HIP_TRY(launch_expect(ea, s->grid, s->stream));
-        double hmu[XMAXW];
-        unsigned long long hn[XMAXW];
-        HIP_TRY(hipMemcpyAsync(hmu, mu, sizeof hmu, hipMemcpyDeviceToHost, s->stream));
-        HIP_TRY(hipMemcpyAsync(hn, n, sizeof hn, hipMemcpyDeviceToHost, s->stream));
-        HIP_TRY(hipStreamSynchronize(s->stream));
-        for (int b = 0; b < W; ++b) {
-            if (b == sl.rank || hn[b] == 0) continue;
-            const double c = std::ceil(hmu[b] + 12.0 * std::sqrt(hmu[b]) + 64.0);
-            caps[(size_t)sl.rank * W + b] = (uint32_t)std::min<double>(c, (double)hn[b]);
+        for (int h = 0; h < NH; ++h) {  // region h: senders [s_lo, s_hi) of the slab (xhalf_range)
+            HIP_TRY(hipMemsetAsync(mu, 0, sizeof(double) * XMAXW, s->stream));
+            HIP_TRY(hipMemsetAsync(n, 0, sizeof(unsigned long long) * XMAXW, s->stream));
+            ExpectArgs ea{};
+            ea.rnd = S.rnd;
+            ea.lo = S.lo;
+            ea.nloc = S.nloc;
+            ea.s_lo = NH == 1 || h == 0 ? 0u : S.nloc / 2;
+            ea.s_hi = NH == 1 || h == 1 ? S.nloc : S.nloc / 2;
+            ea.W = W;
+            ea.me = sl.rank;
+            for (int w = 0; w <= W; ++w) ea.bounds[w] = s->bounds[w];
+            ea.G = S.G;
+            ea.mu = mu;
+            ea.n = n;
+            HIP_TRY(launch_expect(ea, s->grid, s->stream));
+            double hmu[XMAXW];
+            unsigned long long hn[XMAXW];
+            HIP_TRY(hipMemcpyAsync(hmu, mu, sizeof hmu, hipMemcpyDeviceToHost, s->stream));
+            HIP_TRY(hipMemcpyAsync(hn, n, sizeof hn, hipMemcpyDeviceToHost, s->stream));
+            HIP_TRY(hipStreamSynchronize(s->stream));
+            for (int b = 0; b < W; ++b) {
+                if (b == sl.rank || hn[b] == 0) continue;
+                const double c = std::ceil(hmu[b] + 12.0 * std::sqrt(hmu[b]) + 64.0);
+                caps[((size_t)h * W + sl.rank) * W + b] = (uint32_t)std::min<double>(c, (double)hn[b]);
+            }
         }
     }
 #ifdef GP_EXPERIMENTS
@@ -525,14 +534,17 @@ int setup_exchange(gp_sim* s) {
     }
 #endif
     if (s->mode == MODE_RCCL && !full) {
-        // every rank learns the capacities of the buffers it will receive
+        // every rank learns the capacities of the buffers it will receive (per region)
         uint32_t* d = nullptr;
         HIP_TRY(tmp_mem.alloc(&d, (size_t)W * W));
-        HIP_TRY(hipMemcpyAsync(d + (size_t)s->rank * W, caps.data() + (size_t)s->rank * W, sizeof(uint32_t) * W,
-                               hipMemcpyHostToDevice, s->stream));
-        NCCL_TRY(ncclAllGather(d + (size_t)s->rank * W, d, W, ncclUint32, s->comm, s->stream));
-        HIP_TRY(hipMemcpyAsync(caps.data(), d, sizeof(uint32_t) * W * W, hipMemcpyDeviceToHost, s->stream));
-        HIP_TRY(hipStreamSynchronize(s->stream));
+        for (int h = 0; h < NH; ++h) {
+            uint32_t* row = caps.data() + (size_t)h * W * W;
+            HIP_TRY(hipMemcpyAsync(d + (size_t)s->rank * W, row + (size_t)s->rank * W, sizeof(uint32_t) * W,
+                                   hipMemcpyHostToDevice, s->stream));
+            NCCL_TRY(ncclAllGather(d + (size_t)s->rank * W, d, W, ncclUint32, s->comm, s->stream));
+            HIP_TRY(hipMemcpyAsync(row, d, sizeof(uint32_t) * W * W, hipMemcpyDeviceToHost, s->stream));
+            HIP_TRY(hipStreamSynchronize(s->stream));
+        }
     }
     int rc;
     for (Slab& sl : s->slab) {
@@ -733,43 +745,23 @@ int launch_round_full_multi(gp_sim* s, uint32_t r, hipEvent_t e0, hipEvent_t e1)
 }
 
 // Halo refresh + Imp3D random-edge exchange for round `rn`, whose state the
-// previous round kernel has just written to buffers rn & 1.
+// previous round kernel has just written to buffers rn & 1.  Push-sum moves the
+// random-edge messages in two regions (s->xhalves): the senders' first half is
+// packed and handed to the exchange stream, whose transfer (with the halo planes)
+// overlaps the second half's packing; the first half is unpacked while the second
+// is in flight.  Events order the streams, so every rank issues its RCCL groups in
+// one order (region 0, region 1), before the finalize all-reduce on the compute
+// stream.
 int exchange(gp_sim* s, uint32_t rn) {
     const int W = s->world;
     if (W == 1 || s->cfg.topology == GP_FULL) return GP_OK;  // full: the exchange is inside the round
     const int b = rn & 1;
     const bool push = s->cfg.algorithm == GP_PUSHSUM;
     const bool imp = s->cfg.topology == GP_IMP3D;
-    if (imp) {
-        for (Slab& sl : s->slab) {
-            DevState& S = sl.S;
-            ZeroArgs z{};
-            PackArgs pa{};
-            pa.nbn = S.nb[b];
-            pa.swn = push ? S.sw[b] : nullptr;
-            pa.rnd = S.rnd;
-            pa.pos = sl.pos;
-            pa.xdst = sl.xdst;
-            pa.lo = S.lo;
-            pa.nloc = S.nloc;
-            pa.base = S.base;
-            pa.W = W;
-            pa.me = sl.rank;
-            pa.push = push ? 1 : 0;
-            pa.counts = col_gossip_counts(S) ? 1 : 0;
-            for (int w = 0; w <= W; ++w) pa.bounds[w] = s->bounds[w];
-            for (int p = 0; p < W; ++p) {
-                pa.peer[p] = xpeer(sl.xsend, sl.soff[p], sl.cap_out[p]);
-                z.cnt[p] = pa.peer[p].cnt;
-            }
-            z.n = W;
-            pa.overflow = sl.overflow;
-            HIP_TRY(launch_zero_counts(z, s->stream));
-            HIP_TRY(launch_pack(pa, s->grid, s->stream));
-        }
-    }
+    const int NH = imp ? s->xhalves : 1;
+    hipStream_t xs = NH > 1 && s->xstream ? s->xstream : s->stream;
     const size_t H = s->halo;
-    if (s->mode == MODE_VIRTUAL) {
+    if (s->mode == MODE_VIRTUAL) {  // halo planes by device copies (round kernel -> next round kernel)
         for (int r = 0; r + 1 < W; ++r) {
             DevState& A = s->slab[r].S;  // lower slab
             DevState& B = s->slab[r + 1].S;
@@ -786,55 +778,104 @@ int exchange(gp_sim* s, uint32_t rn) {
                                        hipMemcpyDeviceToDevice, s->stream));
             }
         }
+    }
+    for (int h = 0; h < NH; ++h) {
         if (imp) {
-            int rc = transfer_xbufs(s, 0, s->stream);
-            if (rc) return rc;
-        }
-    } else {
-        Slab& sl = s->slab[0];
-        DevState& S = sl.S;
-        const int r = sl.rank;
-        NCCL_TRY(ncclGroupStart());
-        if (r > 0) {  // my first H ids <-> lower neighbour's last H ids
-            NCCL_TRY(ncclSend(S.nb[b] + (S.lo - S.base), H, ncclUint8, r - 1, s->comm, s->stream));
-            NCCL_TRY(ncclRecv(S.nb[b] + (S.lo - H - S.base), H, ncclUint8, r - 1, s->comm, s->stream));
-            if (push) {
-                NCCL_TRY(ncclSend(S.sw[b] + (S.lo - S.base), H * 16, ncclUint8, r - 1, s->comm, s->stream));
-                NCCL_TRY(ncclRecv(S.sw[b] + (S.lo - H - S.base), H * 16, ncclUint8, r - 1, s->comm, s->stream));
+            for (Slab& sl : s->slab) {
+                DevState& S = sl.S;
+                ZeroArgs z{};
+                PackArgs pa{};
+                pa.nbn = S.nb[b];
+                pa.swn = push ? S.sw[b] : nullptr;
+                pa.rnd = S.rnd;
+                pa.pos = sl.pos;
+                pa.xdst = sl.xdst;
+                pa.lo = S.lo;
+                pa.nloc = S.nloc;
+                pa.s_lo = NH == 1 || h == 0 ? 0u : S.nloc / 2;
+                pa.s_hi = NH == 1 || h == 1 ? S.nloc : S.nloc / 2;
+                pa.base = S.base;
+                pa.W = W;
+                pa.me = sl.rank;
+                pa.push = push ? 1 : 0;
+                pa.counts = col_gossip_counts(S) ? 1 : 0;
+                for (int w = 0; w <= W; ++w) pa.bounds[w] = s->bounds[w];
+                for (int p = 0; p < W; ++p) {
+                    const size_t i = (size_t)h * W + p;
+                    pa.peer[p] = xpeer(sl.xsend, sl.soff[i], sl.cap_out[i]);
+                    z.cnt[p] = pa.peer[p].cnt;
+                }
+                z.n = W;
+                pa.overflow = sl.overflow;
+                HIP_TRY(launch_zero_counts(z, s->stream));
+                HIP_TRY(launch_pack(pa, s->grid, s->stream));
             }
         }
-        if (r < W - 1) {  // my last H ids <-> upper neighbour's first H ids
-            NCCL_TRY(ncclSend(S.nb[b] + (sl.hi - H - S.base), H, ncclUint8, r + 1, s->comm, s->stream));
-            NCCL_TRY(ncclRecv(S.nb[b] + (sl.hi - S.base), H, ncclUint8, r + 1, s->comm, s->stream));
-            if (push) {
-                NCCL_TRY(ncclSend(S.sw[b] + (sl.hi - H - S.base), H * 16, ncclUint8, r + 1, s->comm, s->stream));
-                NCCL_TRY(ncclRecv(S.sw[b] + (sl.hi - S.base), H * 16, ncclUint8, r + 1, s->comm, s->stream));
-            }
+        if (xs != s->stream) {
+            HIP_TRY(hipEventRecord(s->ev_send[h], s->stream));
+            HIP_TRY(hipStreamWaitEvent(xs, s->ev_send[h], 0));
         }
-        if (imp)
-            for (int p = 0; p < W; ++p) {
-                if (p == r) continue;
-                if (sl.sbytes[p]) NCCL_TRY(ncclSend(sl.xsend + sl.soff[p], sl.sbytes[p], ncclUint8, p, s->comm, s->stream));
-                if (sl.rbytes[p]) NCCL_TRY(ncclRecv(sl.xrecv + sl.roff[p], sl.rbytes[p], ncclUint8, p, s->comm, s->stream));
+        if (s->mode == MODE_VIRTUAL) {
+            if (imp) {
+                int rc = transfer_xbufs(s, h, xs);
+                if (rc) return rc;
             }
-        NCCL_TRY(ncclGroupEnd());
+        } else {
+            Slab& sl = s->slab[0];
+            DevState& S = sl.S;
+            const int r = sl.rank;
+            NCCL_TRY(ncclGroupStart());
+            if (h == 0 && r > 0) {  // my first H ids <-> lower neighbour's last H ids
+                NCCL_TRY(ncclSend(S.nb[b] + (S.lo - S.base), H, ncclUint8, r - 1, s->comm, xs));
+                NCCL_TRY(ncclRecv(S.nb[b] + (S.lo - H - S.base), H, ncclUint8, r - 1, s->comm, xs));
+                if (push) {
+                    NCCL_TRY(ncclSend(S.sw[b] + (S.lo - S.base), H * 16, ncclUint8, r - 1, s->comm, xs));
+                    NCCL_TRY(ncclRecv(S.sw[b] + (S.lo - H - S.base), H * 16, ncclUint8, r - 1, s->comm, xs));
+                }
+            }
+            if (h == 0 && r < W - 1) {  // my last H ids <-> upper neighbour's first H ids
+                NCCL_TRY(ncclSend(S.nb[b] + (sl.hi - H - S.base), H, ncclUint8, r + 1, s->comm, xs));
+                NCCL_TRY(ncclRecv(S.nb[b] + (sl.hi - S.base), H, ncclUint8, r + 1, s->comm, xs));
+                if (push) {
+                    NCCL_TRY(ncclSend(S.sw[b] + (sl.hi - H - S.base), H * 16, ncclUint8, r + 1, s->comm, xs));
+                    NCCL_TRY(ncclRecv(S.sw[b] + (sl.hi - S.base), H * 16, ncclUint8, r + 1, s->comm, xs));
+                }
+            }
+            if (imp)
+                for (int p = 0; p < W; ++p) {
+                    if (p == r) continue;
+                    const size_t i = (size_t)h * W + p;
+                    if (sl.sbytes[i]) NCCL_TRY(ncclSend(sl.xsend + sl.soff[i], sl.sbytes[i], ncclUint8, p, s->comm, xs));
+                    if (sl.rbytes[i]) NCCL_TRY(ncclRecv(sl.xrecv + sl.roff[i], sl.rbytes[i], ncclUint8, p, s->comm, xs));
+                }
+            NCCL_TRY(ncclGroupEnd());
+        }
+        if (xs != s->stream) HIP_TRY(hipEventRecord(s->ev_xfer[h], xs));
     }
     if (imp) {
-        for (Slab& sl : s->slab) {
-            UnpackArgs ua{};
-            ua.rtag = sl.S.rtag;
-            ua.rmsg = sl.S.rmsg;
-            ua.rq = col_gossip_counts(sl.S) ? sl.S.rq[rn & 1] : nullptr;  // next round's deliveries
-            ua.rq8 = sl.S.rq8;
-            ua.nedges = ua.rq ? sl.S.nloc : sl.nedges;
-            ua.W = W;
-            ua.me = sl.rank;
-            ua.push = push ? 1 : 0;
-            for (int p = 0; p < W; ++p) ua.peer[p] = xpeer(sl.xrecv, sl.roff[p], sl.cap_in[p]);
-            ua.overflow = sl.overflow;
-            ua.all_active = &sl.S.ctl->all_active;
-            HIP_TRY(launch_unpack(ua, rn, std::max(1, s->grid / 8), s->stream));
+        for (int h = 0; h < NH; ++h) {
+            if (xs != s->stream) HIP_TRY(hipStreamWaitEvent(s->stream, s->ev_xfer[h], 0));
+            for (Slab& sl : s->slab) {
+                UnpackArgs ua{};
+                ua.rtag = sl.S.rtag;
+                ua.rmsg = sl.S.rmsg;
+                ua.rq = col_gossip_counts(sl.S) ? sl.S.rq[rn & 1] : nullptr;  // next round's deliveries
+                ua.rq8 = sl.S.rq8;
+                ua.nedges = ua.rq ? sl.S.nloc : sl.nedges;
+                ua.W = W;
+                ua.me = sl.rank;
+                ua.push = push ? 1 : 0;
+                for (int p = 0; p < W; ++p) {
+                    const size_t i = (size_t)h * W + p;
+                    ua.peer[p] = xpeer(sl.xrecv, sl.roff[i], sl.cap_in[i]);
+                }
+                ua.overflow = sl.overflow;
+                ua.all_active = &sl.S.ctl->all_active;
+                HIP_TRY(launch_unpack(ua, rn, std::max(1, s->grid / 8), s->stream));
+            }
         }
+    } else if (xs != s->stream) {
+        HIP_TRY(hipStreamWaitEvent(s->stream, s->ev_xfer[NH - 1], 0));
     }
     return GP_OK;
 }

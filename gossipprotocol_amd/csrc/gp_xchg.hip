@@ -49,13 +49,13 @@ static_assert(XMAXW <= 16, "k_pack keeps a destination rank in 4 bits");
 __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
     __shared__ uint32_t cnt[XMAXW], off[XMAXW];
     __shared__ uint32_t bnd[XMAXW + 1];
-    const uint32_t r0 = blockIdx.x * PACK_RANGE;
-    if (r0 >= a.nloc) return;
+    const uint32_t r0 = a.s_lo + blockIdx.x * PACK_RANGE;
+    if (r0 >= a.s_hi) return;
     if (threadIdx.x < XMAXW) cnt[threadIdx.x] = 0u;
     if (threadIdx.x <= (uint32_t)a.W) bnd[threadIdx.x] = a.bounds[threadIdx.x];
     __syncthreads();
     const uint32_t me = (uint32_t)a.me;
-    const uint32_t last = a.nloc - 1;
+    const uint32_t last = a.s_hi - 1;
     // destination rank per sender, a nibble each; `me` means "no message" (a sender never
     // packs for its own rank, so the value is free for every world size up to XMAXW = 16)
     const uint32_t none = (uint32_t)a.me;
@@ -74,7 +74,7 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
         for (int h = 0; h < 8; ++h) {
             const uint32_t li = r0 + (g * 8 + h) * 256u + threadIdx.x;
             uint32_t d = none;
-            if (li < a.nloc && (b[h] & DIR_MASK) == DIR_RANDOM && t[h] != me) {
+            if (li < a.s_hi && (b[h] & DIR_MASK) == DIR_RANDOM && t[h] != me) {
                 d = t[h];
                 atomicAdd(&cnt[d], 1u);
             }
@@ -196,7 +196,7 @@ __global__ __launch_bounds__(256) void k_expect(ExpectArgs a) {
         scnt[threadIdx.x] = 0ull;
     }
     __syncthreads();
-    for (uint32_t li = blockIdx.x * 256 + threadIdx.x; li < a.nloc; li += gridDim.x * 256) {
+    for (uint32_t li = a.s_lo + blockIdx.x * 256 + threadIdx.x; li < a.s_hi; li += gridDim.x * 256) {
         const uint32_t own = owner_of(a.rnd[li], a.bounds, a.W);
         if (own == (uint32_t)a.me) continue;
         const uint32_t deg = popc6(present_mask<IMP3D>(a.lo + li, a.G)) + 1u;
@@ -213,7 +213,7 @@ __global__ __launch_bounds__(256) void k_expect(ExpectArgs a) {
 // ---------------------------------------------------------------- launchers
 hipError_t launch_pack(const PackArgs& a, int grid, hipStream_t st) {
     (void)grid;
-    const uint32_t blocks = (a.nloc + PACK_RANGE - 1) / PACK_RANGE;
+    const uint32_t blocks = a.s_hi > a.s_lo ? (a.s_hi - a.s_lo + PACK_RANGE - 1) / PACK_RANGE : 0u;
     if (blocks) hipLaunchKernelGGL(k_pack, dim3(blocks), dim3(256), 0, st, a);
     return hipGetLastError();
 }

@@ -23,6 +23,7 @@ struct PackArgs {
     const uint8_t* xdst;  // owner rank of that edge's target (id - lo)
     const uint32_t* pos;  // its slot in the destination's in-edge array (id - lo; null in counts mode)
     uint32_t lo, nloc, base;
+    uint32_t s_lo, s_hi;  // the senders packed by this launch (local ids, one exchange region)
     int W, me, push;
     int counts;           // gossip column kernel: the entry is the target's local id at its owner
                           // (a delivery count, k_unpack adds it to rq), not an in-edge slot
@@ -67,6 +68,7 @@ struct PosArgs {
 struct ExpectArgs {
     const uint32_t* rnd;
     uint32_t lo, nloc;
+    uint32_t s_lo, s_hi;  // senders counted (local ids)
     int W, me;
     uint32_t bounds[XMAXW + 1];
     Geom G;

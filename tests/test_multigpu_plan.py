@@ -77,12 +77,14 @@ def test_c5_imp3d_pushsum_1e9_world8_plan():
     bounds, mu, var = imp3d_pair_stats(P, g, W)
     assert [(bounds[w + 1] - bounds[w]) // (g * g) for w in range(W)] == [125] * 8  # planes per rank
     for a in range(W):
-        caps_out = [cap_of(mu[a, b]) if b != a else 0 for b in range(W)]
-        caps_in = [cap_of(mu[b, a]) if b != a else 0 for b in range(W)]
+        # push-sum: two regions per pair, one per half of the sender's slab, each sized for
+        # its own expectation (setup_exchange; both halves hold ~half of the pair's senders)
+        caps_out = [cap_of(mu[a, b] / 2) if b != a else 0 for b in range(W) for _ in range(2)]
+        caps_in = [cap_of(mu[b, a] / 2) if b != a else 0 for b in range(W) for _ in range(2)]
         for b in range(W):
             if b == a:
                 continue
-            margin = (caps_out[b] - mu[a, b]) / math.sqrt(var[a, b])
+            margin = (cap_of(mu[a, b] / 2) - mu[a, b] / 2) / math.sqrt(var[a, b] / 2)
             assert margin >= 12.0  # per-round overflow probability below GAUSS_12SIGMA_TAIL
             assert 2.0e6 < mu[a, b] < 2.5e6  # ~2.2 M messages per pair per round
         nloc = bounds[a + 1] - bounds[a]
@@ -157,16 +159,19 @@ def test_realised_imp3d_counts_stay_below_capacity_world8():
     src_rank = np.searchsorted(np.array(bounds[1:-1]), ids, side="right")
     dst_rank = np.searchsorted(np.array(bounds[1:-1]), rnd, side="right")
     inv_deg = 1.0 / geo.degree(ids)
-    mu = np.zeros((W, W))
-    np.add.at(mu, (src_rank, dst_rank), inv_deg)
+    # push-sum exchange region of every sender: the half of its slab it lies in (setup_exchange)
+    b_arr = np.array(bounds)
+    half = ((ids - b_arr[src_rank]) >= (b_arr[src_rank + 1] - b_arr[src_rank]) // 2).astype(np.int64)
+    mu = np.zeros((2, W, W))
+    np.add.at(mu, (half, src_rank, dst_rank), inv_deg)
     cap = np.vectorize(lambda m: min(cap_of(m), 10**9))(mu)
     worst = 0.0
+    off = np.broadcast_to(~np.eye(W, dtype=bool), (2, W, W))
     for r in range(40):
         d = geo.draw_dir(ids, S_PUSHSUM, r)
         sent = d == DIR_RANDOM
-        cnt = np.zeros((W, W), dtype=np.int64)
-        np.add.at(cnt, (src_rank[sent], dst_rank[sent]), 1)
-        off = ~np.eye(W, dtype=bool)
+        cnt = np.zeros((2, W, W), dtype=np.int64)
+        np.add.at(cnt, (half[sent], src_rank[sent], dst_rank[sent]), 1)
         assert np.all(cnt[off] <= cap[off])
         worst = max(worst, float(np.max((cnt[off] - mu[off]) / np.sqrt(mu[off]))))
     assert worst < 6.0  # realised fluctuations are a few sigma; the capacity allows 12

@@ -93,8 +93,8 @@ def pair_bytes(n, topo, alg, W, halves=1):
             _, mu, _ = imp3d_pair_stats(P, g, W)
             for a in range(W):
                 for b in range(W):
-                    if b != a:
-                        B[a][b] = xbuf(cap_of(mu[a, b]))
+                    if b != a:  # push-sum: one region per half of the sender's slab
+                        B[a][b] = sum(xbuf(cap_of(mu[a, b] / halves)) for _ in range(halves))
     return P, bounds, B, halo
 
 
@@ -141,9 +141,11 @@ def model(tdir, n, topo, alg, W, rounds, out=None):
         copy_ms.append(cp)
         for k in range(W):
             rank_ms[k].append(tr[k])
-    # full push-sum runs its exchange in two halves overlapped with the send / coarse
-    # passes (gp_api.hip launch_round_full_multi): those kernels appear twice per slab
-    halves = 2 if topo == "full" and alg == "push-sum" else 1
+    # push-sum runs its exchange in two halves overlapped with the send / coarse passes
+    # (full, gp_api.hip launch_round_full_multi) or the pack / unpack (Imp3D, exchange):
+    # those kernels appear twice per slab
+    halves = 2 if alg == "push-sum" and topo in ("full", "Imp3D") else 1
+    first_k, second_k = ("k_fbm_send", "k_fbm_coarse") if topo == "full" else ("k_pack", "k_unpack")
     P, bounds, B, halo = pair_bytes(n, topo, alg, W, halves)
     kern = {k: [statistics.mean(x[s] for x in v) for s in range(W)] for k, v in per_slab.items()}
     comp = [statistics.mean(v) for v in rank_ms]
@@ -156,13 +158,13 @@ def model(tdir, n, topo, alg, W, rounds, out=None):
             by = {}
             for name, ms in grp:
                 by.setdefault(short(name), []).append(ms)
-            for nm in ("k_fbm_send", "k_fbm_coarse"):
+            for nm in (first_k, second_k):
                 v = by.get(nm, [])
                 if len(v) == 2 * W:
                     hk.setdefault(nm, []).append(v)
-        if len(hk.get("k_fbm_send", [])) and len(hk.get("k_fbm_coarse", [])):
-            s_h = [[statistics.mean(x[h * W + k] for x in hk["k_fbm_send"]) for k in range(W)] for h in range(2)]
-            c_h = [[statistics.mean(x[h * W + k] for x in hk["k_fbm_coarse"]) for k in range(W)] for h in range(2)]
+        if len(hk.get(first_k, [])) and len(hk.get(second_k, [])):
+            s_h = [[statistics.mean(x[h * W + k] for x in hk[first_k]) for k in range(W)] for h in range(2)]
+            c_h = [[statistics.mean(x[h * W + k] for x in hk[second_k]) for k in range(W)] for h in range(2)]
             piped = {"send_half_ms": [max(v) for v in s_h], "coarse_half_ms": [max(v) for v in c_h],
                      "rest_ms": max(comp[k] - s_h[0][k] - s_h[1][k] - c_h[0][k] - c_h[1][k] for k in range(W))}
     res = {"workload": f"{alg} {topo} n={n} P={P}", "W": W, "rounds_measured": len(groups),
@@ -185,7 +187,7 @@ def model(tdir, n, topo, alg, W, rounds, out=None):
         t_x = link / (bw * 1e9) * 1e3 + (GROUP_LAT_MS if link else 0.0) * halves
         serial = t_comp + t_x + ALLREDUCE_LAT_MS
         overlap = max(t_comp, t_x) + ALLREDUCE_LAT_MS
-        if piped:  # as scheduled: x_h after send_h, coarse_h after x_h (one exchange stream)
+        if piped:  # as scheduled: x_h after send_h / pack_h, coarse_h / unpack_h after x_h (one exchange stream)
             xh = t_x / 2
             s0, s1 = piped["send_half_ms"]
             c0, c1 = piped["coarse_half_ms"]
