@@ -994,13 +994,15 @@ void choose_kernel(gp_sim* s, int64_t nloc_max, int& kernel, uint32_t& col_xsegs
     if (const char* e = std::getenv("GP_WALK")) walk = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("GP_WX")) wx = (uint32_t)std::max(1, std::atoi(e));
 #endif
-    // size class of the tiled kernels: a slab with at most two tiles per resident block of the
-    // 4-nodes-per-thread kernel (~2500 tiles, P <~ 2.6e6 per slab) runs the 1024-thread, one-node-
-    // per-thread build (gp_round_wide.hip): its node phase is one memory round trip per tile
-    // instead of four, which is what bounds a round with few tiles per block (C2, P = 1e6: 26.4 ->
-    // 21.0 us per round; profiles/r04/c2_tile_shape.txt)
+    // size class of the tiled kernels: line / 3D push-sum on a slab with at most two tiles per
+    // resident block of the 4-nodes-per-thread kernel (~2500 tiles, P <~ 2.6e6 per slab) runs the
+    // 1024-thread, one-node-per-thread build (gp_round_wide.hip): its node phase is one memory
+    // round trip per tile instead of four, which is what bounds a round with few tiles per block
+    // (C2, 3D push-sum P = 1e6: 26.5 -> 20.7 us per round; line push-sum n = 1000: 10.2 -> 8.8).
+    // Imp3D push-sum (its in-edge pass spills at 8 waves) and the gossip tile kernel measured
+    // slower in that build at every size (profiles/r04/tile_size_class.txt)
     wide = 0;
-    if (kernel == KERNEL_TILE) {
+    if (kernel == KERNEL_TILE && push && cfg->topology != GP_IMP3D) {
         const int topo = cfg->topology == GP_LINE ? LINE : cfg->topology == GP_3D ? GRID3D : IMP3D;
         const int64_t tiles = (nloc_max + 1023) / 1024 + 1;
         const int64_t res4 = ps_tile_resident_blocks(topo, s->world > 1 && topo == IMP3D, s->device);

@@ -145,6 +145,8 @@ def test_c4_full_pushsum_1e8_to_convergence(c4, seg):
 
 
 def test_c4_converged(c4):
+    if os.environ.get("GP_BASELINE_FULL") != "1":
+        pytest.skip("lock-step to convergence: GP_BASELINE_FULL=1 (test_run_to_convergence_matches_oracle_record)")
     assert c4.finished and c4.sim.alerts_total >= c4.sim.threshold
     assert c4.sim.rounds == c4.orc.rounds
 
