@@ -10,3 +10,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
 python3 tools/kt_steady.py $O/prof_kt k_ps_tile --last 20
 GP_BENCH_DEVICE=0 timeout -k 10 400 python -u bench.py --gpus 2 --steps 10 > $O/bench_gpus2_rehearsal.json 2> $O/bench_gpus2_rehearsal.err || { tail -20 $O/bench_gpus2_rehearsal.err; exit 1; }
 cat $O/bench_gpus2_rehearsal.json
+timeout -k 10 200 python -u tools/converge.py 1000000000 Imp3D push-sum 1 $O/c5_converge_1e9.json > $O/converge.log 2>&1 || { tail -20 $O/converge.log; exit 1; }
+tail -1 $O/converge.log
