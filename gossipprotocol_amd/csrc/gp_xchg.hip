@@ -42,16 +42,40 @@ __device__ __forceinline__ uint32_t owner_of(uint32_t t, const uint32_t* bounds,
 // run offset (an LDS counter per rank).  (The previous form reserved per wave
 // and rank: ~7 returning atomics per 64 senders on 7 words -- 15.4 ms per slab
 // and round at world 8, against 2.2 ms for the round kernel.)
+//
+// Sweep 2 takes 8 senders per thread at a time: their run slots (LDS atomics),
+// then every slot / payload load of the 8 at once, then the stores.  The loads
+// are buffer loads over the block's senders; a sender without a message loads
+// from past the end of the buffer, which returns 0 and touches no memory -- so
+// no load sits under a branch (the compiler would wait for each in turn) and
+// only senders with a message cost bytes.  The destination buffers' addresses
+// sit in LDS (indexing the kernel arguments by a per-lane rank was a global
+// load per message).
 constexpr int PACK_PER = 32;                     // senders per thread
 constexpr uint32_t PACK_RANGE = 256u * PACK_PER;  // senders per block
 static_assert(XMAXW <= 16, "k_pack keeps a destination rank in 4 bits");
+constexpr int BUF_WORD3 = 0x00020000;             // gfx9 raw buffer: 32-bit data format, no swizzle
+constexpr uint32_t BUF_NONE = 0x80000000u;        // an offset past every buffer's end
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, BUF_WORD3);
+}
 
 __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
-    __shared__ uint32_t cnt[XMAXW], off[XMAXW];
+    __shared__ uint32_t cnt[XMAXW], off[XMAXW], cap[XMAXW];
+    __shared__ uint32_t* oslots[XMAXW];
+    __shared__ double2* ovals[XMAXW];
     __shared__ uint32_t bnd[XMAXW + 1];
     const uint32_t r0 = a.s_lo + blockIdx.x * PACK_RANGE;
     if (r0 >= a.s_hi) return;
-    if (threadIdx.x < XMAXW) cnt[threadIdx.x] = 0u;
+    if (threadIdx.x < XMAXW) {
+        cnt[threadIdx.x] = 0u;
+        if (threadIdx.x < (uint32_t)a.W) {
+            oslots[threadIdx.x] = a.peer[threadIdx.x].slots;
+            ovals[threadIdx.x] = a.peer[threadIdx.x].vals;
+            cap[threadIdx.x] = a.peer[threadIdx.x].cap;
+        }
+    }
     if (threadIdx.x <= (uint32_t)a.W) bnd[threadIdx.x] = a.bounds[threadIdx.x];
     __syncthreads();
     const uint32_t me = (uint32_t)a.me;
@@ -88,17 +112,37 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
         off[threadIdx.x] = n ? atomicAdd(a.peer[threadIdx.x].cnt, n) : 0u;
     }
     __syncthreads();
+    // (uniform values kept in scalar registers: a resource in vector registers costs a
+    // readfirstlane loop around every buffer load)
+    const uint32_t nr = __builtin_amdgcn_readfirstlane(min(PACK_RANGE, a.s_hi - r0));
+    const uint32_t sw0 = __builtin_amdgcn_readfirstlane(a.lo + r0 - a.base);
+    // the entry: the in-edge slot at the destination, or (counts mode) the random edge's target
+    const __amdgpu_buffer_rsrc_t rs_ent = buf_rsrc((a.counts ? a.rnd : a.pos) + r0, nr * 4u);
+    const __amdgpu_buffer_rsrc_t rs_sw = buf_rsrc(a.swn + sw0, a.push ? nr * 16u : 0u);
 #pragma unroll
     for (int g = 0; g < PACK_PER / 8; ++g) {
+        uint32_t d[8], idx[8], ent[8];
+        double2 v[8];
 #pragma unroll
         for (int h = 0; h < 8; ++h) {
-            const uint32_t d = (dst[g] >> (4 * h)) & 15u;
-            if (d == none) continue;
-            const uint32_t li = r0 + (g * 8 + h) * 256u + threadIdx.x;
-            const uint32_t idx = atomicAdd(&off[d], 1u);
-            if (idx < a.peer[d].cap) {
-                a.peer[d].slots[idx] = a.counts ? a.rnd[li] - bnd[d] : a.pos[li];
-                if (a.push) a.peer[d].vals[idx] = a.swn[a.lo + li - a.base];
+            d[h] = (dst[g] >> (4 * h)) & 15u;
+            idx[h] = d[h] != none ? atomicAdd(&off[d[h]], 1u) : 0u;
+        }
+#pragma unroll
+        for (int h = 0; h < 8; ++h) {
+            const uint32_t q = (g * 8 + h) * 256u + threadIdx.x;  // sender r0 + q
+            const bool m = d[h] != none;
+            ent[h] = __builtin_amdgcn_raw_buffer_load_b32(rs_ent, m ? q * 4u : BUF_NONE, 0, 0);
+            const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs_sw, m ? q * 16u : BUF_NONE, 0, 0);
+            v[h] = __builtin_bit_cast(double2, x);
+        }
+#pragma unroll
+        for (int h = 0; h < 8; ++h) {
+            if (d[h] == none) continue;
+            const uint32_t k = d[h];
+            if (idx[h] < cap[k]) {
+                oslots[k][idx[h]] = a.counts ? ent[h] - bnd[k] : ent[h];
+                if (a.push) ovals[k][idx[h]] = v[h];
             } else {
                 atomicOr(a.overflow, 1u);
             }

@@ -587,6 +587,21 @@ int64_t or_population(const or_sim* s) { return s->P; }
 int64_t or_threshold(const or_sim* s) { return s->T; }
 int64_t or_seed_node(const or_sim* s) { return s->seed_node; }
 
+/* CPU-baseline timing only (bench.py cpu_baseline): mark every push-sum node active,
+ * so a round costs what a steady-state round costs (every node sends) without the
+ * activation pre-roll, which at P = 1e9 would take minutes of full-population
+ * passes.  Not an SRS v1 transition -- never used by a parity check.  Returns the
+ * number of nodes it activated, or -1 for gossip. */
+int64_t or_activate_all(or_sim* s) {
+    if (s->alg != OR_PUSHSUM) return -1;
+    int64_t n = 0;
+    for (int64_t i = 0; i < s->P; ++i) {
+        n += !s->active[i];
+        s->active[i] = 1;
+    }
+    return n;
+}
+
 int64_t or_active_count(const or_sim* s) {
     int64_t a = 0;
     for (int64_t i = 0; i < s->P; ++i) {

@@ -57,6 +57,8 @@ int64_t or_population(const or_sim* s);
 int64_t or_threshold(const or_sim* s);
 int64_t or_seed_node(const or_sim* s);
 int64_t or_active_count(const or_sim* s);
+/* bench.py cpu_baseline timing only: every push-sum node active (not an SRS v1 transition) */
+int64_t or_activate_all(or_sim* s);
 /* neighbour list of node i in reference slot order; returns degree.
  * out may be NULL (degree only). */
 int or_neighbors(const or_sim* s, int64_t i, int64_t* out);

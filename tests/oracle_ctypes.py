@@ -34,7 +34,7 @@ def lib():
         L.or_step.restype = i64
         L.or_step.argtypes = [vp, i64, C.POINTER(i64)]
         for f in ("or_rounds_done", "or_alerts_total", "or_population", "or_threshold",
-                  "or_seed_node", "or_active_count"):
+                  "or_seed_node", "or_active_count", "or_activate_all"):
             getattr(L, f).restype = i64
             getattr(L, f).argtypes = [vp]
         L.or_neighbors.restype = i32
@@ -132,6 +132,11 @@ class Oracle:
 
     def active_count(self):
         return lib().or_active_count(self._h)
+
+    def activate_all(self):
+        """bench.py cpu_baseline timing only: every push-sum node active (skips the
+        activation pre-roll; not an SRS v1 transition)."""
+        return lib().or_activate_all(self._h)
 
     def neighbors(self, i):
         d = lib().or_neighbors(self._h, i, None)

@@ -178,3 +178,21 @@ def test_pushsum_receivers_matches_whole_network_round(n, topo, seed, warms):
         np.testing.assert_array_equal(fo, nx["flags"][ids])
         assert conv == int(np.count_nonzero((nx["flags"][ids] & 2) & ~(st["flags"][ids] & 2)))
     orc.close()
+
+
+def test_activate_all_is_a_steady_state_round():
+    """Oracle.activate_all (bench.py's CPU-baseline sample only): every node active, and
+    a round after it sends from every node and conserves the mass, like any round."""
+    from tests.oracle_ctypes import Oracle
+    orc = Oracle(27000, "Imp3D", "push-sum", 1, threads=1)
+    P = orc.P
+    assert orc.activate_all() == P - 1  # the seed was already active
+    assert orc.active_count() == P
+    st0 = orc.state()
+    orc.step(1)
+    st1 = orc.state()
+    assert abs(st1["s"].sum() - st0["s"].sum()) <= 1e-9 * abs(st0["s"].sum())
+    assert abs(st1["w"].sum() - P) <= 1e-9 * P
+    assert (st1["w"] != 1.0).sum() > P // 2  # every node halved and/or received
+    orc.close()
+    assert Oracle(1000, "line", "gossip", 1).activate_all() == -1
