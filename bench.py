@@ -119,11 +119,14 @@ def cpu_baseline(args):
                 break
         pre = f"after a {orc.rounds}-round activation pre-roll"
     t_setup = time.perf_counter() - t0
+    log(f"[bench] cpu baseline: oracle P={P} ready ({t_setup:.1f} s, {threads} threads)")
     rounds, t = 0, 0.0
     while (t < args.cpu_seconds or rounds == 0) and rounds < 400:
         t1 = time.perf_counter()
         rounds += len(orc.step(1 if direct else 2))
         t += time.perf_counter() - t1
+        if direct:
+            log(f"[bench] cpu baseline: {rounds} round(s), {t:.1f} s")
     orc.close()
     return {
         "value": P * rounds / t,
