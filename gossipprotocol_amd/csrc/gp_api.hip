@@ -317,6 +317,11 @@ int alloc_slab(gp_sim* s, Slab& sl, int r) {
         S.fb_nb2 = fp.nb2;
         S.fb_cap1 = fp.cap1;
         S.fb_cap2 = fp.cap2;
+        // one rank: the fold of round r bins round r+1's messages (k_fb_fold<true>)
+        S.fb_fused = s->world == 1 && fp.nb1 <= full_bin_fused_max_bins() ? 1u : 0u;
+#ifdef GP_EXPERIMENTS
+        if (const char* e = std::getenv("GP_FB_FUSED")) S.fb_fused = S.fb_fused && e[0] == '1';  // A/B: 3 passes
+#endif
         const size_t m1 = (size_t)fp.nb1 * fp.cap1, m2 = (size_t)fp.nb2 * fp.cap2;
         if ((rc = dev_alloc_t(s, &S.fb_cnt1, fp.nb1)) || (rc = dev_alloc_t(s, &S.fb_cnt2, fp.nb2)) ||
             (rc = dev_alloc_t(s, &S.fb_hdr1, m1)) || (rc = dev_alloc_t(s, &S.fb_pay1, m1)) ||
@@ -925,7 +930,9 @@ double alg_bytes(const gp_sim* s) {
         if (S.topo != FULL) return 34.0;
         // send: byte 1 (sweep 1) + byte 1 + own (s, w) 16 + message write 20; split: sender
         // id 4 (sweep 1) + message r+w 40; fold: message 20 + own (s, w) r+w 32 + byte r+w 2
-        // (gp_fullbin.hip, range binning)
+        // (gp_fullbin.hip, range binning).  One rank: the fold writes the next round's
+        // messages from the state it just computed, so the send's reads (18) go.
+        if (S.fb_fused) return 20.0 + 4.0 + 40.0 + 20.0 + 32.0 + 2.0;
         return 1.0 + 1.0 + 16.0 + 20.0 + 4.0 + 40.0 + 20.0 + 32.0 + 2.0;
     }
     // gossip: counter r+w 8, direction byte r+w 2; Imp3D:

@@ -559,16 +559,29 @@ __global__ __launch_bounds__(FBR_THREADS, GP_FBR_MINB) void k_fbm_coarse(FullBin
 #endif
 constexpr int FBF_THREADS = GP_FBF_THREADS;
 
+//
+// SEND (one rank, FullBinArgs::fused): after a tile is folded, its nodes' sends of
+// round r+1 are binned straight from the registers that hold the new state --
+// the active flag and (s, w) the fold just wrote (Program.fs:104-106,125-128 one
+// round on) -- into the coarse bins of A, as k_fb_send would bin them: target
+// from the node's Philox draw for round r+1, {id | s/2, w/2}, LDS bin order
+// (reusing the fold's arrays), one reservation per (tile, bin), coalesced runs.
+// The next round then starts at B: no send pass re-reads the state (18 B/node).
+constexpr uint32_t FBF_MAXB1 = 1024;  // coarse bins the fused send can bin into (LDS reservation slots)
+
+template <bool SEND>
 __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t r) {
     constexpr int TILE = 1 << FB_TB;
     constexpr int NPT = TILE / FBF_THREADS;
     constexpr int FQ = (FB_CAP2 + FBF_THREADS - 1) / FBF_THREADS;
+    static_assert(TILE <= FB_CAP2 && FBF_MAXB1 <= TILE, "the fused send reuses msg / src / idx / cnt");
     __shared__ uint32_t cnt[TILE + 1];            // per receiver: count, then start
     __shared__ double2 msg[FB_CAP2];              // payloads in receiver order
     __shared__ uint32_t src[FB_CAP2];             // sender ids in receiver order, sorted per receiver
     __shared__ uint16_t idx[FB_CAP2];             // the message's slot in msg, permuted with src
     __shared__ uint32_t tmp[FBF_THREADS / 64];
     __shared__ uint32_t red[2][FBF_THREADS / 64];
+    __shared__ uint32_t sbase[SEND ? FBF_MAXB1 : 1];  // fused send: the tile's run start per coarse bin
     Ctl* ctl = a.ctl;
     if (ld_agent(&ctl->done)) return;
     const uint32_t P = a.P;
@@ -586,6 +599,8 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
         double ps[FQ], pw[FQ];  // (two scalar arrays: a double2 array here went to scratch)
         uint8_t bk[NPT];
         double2 svk[NPT];
+        uint32_t nfl[NPT];  // fused send: active in round r+1, and the half it sends
+        double2 nsw[NPT];
 #pragma unroll
         for (int k = 0; k < FQ; ++k) {
             const uint32_t q = min((uint32_t)(k * FBF_THREADS + threadIdx.x), n > 0 ? n - 1 : 0u);
@@ -666,10 +681,63 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
                 nbp[j] = (uint8_t)flags;
             }
             if (j < a.nloc) swn[j] = make_double2(acc_s, acc_w);
+            if (SEND) {
+                nfl[k] = j < a.nloc && P > 1 && (b & B_ACTIVE || p1 > p0) ? 1u : 0u;  // active next round
+                nsw[k] = make_double2(acc_s * 0.5, acc_w * 0.5);
+            }
         }
         __syncthreads();
         for (uint32_t v = threadIdx.x; v < TILE; v += FBF_THREADS) cnt[v] = 0u;
         __syncthreads();
+        if (SEND) {
+            // round r+1: coarse bin of every active node's target, LDS rank per bin
+            uint32_t node[NPT], xs[NPT], ys[NPT], key[NPT], rank[NPT];
+#pragma unroll
+            for (int k = 0; k < NPT; ++k) node[k] = a.lo + f * TILE + k * FBF_THREADS + threadIdx.x;
+            philox2_batch<NPT>(node, r + 1, S_PUSHSUM, a.k0, a.k1, xs, ys);
+#pragma unroll
+            for (int k = 0; k < NPT; ++k) {
+                key[k] = FB_NONE;
+                rank[k] = 0u;
+                if (nfl[k]) {
+                    key[k] = full_target(node[k], uniform_from(xs[k], ys[k], P - 1)) >> a.s1;
+                    rank[k] = atomicAdd(&cnt[key[k]], 1u);
+                }
+            }
+            __syncthreads();
+            const uint32_t total = lds_excl_scan<FBF_THREADS>(cnt, a.nb1, tmp);  // count -> first LDS position
+            for (uint32_t q = threadIdx.x; q < a.nb1; q += FBF_THREADS) {  // one reservation per (tile, bin)
+                const uint32_t n = (q + 1 < a.nb1 ? cnt[q + 1] : total) - cnt[q];
+                sbase[q] = n ? atomicAdd(&a.cnt1[q], n) : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < NPT; ++k) {
+                if (key[k] == FB_NONE) continue;
+                const uint32_t p = cnt[key[k]] + rank[k];
+                src[p] = node[k];
+                msg[p] = nsw[k];
+                idx[p] = (uint16_t)key[k];
+            }
+            __syncthreads();
+            // write-out in bin order: consecutive threads, consecutive slots of one run
+#pragma unroll
+            for (int k = 0; k < NPT; ++k) {
+                const uint32_t p = k * FBF_THREADS + threadIdx.x;
+                if (p >= total) break;
+                const uint32_t q = idx[p];
+                const uint32_t slot = sbase[q] + (p - cnt[q]);
+                if (slot < a.cap1) {
+                    const size_t o = (size_t)q * a.cap1 + slot;
+                    a.hdr1[o] = src[p];
+                    a.pay1[o] = msg[p];
+                } else {
+                    atomicOr(a.overflow, 1u);
+                }
+            }
+            __syncthreads();
+            for (uint32_t v = threadIdx.x; v < a.nb1; v += FBF_THREADS) cnt[v] = 0u;
+            __syncthreads();
+        }
     }
     uint32_t x = alerts, y = newly;
 #pragma unroll
@@ -747,22 +815,36 @@ hipError_t launch_full_bin_split_fold(const FullBinArgs& a, uint32_t round, int 
     const uint32_t items_b = split_items(a);
     hipLaunchKernelGGL(k_fb_split, dim3(items_b), dim3(FBR_THREADS), 2 * sizeof(uint32_t) * (1u << (a.s1 - FB_TB)), st,
                        a, round);
-    hipLaunchKernelGGL(k_fb_fold, dim3(std::min<uint32_t>(a.nb2, (uint32_t)grid * 256 / FBF_THREADS)),
+    hipLaunchKernelGGL(k_fb_fold<false>, dim3(std::min<uint32_t>(a.nb2, (uint32_t)grid * 256 / FBF_THREADS)),
                        dim3(FBF_THREADS), 0, st, a, round);
     return hipGetLastError();
 }
 
+uint32_t full_bin_fused_max_bins() {
+    return FBF_MAXB1;
+}
+
+// One rank.  Three passes (A send, B split, C fold); fused (a.fused): round 0
+// runs A, every fold bins the next round's messages, so a round is B + C.  The
+// coarse-bin counters are cleared once B has read them, before C refills them.
 hipError_t launch_full_bin_round(const FullBinArgs& a, uint32_t round, int grid, hipStream_t st) {
     hipError_t e;
-    if ((e = hipMemsetAsync(a.cnt1, 0, sizeof(uint32_t) * a.nb1, st)) != hipSuccess) return e;
+    if (!a.fused || round == 0) {
+        if ((e = hipMemsetAsync(a.cnt1, 0, sizeof(uint32_t) * a.nb1, st)) != hipSuccess) return e;
+        const uint32_t items_a = (uint32_t)(((uint64_t)a.P + FBR_ITEM - 1) / FBR_ITEM);
+        hipLaunchKernelGGL(k_fb_send, dim3(items_a), dim3(FBR_THREADS), 2 * sizeof(uint32_t) * a.nb1, st, a, round);
+    }
     if ((e = hipMemsetAsync(a.cnt2, 0, sizeof(uint32_t) * a.nb2, st)) != hipSuccess) return e;
-    const uint32_t items_a = (uint32_t)(((uint64_t)a.P + FBR_ITEM - 1) / FBR_ITEM);
-    hipLaunchKernelGGL(k_fb_send, dim3(items_a), dim3(FBR_THREADS), 2 * sizeof(uint32_t) * a.nb1, st, a, round);
     const uint32_t items_b = split_items(a);
     hipLaunchKernelGGL(k_fb_split, dim3(items_b), dim3(FBR_THREADS), 2 * sizeof(uint32_t) * (1u << (a.s1 - FB_TB)), st,
                        a, round);
-    hipLaunchKernelGGL(k_fb_fold, dim3(std::min<uint32_t>(a.nb2, (uint32_t)grid * 256 / FBF_THREADS)),
-                       dim3(FBF_THREADS), 0, st, a, round);
+    const dim3 gc(std::min<uint32_t>(a.nb2, (uint32_t)grid * 256 / FBF_THREADS));
+    if (a.fused) {
+        if ((e = hipMemsetAsync(a.cnt1, 0, sizeof(uint32_t) * a.nb1, st)) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_fb_fold<true>, gc, dim3(FBF_THREADS), 0, st, a, round);
+    } else {
+        hipLaunchKernelGGL(k_fb_fold<false>, gc, dim3(FBF_THREADS), 0, st, a, round);
+    }
     return hipGetLastError();
 }
 

@@ -40,6 +40,7 @@ struct FullBinArgs {
     // from lo
     uint32_t lo, nloc;
     uint32_t s_lo, s_hi;  // several ranks: k_fbm_send bins the senders lo + [s_lo, s_hi) (a half of the slab)
+    uint32_t fused;       // one rank: k_fb_fold<true> also bins the next round's messages into hdr1 / pay1
     // several ranks (k_fbm_send / k_fbm_coarse): senders' messages binned by
     // destination rank into the exchange buffers, then the received ones by coarse bin
     int W, me;
@@ -60,5 +61,6 @@ hipError_t launch_full_bin_recv_reset(const FullBinArgs& a, hipStream_t st);
 hipError_t launch_full_bin_coarse(const FullBinArgs& a, uint32_t round, hipStream_t st);
 hipError_t launch_full_bin_split_fold(const FullBinArgs& a, uint32_t round, int grid, hipStream_t st);
 uint32_t full_bin_item_messages();
+uint32_t full_bin_fused_max_bins();  // coarse bins the fused fold can bin into
 
 }  // namespace gp

@@ -165,6 +165,7 @@ struct DevState {
     int32_t* inc;          // gossip deliveries per node
     // push-sum, one rank: two-level LDS binning of the round's messages (gp_fullbin.hip)
     uint32_t fb_s1, fb_nb1, fb_nb2, fb_cap1, fb_cap2;
+    uint32_t fb_fused;  // one rank: the fold bins the next round's messages (no send pass after round 0)
     uint32_t *fb_cnt1, *fb_cnt2;
     uint32_t *fb_hdr1, *fb_hdr2;  // sender ids
     double2 *fb_pay1, *fb_pay2;

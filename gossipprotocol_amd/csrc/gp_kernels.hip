@@ -400,6 +400,7 @@ const char* bulk_kernel_name(const DevState& S) {
                                     "k_gossip_tile<IMP3D>"},
                                    {"k_gossip_tile<LINE>", "k_full_gossip_send+recv", "k_gossip_col<GRID3D>",
                                     "k_gossip_col<IMP3D>"}};
+    if (S.topo == FULL && S.alg == PUSHSUM && S.fb_fused) return "k_fb_split+fold<send>";  // one rank, fused
     const int v = S.kernel == KERNEL_COL ? 1 : 0;
     if (v == 0 && S.tile_wide && S.topo != FULL) {  // the 1024-thread size class (gp_round_wide.hip)
         static const char* w[2][4] = {{"wide::k_gossip_tile<LINE>", "", "wide::k_gossip_tile<GRID3D>",
@@ -482,6 +483,7 @@ hipError_t launch_full_pushsum_round(const DevState& S, uint32_t round, int grid
     a.lo = S.lo;      // one rank: 0
     a.nloc = S.nloc;  // one rank: P
     a.W = 1;
+    a.fused = S.fb_fused;
     return launch_full_bin_round(a, round, grid, st);
 }
 }  // namespace gp

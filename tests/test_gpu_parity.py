@@ -95,9 +95,12 @@ def test_live_parity(n, topo, alg, seed, rounds, chk):
 @pytest.mark.parametrize("n", [1, 2, 3, 1023, 1024, 4095, 4096, 16383, 16384, 65535, 65536, 131071])
 def test_full_pushsum_boundary_sizes(n):
     """Full push-sum (range binning, gp_fullbin.hip) at populations P = n + 1 on and
-    around its chunk (4096), work-item (16384 senders) and fine-tile (1024) sizes:
-    bit-exact state every 25 rounds through convergence."""
+    around its chunk (4096 messages), work-item (16384 senders) and fine-tile (4096
+    receivers) sizes: bit-exact state every 25 rounds through convergence.  One rank
+    runs the fused form: round 0's send pass, then every fold bins the next round's
+    messages (k_fb_fold<true>)."""
     sim, orc = Sim(n, "full", "push-sum", seed=n + 3), Oracle(n, "full", "push-sum", n + 3)
+    assert sim.kernel_stats()[2] == "k_fb_split+fold<send>"
     done = 0
     while done < 400:
         ga, oa = sim.step(25), orc.step(25)
@@ -107,6 +110,23 @@ def test_full_pushsum_boundary_sizes(n):
         if len(ga) < 25:
             break
     assert sim.rounds == orc.rounds and sim.alerts_total == orc.alerts_total
+    sim.close()
+
+
+@pytest.mark.parametrize("n,seed", [(4095, 11), (131071, 12), (2000000, 13)])
+def test_full_pushsum_three_pass_parity(n, seed, monkeypatch):
+    """The three-pass full push-sum round (send, split, fold every round; experiments
+    build, GP_FB_FUSED=0) stays bit-exact too: it is the form several ranks run
+    (k_fbm_send bins by destination rank), and the A/B reference for the fused one."""
+    monkeypatch.setenv("GP_FB_FUSED", "0")
+    sim, orc = Sim(n, "full", "push-sum", seed=seed, experimental=True), Oracle(n, "full", "push-sum", seed)
+    assert sim.kernel_stats()[2] == "k_fb_send+split+fold"
+    for _ in range(4):
+        ga, oa = sim.step(30), orc.step(30)
+        assert ga == oa
+        assert_same_state("push-sum", sim.state(), orc.state())
+        if len(ga) < 30:
+            break
     sim.close()
 
 

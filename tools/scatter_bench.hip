@@ -8,8 +8,11 @@
 //   s32        the same messages in 32-B slots, each write a whole aligned
 //              32-B sector (16 B of payload + 16 B of padding, two lanes)
 //   s32one     the same 32-B slots, but only the 16 payload bytes written
-//   s16sorted  16-B writes, slots ascending in runs of 4096 (a pack that
-//              bins messages by slot range)
+//   s16sorted  16-B writes, slots ascending in runs of 4096
+//   s16grpG    16-B writes, messages grouped by slot range (G groups of the
+//              array, random order inside a group; a pack that bins messages
+//              by destination range), groups in order
+//   s16full    16-B writes, all slots ascending
 //   r16 / r32  reading the used slots back by gather (the round kernel's
 //              remote in-edge reads), 16-B vs 32-B slot stride
 // Build: hipcc --offload-arch=gfx950 -O3 -o build/scatter_bench tools/scatter_bench.hip
@@ -87,13 +90,16 @@ int main(int argc, char** argv) {
     const int grid = 8192;
     double2 *a, *fl;
     double* dout;
-    uint32_t *slot, *sorted;
+    uint32_t *slot, *sorted, *grp64, *grp512, *full;
     CK(hipMalloc(&a, (size_t)NS * 32));
     const size_t NF = (size_t)1 << 26;  // 1 GiB flush buffer
     CK(hipMalloc(&fl, NF * 16));
     CK(hipMalloc(&dout, 256));
     CK(hipMalloc(&slot, (size_t)M * 4));
     CK(hipMalloc(&sorted, (size_t)M * 4));
+    CK(hipMalloc(&grp64, (size_t)M * 4));
+    CK(hipMalloc(&grp512, (size_t)M * 4));
+    CK(hipMalloc(&full, (size_t)M * 4));
     CK(hipMemset(a, 0, (size_t)NS * 32));
     // M distinct uniform slots (a random subset), in random order; and the same sorted in runs of 4096
     std::vector<uint32_t> h(M);
@@ -111,6 +117,17 @@ int main(int argc, char** argv) {
         }
     }
     CK(hipMemcpy(slot, h.data(), (size_t)M * 4, hipMemcpyHostToDevice));
+    {  // grouped by slot range, random order inside a group (stable partition of the random order)
+        for (int G : {64, 512}) {
+            std::vector<uint32_t> g2(h);
+            const uint64_t span = ((uint64_t)NS + G - 1) / G;
+            std::stable_sort(g2.begin(), g2.end(), [&](uint32_t x, uint32_t y) { return x / span < y / span; });
+            CK(hipMemcpy(G == 64 ? grp64 : grp512, g2.data(), (size_t)M * 4, hipMemcpyHostToDevice));
+        }
+        std::vector<uint32_t> f(h);
+        std::sort(f.begin(), f.end());
+        CK(hipMemcpy(full, f.data(), (size_t)M * 4, hipMemcpyHostToDevice));
+    }
     for (uint32_t k = 0; k < M; k += 4096) std::sort(h.begin() + k, h.begin() + std::min<uint32_t>(M, k + 4096));
     CK(hipMemcpy(sorted, h.data(), (size_t)M * 4, hipMemcpyHostToDevice));
     CK(hipDeviceSynchronize());
@@ -130,6 +147,15 @@ int main(int argc, char** argv) {
         flush();
         t = timeit([&] { hipLaunchKernelGGL(k_s16, dim3(grid), dim3(TPB), 0, 0, a, sorted, M); });
         std::printf("s16sorted  %.3f ms  %.1f M/ms\n", t, M / t / 1e6);
+        flush();
+        t = timeit([&] { hipLaunchKernelGGL(k_s16, dim3(grid), dim3(TPB), 0, 0, a, grp64, M); });
+        std::printf("s16grp64   %.3f ms  %.1f M/ms\n", t, M / t / 1e6);
+        flush();
+        t = timeit([&] { hipLaunchKernelGGL(k_s16, dim3(grid), dim3(TPB), 0, 0, a, grp512, M); });
+        std::printf("s16grp512  %.3f ms  %.1f M/ms\n", t, M / t / 1e6);
+        flush();
+        t = timeit([&] { hipLaunchKernelGGL(k_s16, dim3(grid), dim3(TPB), 0, 0, a, full, M); });
+        std::printf("s16full    %.3f ms  %.1f M/ms\n", t, M / t / 1e6);
         flush();
         t = timeit([&] { hipLaunchKernelGGL(k_s32, dim3(grid), dim3(TPB), 0, 0, a, sorted, M); });
         std::printf("s32sorted  %.3f ms  %.1f M/ms\n", t, M / t / 1e6);
