@@ -622,8 +622,8 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
             vr[k] = (full_target(snd[k], uniform_from(x[k], y[k], P - 1)) - a.lo) & (TILE - 1);
             rk[k] = q < n ? atomicAdd(&cnt[vr[k]], 1u) : 0u;
         }
-        __syncthreads();
-        lds_excl_scan<FBF_THREADS>(cnt, TILE, tmp);
+        lds_barrier();
+        lds_excl_scan<FBF_THREADS, true>(cnt, TILE, tmp);
         if (threadIdx.x == 0) cnt[TILE] = n;
 #pragma unroll
         for (int k = 0; k < FQ; ++k) {
@@ -634,7 +634,7 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
                 idx[p] = (uint16_t)p;
             }
         }
-        __syncthreads();
+        lds_barrier();
 #pragma unroll
         for (int k = 0; k < NPT; ++k) {
             const uint32_t v = k * FBF_THREADS + threadIdx.x;
@@ -686,9 +686,9 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
                 nsw[k] = make_double2(acc_s * 0.5, acc_w * 0.5);
             }
         }
-        __syncthreads();
+        lds_barrier();
         for (uint32_t v = threadIdx.x; v < TILE; v += FBF_THREADS) cnt[v] = 0u;
-        __syncthreads();
+        lds_barrier();
         if (SEND) {
             // round r+1: coarse bin of every active node's target, LDS rank per bin
             uint32_t node[NPT], xs[NPT], ys[NPT], key[NPT], rank[NPT];
@@ -704,8 +704,8 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
                     rank[k] = atomicAdd(&cnt[key[k]], 1u);
                 }
             }
-            __syncthreads();
-            const uint32_t total = lds_excl_scan<FBF_THREADS>(cnt, a.nb1, tmp);  // count -> first LDS position
+            lds_barrier();
+            const uint32_t total = lds_excl_scan<FBF_THREADS, true>(cnt, a.nb1, tmp);  // count -> first LDS position
             for (uint32_t q = threadIdx.x; q < a.nb1; q += FBF_THREADS) {  // one reservation per (tile, bin)
                 const uint32_t n = (q + 1 < a.nb1 ? cnt[q + 1] : total) - cnt[q];
                 sbase[q] = n ? atomicAdd(&a.cnt1[q], n) : 0u;
@@ -718,7 +718,7 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
                 msg[p] = nsw[k];
                 idx[p] = (uint16_t)key[k];
             }
-            __syncthreads();
+            lds_barrier();
             // write-out in bin order: consecutive threads, consecutive slots of one run
 #pragma unroll
             for (int k = 0; k < NPT; ++k) {
@@ -734,9 +734,9 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
                     atomicOr(a.overflow, 1u);
                 }
             }
-            __syncthreads();
+            lds_barrier();
             for (uint32_t v = threadIdx.x; v < a.nb1; v += FBF_THREADS) cnt[v] = 0u;
-            __syncthreads();
+            lds_barrier();
         }
     }
     uint32_t x = alerts, y = newly;
