@@ -311,17 +311,18 @@ int alloc_slab(gp_sim* s, Slab& sl, int r) {
         }
     }
     if (S.topo == FULL && S.alg == PUSHSUM) {  // LDS-binned message staging of this rank's receivers (gp_fullbin.hip)
-        const FullBinPlan fp = full_bin_plan(S.nloc);
+        // one rank: the fold of round r bins round r+1's messages (k_fb_fold<true>)
+        bool fused = s->world == 1;
+#ifdef GP_EXPERIMENTS
+        if (const char* e = std::getenv("GP_FB_FUSED")) fused = fused && e[0] == '1';  // A/B: three passes
+#endif
+        const FullBinPlan fp = full_bin_plan(S.nloc, fused);
         S.fb_s1 = fp.s1;
         S.fb_nb1 = fp.nb1;
         S.fb_nb2 = fp.nb2;
         S.fb_cap1 = fp.cap1;
         S.fb_cap2 = fp.cap2;
-        // one rank: the fold of round r bins round r+1's messages (k_fb_fold<true>)
-        S.fb_fused = s->world == 1 && fp.nb1 <= full_bin_fused_max_bins() ? 1u : 0u;
-#ifdef GP_EXPERIMENTS
-        if (const char* e = std::getenv("GP_FB_FUSED")) S.fb_fused = S.fb_fused && e[0] == '1';  // A/B: 3 passes
-#endif
+        S.fb_fused = fused && fp.nb1 <= full_bin_fused_max_bins() ? 1u : 0u;
         const size_t m1 = (size_t)fp.nb1 * fp.cap1, m2 = (size_t)fp.nb2 * fp.cap2;
         if ((rc = dev_alloc_t(s, &S.fb_cnt1, fp.nb1)) || (rc = dev_alloc_t(s, &S.fb_cnt2, fp.nb2)) ||
             (rc = dev_alloc_t(s, &S.fb_hdr1, m1)) || (rc = dev_alloc_t(s, &S.fb_pay1, m1)) ||

@@ -763,18 +763,22 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
 
 // ---------------------------------------------------------------- host side
 // Bins for the nrecv receivers of a rank (one rank: nrecv = P).
-FullBinPlan full_bin_plan(uint32_t P) {
+FullBinPlan full_bin_plan(uint32_t P, bool fused) {
     FullBinPlan p{};
     uint32_t bits = 1;
     while (bits < 32 && ((uint64_t)1 << bits) < P) ++bits;
     // coarse bins ~ sqrt(P / TILE) so both passes write runs of ~10-20 messages;
-    // at most FB_MAXBINS coarse bins and FB_MAXBINS fine tiles per coarse bin
-    uint32_t s1 = (bits + FB_TB + 1) / 2;
+    // at most FB_MAXBINS coarse bins and FB_MAXBINS fine tiles per coarse bin.  The
+    // fused fold (one rank) takes coarse bins half that size: the split's runs get
+    // longer and the fold's shorter; P = 1e8, same box: rule 3.37, -1 3.26, -2 3.25,
+    // -3 3.38-3.40 ms/round (profiles/r04/c4_fused/s1_sweep.txt)
+    uint32_t s1 = (bits + FB_TB + 1) / 2 - (fused ? 1u : 0u);
 #ifdef GP_EXPERIMENTS
     if (const char* e = std::getenv("GP_FB_S1D")) s1 += (uint32_t)std::atoi(e);  // coarse-bin size sweep
 #endif
     if (s1 < FB_TB) s1 = FB_TB;
     while (((uint64_t)P >> s1) >= FB_MAXBINS) ++s1;
+    while (fused && (((uint64_t)P + (1ull << s1) - 1) >> s1) > FBF_MAXB1) ++s1;
     while (s1 - FB_TB > 12) --s1;
     p.s1 = s1;
     p.nb1 = (uint32_t)(((uint64_t)P + (1ull << s1) - 1) >> s1);

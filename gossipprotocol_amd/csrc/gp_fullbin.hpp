@@ -50,7 +50,7 @@ struct FullBinArgs {
     uint32_t in_item0[XMAXW + 1];  // first k_fbm_coarse work item of each source rank
 };
 
-FullBinPlan full_bin_plan(uint32_t nrecv);
+FullBinPlan full_bin_plan(uint32_t nrecv, bool fused);  // fused: one rank, k_fb_fold<true>
 hipError_t launch_full_bin_round(const FullBinArgs& a, uint32_t round, int grid, hipStream_t st);
 // several ranks: messages of the senders [s_lo, s_hi) into the exchange buffers (before the
 // exchange) ...
