@@ -575,6 +575,7 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
     constexpr int NPT = TILE / FBF_THREADS;
     constexpr int FQ = (FB_CAP2 + FBF_THREADS - 1) / FBF_THREADS;
     static_assert(TILE <= FB_CAP2 && FBF_MAXB1 <= TILE, "the fused send reuses msg / src / idx / cnt");
+    static_assert(!SEND || NPT % 2 == 0, "the fused send packs two coarse bins per word");
     __shared__ uint32_t cnt[TILE + 1];            // per receiver: count, then start
     __shared__ double2 msg[FB_CAP2];              // payloads in receiver order
     __shared__ uint32_t src[FB_CAP2];             // sender ids in receiver order, sorted per receiver
@@ -614,6 +615,21 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
             const uint32_t j = min(f * TILE + k * FBF_THREADS + threadIdx.x, a.nloc - 1);
             bk[k] = nbp[j];
             svk[k] = swc[j];
+        }
+        // fused send: the coarse bin of each of this thread's nodes' round-r+1 targets, drawn
+        // while the tile's loads are in flight (whether the node sends is known after the fold)
+        uint32_t nkey[SEND ? NPT / 2 : 1];
+        if (SEND) {
+            uint32_t node[NPT], xs[NPT], ys[NPT];
+#pragma unroll
+            for (int k = 0; k < NPT; ++k) node[k] = a.lo + f * TILE + k * FBF_THREADS + threadIdx.x;
+            philox2_batch<NPT>(node, r + 1, S_PUSHSUM, a.k0, a.k1, xs, ys);
+#pragma unroll
+            for (int k = 0; k < NPT; k += 2)
+                nkey[k / 2] = (P > 1 ? full_target(node[k], uniform_from(xs[k], ys[k], P - 1)) >> a.s1 : 0u) |
+                              ((P > 1 ? full_target(node[k + 1], uniform_from(xs[k + 1], ys[k + 1], P - 1)) >> a.s1
+                                      : 0u)
+                               << 16);
         }
         philox2_batch<FQ>(snd, r, S_PUSHSUM, a.k0, a.k1, x, y);
 #pragma unroll
@@ -690,25 +706,29 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
         for (uint32_t v = threadIdx.x; v < TILE; v += FBF_THREADS) cnt[v] = 0u;
         lds_barrier();
         if (SEND) {
-            // round r+1: coarse bin of every active node's target, LDS rank per bin
-            uint32_t node[NPT], xs[NPT], ys[NPT], key[NPT], rank[NPT];
-#pragma unroll
-            for (int k = 0; k < NPT; ++k) node[k] = a.lo + f * TILE + k * FBF_THREADS + threadIdx.x;
-            philox2_batch<NPT>(node, r + 1, S_PUSHSUM, a.k0, a.k1, xs, ys);
+            // round r+1: coarse bin of every active node's target (drawn above), LDS rank per bin
+            uint32_t node[NPT], key[NPT], rank[NPT];
 #pragma unroll
             for (int k = 0; k < NPT; ++k) {
+                node[k] = a.lo + f * TILE + k * FBF_THREADS + threadIdx.x;
                 key[k] = FB_NONE;
                 rank[k] = 0u;
                 if (nfl[k]) {
-                    key[k] = full_target(node[k], uniform_from(xs[k], ys[k], P - 1)) >> a.s1;
+                    key[k] = (nkey[k / 2] >> (16 * (k & 1))) & 0xFFFFu;
                     rank[k] = atomicAdd(&cnt[key[k]], 1u);
                 }
             }
             lds_barrier();
             const uint32_t total = lds_excl_scan<FBF_THREADS, true>(cnt, a.nb1, tmp);  // count -> first LDS position
-            for (uint32_t q = threadIdx.x; q < a.nb1; q += FBF_THREADS) {  // one reservation per (tile, bin)
-                const uint32_t n = (q + 1 < a.nb1 ? cnt[q + 1] : total) - cnt[q];
-                sbase[q] = n ? atomicAdd(&a.cnt1[q], n) : 0u;
+            // one reservation per (tile, bin), thread q for bin q (nb1 <= FBF_MAXB1 <= threads);
+            // the returned offset is stored after the LDS scatter, so the atomic's round
+            // trip overlaps it
+            static_assert(FBF_MAXB1 <= FBF_THREADS, "one coarse bin per thread");
+            uint32_t res = 0u;
+            const uint32_t q0 = threadIdx.x;
+            if (q0 < a.nb1) {
+                const uint32_t n = (q0 + 1 < a.nb1 ? cnt[q0 + 1] : total) - cnt[q0];
+                if (n) res = atomicAdd(&a.cnt1[q0], n);
             }
 #pragma unroll
             for (int k = 0; k < NPT; ++k) {
@@ -718,6 +738,7 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
                 msg[p] = nsw[k];
                 idx[p] = (uint16_t)key[k];
             }
+            if (q0 < a.nb1) sbase[q0] = res;
             lds_barrier();
             // write-out in bin order: consecutive threads, consecutive slots of one run
 #pragma unroll
