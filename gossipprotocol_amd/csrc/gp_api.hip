@@ -938,11 +938,12 @@ double alg_bytes(const gp_sim* s) {
     }
     // gossip: counter r+w 8, direction byte r+w 2; Imp3D:
     //   column kernel (counts random-edge sends at their targets a round ahead): rnd 4 +
-    //   delivery count read 4, its zeroing where non-zero and the senders' atomic
-    //   increments (~1/7 of nodes each, 4 B) -> 18 + 8/7 (several ranks: the remote 7/8
-    //   of the increments arrive through k_unpack instead);
+    //   delivery count read (a byte since round 4; was 4 B), its zeroing where non-zero
+    //   and the senders' atomic increments (~1/7 of nodes each, a 4-B word atomic) ->
+    //   15 + 5/7 (4-B counts: 18 + 8/7; several ranks: the remote 7/8 of the increments
+    //   arrive through k_unpack instead);
     //   tile kernel: in-list 8
-    if (S.topo == IMP3D) return S.rq[0] ? 18.0 + 8.0 / 7.0 : 18.0;
+    if (S.topo == IMP3D) return S.rq[0] ? (S.rq8 ? 15.0 + 5.0 / 7.0 : 18.0 + 8.0 / 7.0) : 18.0;
     if (S.topo != FULL) return 10.0;
     return 4.0 + 8.0 + 8.0 + 8.0;  // send: c + atomic RMW; recv: inc r+w, c r+w
 }
