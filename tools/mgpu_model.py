@@ -43,7 +43,9 @@ def run(n, topo, alg, W, rounds):
     import time
 
     from gossipprotocol_amd import Simulation
-    s = Simulation(n, topo, alg, virtual_ranks=W)
+    # the experiments build (GP_* overrides) when asked for, as tools/perf_round.py
+    exp = bool(os.environ.get("GOSSIP_HIP_LIB_EXPERIMENT") or os.environ.get("GP_EXP"))
+    s = Simulation(n, topo, alg, virtual_ranks=W, experimental=exp)
     P = s.population
     pre = 0
     t = time.perf_counter()
