@@ -58,6 +58,15 @@ namespace wide {
 #ifndef GP_ZDPP
 #define GP_ZDPP 1        // push-sum tile kernel: the j+-1 messages from the neighbour lane's registers (DPP)
 #endif
+#ifndef GP_SETPRIO
+// push-sum tile kernel: wave priority raised (s_setprio 2) while a wave issues its memory
+// operations -- each node slot's loads (1), also the in-edge pass's gathers (2), and on
+// through the staging copies (3) -- and dropped for the fold and the direction draws, so
+// waves about to issue loads win the SIMD over waves with ALU work and more loads are in
+// flight.  P = 1e9, same box, alternated (profiles/r04/setprio_ab.txt): 0 13.19-13.68,
+// 1 13.11-13.15, 2 12.94-13.18, 3 12.93-13.15 ms/round
+#define GP_SETPRIO 3
+#endif
 #ifndef GP_NG
 #define GP_NG 1          // push-sum tile kernel: node slots whose loads are in flight together
 #endif
@@ -512,6 +521,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                         if (q < cnt && isrc[m] - a.lo >= a.nloc) sent[m] = a.rtag[e_lo + q] == r;
                     }
                 }
+                if (GP_SETPRIO >= 2) __builtin_amdgcn_s_setprio(2);
 #pragma unroll
                 for (int m = 0; m < FU; ++m) {
                     const unsigned long long bal = __ballot(sent[m]);
@@ -528,6 +538,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                     }
                 }
                 if (threadIdx.x == 0) L.bits[FU * (TPB / 64)] = 0ull;
+                if (GP_SETPRIO == 2) __builtin_amdgcn_s_setprio(0);
             }
         }
         GP_STAMP(t1);
@@ -554,6 +565,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
         if (TOPO == IMP3D) dma_copy<DMA_ONCE>(L.ind, reinterpret_cast<const char*>(a.ind4 + T / 2), TILE / 2);
         GP_STAMP(t2);
         if (dyn && threadIdx.x == 0) L.qn[it & 1] = claim;
+        if (GP_SETPRIO >= 3) __builtin_amdgcn_s_setprio(0);
         __syncthreads();  // staging copies, in-edge bitmap and gathered messages retired
         GP_STAMP(t3);
         // Imp3D: node jl's in-edges are [e_lo + pre(jl), + d(jl)), pre = exclusive
@@ -625,6 +637,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
             static_assert(NPT % NG == 0, "node groups must divide the nodes per thread");
 #pragma unroll
             for (int k0 = 0; k0 < NPT; k0 += NG) {
+                if (GP_SETPRIO) __builtin_amdgcn_s_setprio(2);
                 // phase A: node byte, present mask, lattice senders (from the staged
                 // direction bytes), one gather per direction -- a direction without a
                 // sender reads the zero sentinel swc[ext_hi] (adding +0.0 is exact)
@@ -705,6 +718,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                             m[h][d] = ld_sw(swc + ((from >> d) & 1u ? nbr<TOPO>(j, d, G) : a.ext_hi));
                         }
                 }
+                if (GP_SETPRIO) __builtin_amdgcn_s_setprio(0);
                 // phase B: canonical fold (own half, lattice slots in slot order, random
                 // edges by ascending sender; every message contributes the sender's half),
                 // ratio test, next-round state
