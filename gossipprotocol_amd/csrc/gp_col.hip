@@ -25,6 +25,9 @@
 // gossip column kernel: waves per SIMD (measured 5..7 with the batched step loads,
 // profiles/r02/col_batch/: Imp3D best at 5, 3D at 7); GP_COL_WAVES (experiments)
 // sets one value for both
+#ifndef GP_COL_PRIO
+#define GP_COL_PRIO 0  // experiments: wave priority raised while a column step issues its loads
+#endif
 #ifdef GP_COL_WAVES
 #define GP_COL_MINW(TOPO) GP_COL_WAVES
 #else
@@ -124,6 +127,7 @@ __global__ __launch_bounds__(BULK_THREADS, GP_COL_MINW(TOPO)) void k_gossip_col(
             uint32_t lnn[NR], led[NR], lrc[NR], lrd[NR];
             int32_t cv[NR];
             const bool ledge = (lane == 0 && z > 0) || (lane == 63 && z + 1 < g);
+            if (GP_COL_PRIO) __builtin_amdgcn_s_setprio(2);
 #pragma unroll
             for (int k = 0; k < NR; ++k) {
                 const uint32_t jl = pxb + yo[k];  // yo = 0 on invalid lanes: the plane's first node
@@ -144,6 +148,7 @@ __global__ __launch_bounds__(BULK_THREADS, GP_COL_MINW(TOPO)) void k_gossip_col(
             for (int k = 0; k < NR; ++k)
                 asm volatile("" : "+v"(lnn[k]), "+v"(cv[k]), "+v"(led[k]), "+v"(lrc[k]), "+v"(lrd[k]));
             asm volatile("" : "+v"(hym), "+v"(hyp));
+            if (GP_COL_PRIO) __builtin_amdgcn_s_setprio(0);
             if (!hmv) hym = DIR_NONE;
             if (!hpv) hyp = DIR_NONE;
             // lane - 1's and lane + 1's bytes of plane x (wave_shr:1 / wave_shl:1)

@@ -41,6 +41,13 @@ namespace gp {
 namespace {
 
 constexpr int FB_MAXBINS = 4096;                   // LDS counters of A and B
+#ifndef GP_FB_PRIO
+#define GP_FB_PRIO 0  // experiments: wave priority raised while the fold / split issue their loads and stores
+#endif
+template <int P>
+__device__ __forceinline__ void fb_prio() {
+    if (GP_FB_PRIO) __builtin_amdgcn_s_setprio(P);
+}
 constexpr uint32_t FB_NONE = 0xFFFFu;
 
 
@@ -169,12 +176,14 @@ __device__ __forceinline__ void fbr_emit_to(FbRangeLds& L, uint32_t* cnt, uint32
         base[b] += (b + 1 < nbins ? cnt[b + 1] : total) - cnt[b];
     // fixed trip count: a loop of unknown length would make the compiler wait for
     // every outstanding load (the next chunk's) before entering it
+    fb_prio<2>();
 #pragma unroll
     for (int k = 0; k < FBR_PER; ++k) {
         const uint32_t p = k * FBR_THREADS + threadIdx.x;
         if (p >= total) break;
         store(L.key[p], L.pos[p], L.hdr[p], L.pay[p]);
     }
+    fb_prio<0>();
     lds_barrier();
 }
 
@@ -376,7 +385,9 @@ __global__ __launch_bounds__(FBR_THREADS, GP_FBR_MINB) void k_fb_split(FullBinAr
             key[k] = (keys[m / 2] >> (16 * (m & 1))) & 0xFFFFu;
             rank[k] = key[k] != FB_NONE ? atomicAdd(&cnt[key[k]], 1u) : 0u;
         }
+        fb_prio<2>();
         cur.load(a, ibase, c0 + FBR_CHUNK < q1 ? c0 + FBR_CHUNK : c0, q1);
+        fb_prio<0>();
         lds_barrier();  // ranks counted
         fbr_emit(L, cnt, base, nfine, key, rank, node, pay, a.hdr2, a.pay2, a.cap2, f0, a.nb2, a.overflow);
     }
@@ -602,6 +613,7 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
         double2 svk[NPT];
         uint32_t nfl[NPT];  // fused send: active in round r+1, and the half it sends
         double2 nsw[NPT];
+        fb_prio<2>();
 #pragma unroll
         for (int k = 0; k < FQ; ++k) {
             const uint32_t q = min((uint32_t)(k * FBF_THREADS + threadIdx.x), n > 0 ? n - 1 : 0u);
@@ -616,6 +628,7 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
             bk[k] = nbp[j];
             svk[k] = swc[j];
         }
+        fb_prio<0>();
         // fused send: the coarse bin of each of this thread's nodes' round-r+1 targets, drawn
         // while the tile's loads are in flight (whether the node sends is known after the fold)
         uint32_t nkey[SEND ? NPT / 2 : 1];
@@ -741,6 +754,7 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
             if (q0 < a.nb1) sbase[q0] = res;
             lds_barrier();
             // write-out in bin order: consecutive threads, consecutive slots of one run
+            fb_prio<2>();
 #pragma unroll
             for (int k = 0; k < NPT; ++k) {
                 const uint32_t p = k * FBF_THREADS + threadIdx.x;
@@ -755,6 +769,7 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
                     atomicOr(a.overflow, 1u);
                 }
             }
+            fb_prio<0>();
             lds_barrier();
             for (uint32_t v = threadIdx.x; v < a.nb1; v += FBF_THREADS) cnt[v] = 0u;
             lds_barrier();

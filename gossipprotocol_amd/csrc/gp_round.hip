@@ -67,6 +67,9 @@ namespace wide {
 // 1 13.11-13.15, 2 12.94-13.18, 3 12.93-13.15 ms/round
 #define GP_SETPRIO 3
 #endif
+#ifndef GP_PRIO
+#define GP_PRIO 2        // the raised priority (experiments: 1..3)
+#endif
 #ifndef GP_NG
 #define GP_NG 1          // push-sum tile kernel: node slots whose loads are in flight together
 #endif
@@ -438,6 +441,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
         }
         if constexpr (TOPO == IMP3D) {
             if (staged) {
+                if (GP_SETPRIO >= 4) __builtin_amdgcn_s_setprio(GP_PRIO);
                 // in-edge q = m * TPB + wave * 64 + lane is bit `lane` of bitmap word
                 // m * 4 + wave; its message (if used) lands in slot q
 #pragma unroll
@@ -521,7 +525,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                         if (q < cnt && isrc[m] - a.lo >= a.nloc) sent[m] = a.rtag[e_lo + q] == r;
                     }
                 }
-                if (GP_SETPRIO >= 2) __builtin_amdgcn_s_setprio(2);
+                if (GP_SETPRIO >= 2) __builtin_amdgcn_s_setprio(GP_PRIO);
 #pragma unroll
                 for (int m = 0; m < FU; ++m) {
                     const unsigned long long bal = __ballot(sent[m]);
@@ -637,7 +641,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
             static_assert(NPT % NG == 0, "node groups must divide the nodes per thread");
 #pragma unroll
             for (int k0 = 0; k0 < NPT; k0 += NG) {
-                if (GP_SETPRIO) __builtin_amdgcn_s_setprio(2);
+                if (GP_SETPRIO) __builtin_amdgcn_s_setprio(GP_PRIO);
                 // phase A: node byte, present mask, lattice senders (from the staged
                 // direction bytes), one gather per direction -- a direction without a
                 // sender reads the zero sentinel swc[ext_hi] (adding +0.0 is exact)

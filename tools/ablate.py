@@ -36,9 +36,13 @@ VARIANTS = {  # name -> extra -D flags for gp_round.hip
     "nozdpp": ["-DGP_ZDPP=0"],
     "t512m6": ["-DGP_TPB=512", "-DGP_NPT=2", "-DGP_MINB=6"],
     "t1024m8": ["-DGP_TPB=1024", "-DGP_NPT=1", "-DGP_MINB=8"],
+    "prio0": ["-DGP_SETPRIO=0"],
     "prio1": ["-DGP_SETPRIO=1"],
     "prio2": ["-DGP_SETPRIO=2"],
     "prio3": ["-DGP_SETPRIO=3"],
+    "prio4": ["-DGP_SETPRIO=4"],
+    "prio3v1": ["-DGP_SETPRIO=3", "-DGP_PRIO=1"],
+    "prio3v3": ["-DGP_SETPRIO=3", "-DGP_PRIO=3"],
 }
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-DGP_EXPERIMENTS"]
 
