@@ -59,16 +59,18 @@ namespace wide {
 #define GP_ZDPP 1        // push-sum tile kernel: the j+-1 messages from the neighbour lane's registers (DPP)
 #endif
 #ifndef GP_SETPRIO
-// push-sum tile kernel: wave priority raised (s_setprio 2) while a wave issues its memory
+// push-sum tile kernel: wave priority raised (s_setprio GP_PRIO) while a wave issues its memory
 // operations -- each node slot's loads (1), also the in-edge pass's gathers (2), and on
 // through the staging copies (3) -- and dropped for the fold and the direction draws, so
 // waves about to issue loads win the SIMD over waves with ALU work and more loads are in
 // flight.  P = 1e9, same box, alternated (profiles/r04/setprio_ab.txt): 0 13.19-13.68,
-// 1 13.11-13.15, 2 12.94-13.18, 3 12.93-13.15 ms/round
+// 1 13.11-13.15, 2 12.94-13.18, 3 12.93-13.15 ms/round; on another box 0 13.34-13.45,
+// 3 13.08-13.26, 3 with priority 1 13.10-13.15, with 3 13.24-13.29, raised from the
+// in-edge pass's start (4) 13.18-13.30
 #define GP_SETPRIO 3
 #endif
 #ifndef GP_PRIO
-#define GP_PRIO 2        // the raised priority (experiments: 1..3)
+#define GP_PRIO 1        // the raised priority (experiments: 1..3)
 #endif
 #ifndef GP_NG
 #define GP_NG 1          // push-sum tile kernel: node slots whose loads are in flight together
