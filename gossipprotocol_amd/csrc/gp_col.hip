@@ -26,7 +26,10 @@
 // profiles/r02/col_batch/: Imp3D best at 5, 3D at 7); GP_COL_WAVES (experiments)
 // sets one value for both
 #ifndef GP_COL_PRIO
-#define GP_COL_PRIO 0  // experiments: wave priority raised while a column step issues its loads
+// wave priority raised (s_setprio 2) while a column step issues its loads, dropped for the
+// step's ALU work (as the push-sum tile kernel, gp_round.hip GP_SETPRIO).  C3, same box,
+// alternated: 0.596-0.603 -> 0.589-0.590 ms/round (profiles/r04/setprio_c3c4.txt)
+#define GP_COL_PRIO 1
 #endif
 #ifdef GP_COL_WAVES
 #define GP_COL_MINW(TOPO) GP_COL_WAVES

@@ -43,6 +43,8 @@ namespace {
 constexpr int FB_MAXBINS = 4096;                   // LDS counters of A and B
 #ifndef GP_FB_PRIO
 #define GP_FB_PRIO 0  // experiments: wave priority raised while the fold / split issue their loads and stores
+                      // (C4, same box: 3.17-3.18 vs 3.03-3.17 ms/round without; not adopted,
+                      // profiles/r04/setprio_c3c4.txt)
 #endif
 template <int P>
 __device__ __forceinline__ void fb_prio() {
