@@ -51,6 +51,14 @@ __device__ __forceinline__ uint32_t owner_of(uint32_t t, const uint32_t* bounds,
 // only senders with a message cost bytes.  The destination buffers' addresses
 // sit in LDS (indexing the kernel arguments by a per-lane rank was a global
 // load per message).
+#ifndef GP_XCHG_PRIO
+#define GP_XCHG_PRIO 0  // experiments: wave priority raised while k_pack / k_unpack issue their loads
+#endif
+template <int P>
+__device__ __forceinline__ void xchg_prio() {
+    if (GP_XCHG_PRIO) __builtin_amdgcn_s_setprio(P);
+}
+
 constexpr int PACK_PER = 32;                     // senders per thread
 constexpr uint32_t PACK_RANGE = 256u * PACK_PER;  // senders per block
 static_assert(XMAXW <= 16, "k_pack keeps a destination rank in 4 bits");
@@ -87,12 +95,14 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
 #pragma unroll
     for (int g = 0; g < PACK_PER / 8; ++g) {
         uint8_t b[8], t[8];
+        xchg_prio<1>();
 #pragma unroll
         for (int h = 0; h < 8; ++h) {  // unconditional loads (clamped), all in flight
             const uint32_t li = min(r0 + (g * 8 + h) * 256u + threadIdx.x, last);
             b[h] = a.nbn[a.lo + li - a.base];
             t[h] = a.xdst[li];
         }
+        xchg_prio<0>();
         uint32_t w = 0;
 #pragma unroll
         for (int h = 0; h < 8; ++h) {
@@ -128,6 +138,7 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
             d[h] = (dst[g] >> (4 * h)) & 15u;
             idx[h] = d[h] != none ? atomicAdd(&off[d[h]], 1u) : 0u;
         }
+        xchg_prio<1>();
 #pragma unroll
         for (int h = 0; h < 8; ++h) {
             const uint32_t q = (g * 8 + h) * 256u + threadIdx.x;  // sender r0 + q
@@ -136,6 +147,7 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
             const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs_sw, m ? q * 16u : BUF_NONE, 0, 0);
             v[h] = __builtin_bit_cast(double2, x);
         }
+        xchg_prio<0>();
 #pragma unroll
         for (int h = 0; h < 8; ++h) {
             if (d[h] == none) continue;
@@ -169,12 +181,14 @@ __global__ __launch_bounds__(256) void k_unpack(UnpackArgs a, uint32_t round) {
     const bool tags = !a.push || __hip_atomic_load(a.all_active, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
     uint32_t slot[UNP];
     double2 v[UNP];
+    xchg_prio<1>();
 #pragma unroll
     for (int u = 0; u < UNP; ++u) {  // clamped: every load unconditional
         const uint32_t k = min(k0 + u * 256u, n - 1u);
         slot[u] = a.peer[p].slots[k];
         if (a.push) v[u] = a.peer[p].vals[k];
     }
+    xchg_prio<0>();
 #pragma unroll
     for (int u = 0; u < UNP; ++u) {
         if (k0 + u * 256u >= n) break;
