@@ -52,7 +52,10 @@ __device__ __forceinline__ uint32_t owner_of(uint32_t t, const uint32_t* bounds,
 // sit in LDS (indexing the kernel arguments by a per-lane rank was a global
 // load per message).
 #ifndef GP_XCHG_PRIO
-#define GP_XCHG_PRIO 0  // experiments: wave priority raised while k_pack / k_unpack issue their loads
+// wave priority raised (s_setprio 1) while k_pack / k_unpack issue their loads.  C5 at W = 8
+// virtual ranks, same box, alternated: pack 4.97-4.99 -> 4.83 ms and unpack 5.59-5.73 ->
+// 5.36-5.71 ms over the 8 slabs (profiles/r04/setprio_xchg.txt)
+#define GP_XCHG_PRIO 1
 #endif
 template <int P>
 __device__ __forceinline__ void xchg_prio() {
