@@ -1,0 +1,12 @@
+#!/bin/bash
+# Headline kernel with wave priority: two node slots in flight at 4 waves/SIMD (ng2m4) against the
+# product form (base), alternated, same box, P = 1e9.
+export TMPDIR=/tmp
+O=${O:-gpurun_out/r4_ng2}
+mkdir -p $O
+for k in 1 2 3; do
+  for v in base ng2m4; do
+    GOSSIP_HIP_LIB_EXPERIMENT=build/ablate/lib_$v.so timeout -k 10 200 python3 tools/perf_round.py 1000000000 Imp3D push-sum 40 > $O/perf_${v}_$k.log 2>&1 || { tail -5 $O/perf_${v}_$k.log; exit 1; }
+    echo "$v $k: $(grep -o '[0-9.]* ms/round kernel' $O/perf_${v}_$k.log | head -1)"
+  done
+done
