@@ -31,6 +31,9 @@
 // alternated: 0.596-0.603 -> 0.589-0.590 ms/round (profiles/r04/setprio_c3c4.txt)
 #define GP_COL_PRIO 1
 #endif
+#ifndef GP_COL_PRIO_VAL
+#define GP_COL_PRIO_VAL 2
+#endif
 #ifdef GP_COL_WAVES
 #define GP_COL_MINW(TOPO) GP_COL_WAVES
 #else
@@ -130,7 +133,7 @@ __global__ __launch_bounds__(BULK_THREADS, GP_COL_MINW(TOPO)) void k_gossip_col(
             uint32_t lnn[NR], led[NR], lrc[NR], lrd[NR];
             int32_t cv[NR];
             const bool ledge = (lane == 0 && z > 0) || (lane == 63 && z + 1 < g);
-            if (GP_COL_PRIO) __builtin_amdgcn_s_setprio(2);
+            if (GP_COL_PRIO) __builtin_amdgcn_s_setprio(GP_COL_PRIO_VAL);
 #pragma unroll
             for (int k = 0; k < NR; ++k) {
                 const uint32_t jl = pxb + yo[k];  // yo = 0 on invalid lanes: the plane's first node

@@ -48,6 +48,10 @@ constexpr int FB_MAXBINS = 4096;                   // LDS counters of A and B
 #endif
 template <int P>
 __device__ __forceinline__ void fb_prio() {
+    if (GP_FB_PRIO == 1) __builtin_amdgcn_s_setprio(P);
+}
+template <int P>
+__device__ __forceinline__ void fb_prio_fold_loads() {  // GP_FB_PRIO 2: the fold's tile loads only
     if (GP_FB_PRIO) __builtin_amdgcn_s_setprio(P);
 }
 constexpr uint32_t FB_NONE = 0xFFFFu;
@@ -615,7 +619,7 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
         double2 svk[NPT];
         uint32_t nfl[NPT];  // fused send: active in round r+1, and the half it sends
         double2 nsw[NPT];
-        fb_prio<2>();
+        fb_prio_fold_loads<2>();
 #pragma unroll
         for (int k = 0; k < FQ; ++k) {
             const uint32_t q = min((uint32_t)(k * FBF_THREADS + threadIdx.x), n > 0 ? n - 1 : 0u);
@@ -630,7 +634,7 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
             bk[k] = nbp[j];
             svk[k] = swc[j];
         }
-        fb_prio<0>();
+        fb_prio_fold_loads<0>();
         // fused send: the coarse bin of each of this thread's nodes' round-r+1 targets, drawn
         // while the tile's loads are in flight (whether the node sends is known after the fold)
         uint32_t nkey[SEND ? NPT / 2 : 1];
