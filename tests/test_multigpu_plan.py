@@ -13,6 +13,8 @@ pair + 12 sigma + 64) are restated here; the tests check that
 """
 import math
 
+import pytest
+
 import numpy as np
 
 from tests.multirank_emu import DIR_RANDOM, Geometry, S_PUSHSUM, S_TOPO, full_capacity, resolve, slab_bounds, uniform
@@ -95,14 +97,17 @@ def test_c5_imp3d_pushsum_1e9_world8_plan():
     assert 1e5 * W * (W - 1) * GAUSS_12SIGMA_TAIL < 1e-25
 
 
-def full_bin_plan(nrecv):
-    """gp_fullbin.hip full_bin_plan: coarse bins of 2^s1 receivers, fine tiles of 4096."""
+def full_bin_plan(nrecv, fused=False):
+    """gp_fullbin.hip full_bin_plan: coarse bins of 2^s1 receivers, fine tiles of 4096; the
+    fused fold (one rank) takes coarse bins one size smaller, at most 1024 of them."""
     fb_tb, cap2 = 12, 4992
     bits = 1
     while bits < 32 and (1 << bits) < nrecv:
         bits += 1
-    s1 = max((bits + fb_tb + 1) // 2, fb_tb)
+    s1 = max((bits + fb_tb + 1) // 2 - (1 if fused else 0), fb_tb)
     while (nrecv >> s1) >= 4096:
+        s1 += 1
+    while fused and ((nrecv + (1 << s1) - 1) >> s1) > 1024:
         s1 += 1
     while s1 - fb_tb > 12:
         s1 -= 1
@@ -175,3 +180,18 @@ def test_realised_imp3d_counts_stay_below_capacity_world8():
         assert np.all(cnt[off] <= cap[off])
         worst = max(worst, float(np.max((cnt[off] - mu[off]) / np.sqrt(mu[off]))))
     assert worst < 6.0  # realised fluctuations are a few sigma; the capacity allows 12
+
+
+@pytest.mark.parametrize("P", [2, 4097, 10**6, 100000001, 2**31 + 5, 2**32 - 1])
+def test_fused_full_bin_plan_fits(P):
+    """One rank runs the fused fold (k_fb_fold<true>) whenever its coarse bins fit the fold's
+    1024 LDS reservation slots: the plan keeps every population up to 2^32 - 1 inside that,
+    the fine tiles of a coarse bin within the split's 4096 LDS counters, and the bins' total
+    capacity above the population (the 12-sigma slack of gp_fullbin.hip)."""
+    nb1, cap1, nb2, cap2 = full_bin_plan(P, fused=True)
+    assert nb1 <= 1024
+    assert nb1 * cap1 >= P and nb2 * cap2 >= P
+    nb1_rule = full_bin_plan(P)[0]
+    assert nb1 >= nb1_rule  # one size smaller bins (more of them), unless the 1024 cap binds
+    if P == 100000001:
+        assert (nb1, nb1_rule) == (191, 96)
