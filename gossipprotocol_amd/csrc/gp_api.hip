@@ -998,7 +998,11 @@ void choose_kernel(gp_sim* s, int64_t nloc_max, int& kernel, uint32_t& col_xsegs
     // push-sum: the same x-windows claimed from per-XCD counters on exactly the
     // resident grid (walk 3; measured, profiles/r02/walk3.txt)
     if (walk == 2 && kernel == KERNEL_TILE && cfg->algorithm == GP_PUSHSUM) walk = 3;
-    wx = 8;
+    // x-window of 8 planes (walk 2); 16 for walk 3 since round 4, where the wave priority
+    // of the tile kernel moved the optimum: P = 1e9, same box, 8 / 12 / 16 / 24 / 32 planes
+    // 13.34-13.36 / 13.17-13.28 / 13.17-13.22 / 13.22-13.25 / 13.15-13.17 ms/round
+    // (profiles/r04/walk_window_nt.txt)
+    wx = walk == 3 ? 16 : 8;
 #ifdef GP_EXPERIMENTS
     if (const char* e = std::getenv("GP_WALK")) walk = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("GP_WX")) wx = (uint32_t)std::max(1, std::atoi(e));

@@ -72,6 +72,9 @@ namespace wide {
 #ifndef GP_PRIO
 #define GP_PRIO 1        // the raised priority (experiments: 1..3)
 #endif
+#ifndef GP_STEAL
+#define GP_STEAL 0       // experiments: walk 3 blocks take items from other XCDs' queues once theirs is empty
+#endif
 #ifndef GP_NG
 #define GP_NG 1          // push-sum tile kernel: node slots whose loads are in flight together
 #endif
@@ -393,6 +396,12 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
         tw.t = L.qn[0];
         ++it;
     }
+#if GP_STEAL
+    // walk 3: once this XCD's list is exhausted, the block takes items from the other
+    // XCDs' queues in turn (their tiles' lattice lines are in another L2, but only
+    // the round's tail runs this way), so no XCD idles while another has work
+    for (uint32_t victim = 0;;) {
+#endif
     while (tw.t < tw.end) {
         uint32_t ti;
         // walk 3: thread 0 claims the next item now; it is published in LDS at the
@@ -909,6 +918,18 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
         // and its node phase writes L.out only after its staging barrier
         tw.t = t_next;
     }
+#if GP_STEAL
+        if (!dyn || ++victim >= 8u) break;
+        const uint32_t c = (blockIdx.x + victim) & 7u;
+        tw.qc = a.tq + c * TQ_STRIDE;
+        tw.wl = a.wt + a.wo[c];
+        tw.end = a.wo[c + 1] - a.wo[c];
+        if (threadIdx.x == 0) L.qn[it & 1] = atomicAdd(tw.qc, 1u);
+        __syncthreads();
+        tw.t = L.qn[it & 1];
+        ++it;
+    }
+#endif
 #if GP_STAMPS
     if (threadIdx.x == 0)
         for (int q = 0; q < 7; ++q) atomicAdd(&gp_stamp_acc[q], (unsigned long long)ph[q]);
