@@ -73,7 +73,11 @@ namespace wide {
 #define GP_PRIO 1        // the raised priority (experiments: 1..3)
 #endif
 #ifndef GP_STEAL
-#define GP_STEAL 0       // experiments: walk 3 blocks take items from other XCDs' queues once theirs is empty
+// walk 3: a block whose XCD's queue is empty takes items from the other XCDs' queues.  Slabs
+// whose planes do not split evenly over the 8 XCDs (W = 8: 125 planes) and tiles of uneven
+// cost otherwise leave XCDs idle at the round's tail.  P = 1e9, same box, alternated: 12.85-12.87
+// -> 12.75-12.81 ms/round; W = 8 slab 1.714 -> 1.699 ms (profiles/r04/walk_steal.txt)
+#define GP_STEAL 1
 #endif
 #ifndef GP_NG
 #define GP_NG 1          // push-sum tile kernel: node slots whose loads are in flight together
