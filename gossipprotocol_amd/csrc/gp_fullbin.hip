@@ -884,7 +884,11 @@ hipError_t launch_full_bin_round(const FullBinArgs& a, uint32_t round, int grid,
     const uint32_t items_b = split_items(a);
     hipLaunchKernelGGL(k_fb_split, dim3(items_b), dim3(FBR_THREADS), 2 * sizeof(uint32_t) * (1u << (a.s1 - FB_TB)), st,
                        a, round);
-    const dim3 gc(std::min<uint32_t>(a.nb2, (uint32_t)grid * 256 / FBF_THREADS));
+    uint32_t nfold = std::min<uint32_t>(a.nb2, (uint32_t)grid * 256 / FBF_THREADS);
+#ifdef GP_EXPERIMENTS
+    if (const char* e = std::getenv("GP_FOLD_BLOCKS")) nfold = std::max<uint32_t>(1, std::min<uint32_t>(a.nb2, (uint32_t)std::atoi(e)));
+#endif
+    const dim3 gc(nfold);
     if (a.fused) {
         if ((e = hipMemsetAsync(a.cnt1, 0, sizeof(uint32_t) * a.nb1, st)) != hipSuccess) return e;
         hipLaunchKernelGGL(k_fb_fold<true>, gc, dim3(FBF_THREADS), 0, st, a, round);
