@@ -854,6 +854,14 @@ hipError_t launch_full_bin_coarse(const FullBinArgs& a, uint32_t round, hipStrea
     return hipGetLastError();
 }
 
+// C's grid: two blocks per CU's worth (the bulk grid is 64 blocks of 256 threads per CU), each
+// walking ~P / 2^FB_TB / 512 tiles.  P = 1e8, same box: 4096 / 2048 / 1024 / 512 / 256 blocks
+// 3.16-3.18 / 3.145-3.147 / 3.137-3.145 / 3.130-3.138 / 3.143-3.147 ms/round once the GPU is
+// warm, one tile per block 3.28 (profiles/r04/c4_fused/fold_grid.txt)
+static uint32_t fold_blocks(const FullBinArgs& a, int grid) {
+    return std::max<uint32_t>(1, std::min<uint32_t>(a.nb2, (uint32_t)grid * 256 / FBF_THREADS / 8));
+}
+
 // B's grid: every coarse bin's ranges
 static uint32_t split_items(const FullBinArgs& a) { return a.nb1 * ((a.cap1 + FBR_ITEM - 1) / FBR_ITEM); }
 
@@ -861,8 +869,7 @@ hipError_t launch_full_bin_split_fold(const FullBinArgs& a, uint32_t round, int 
     const uint32_t items_b = split_items(a);
     hipLaunchKernelGGL(k_fb_split, dim3(items_b), dim3(FBR_THREADS), 2 * sizeof(uint32_t) * (1u << (a.s1 - FB_TB)), st,
                        a, round);
-    hipLaunchKernelGGL(k_fb_fold<false>, dim3(std::min<uint32_t>(a.nb2, (uint32_t)grid * 256 / FBF_THREADS)),
-                       dim3(FBF_THREADS), 0, st, a, round);
+    hipLaunchKernelGGL(k_fb_fold<false>, dim3(fold_blocks(a, grid)), dim3(FBF_THREADS), 0, st, a, round);
     return hipGetLastError();
 }
 
@@ -884,7 +891,7 @@ hipError_t launch_full_bin_round(const FullBinArgs& a, uint32_t round, int grid,
     const uint32_t items_b = split_items(a);
     hipLaunchKernelGGL(k_fb_split, dim3(items_b), dim3(FBR_THREADS), 2 * sizeof(uint32_t) * (1u << (a.s1 - FB_TB)), st,
                        a, round);
-    uint32_t nfold = std::min<uint32_t>(a.nb2, (uint32_t)grid * 256 / FBF_THREADS);
+    uint32_t nfold = fold_blocks(a, grid);
 #ifdef GP_EXPERIMENTS
     if (const char* e = std::getenv("GP_FOLD_BLOCKS")) nfold = std::max<uint32_t>(1, std::min<uint32_t>(a.nb2, (uint32_t)std::atoi(e)));
 #endif
