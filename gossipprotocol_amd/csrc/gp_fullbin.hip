@@ -854,8 +854,8 @@ hipError_t launch_full_bin_coarse(const FullBinArgs& a, uint32_t round, hipStrea
     return hipGetLastError();
 }
 
-// C's grid: two blocks per CU's worth (the bulk grid is 64 blocks of 256 threads per CU), each
-// walking ~P / 2^FB_TB / 512 tiles.  P = 1e8, same box: 4096 / 2048 / 1024 / 512 / 256 blocks
+// C's grid, one rank: two blocks per CU's worth (the bulk grid is 64 blocks of 256 threads per
+// CU), each walking ~P / 2^FB_TB / 512 tiles.  P = 1e8, same box: 4096 / 2048 / 1024 / 512 / 256 blocks
 // 3.16-3.18 / 3.145-3.147 / 3.137-3.145 / 3.130-3.138 / 3.143-3.147 ms/round once the GPU is
 // warm, one tile per block 3.28 (profiles/r04/c4_fused/fold_grid.txt)
 static uint32_t fold_blocks(const FullBinArgs& a, int grid) {
@@ -869,7 +869,10 @@ hipError_t launch_full_bin_split_fold(const FullBinArgs& a, uint32_t round, int 
     const uint32_t items_b = split_items(a);
     hipLaunchKernelGGL(k_fb_split, dim3(items_b), dim3(FBR_THREADS), 2 * sizeof(uint32_t) * (1u << (a.s1 - FB_TB)), st,
                        a, round);
-    hipLaunchKernelGGL(k_fb_fold<false>, dim3(fold_blocks(a, grid)), dim3(FBF_THREADS), 0, st, a, round);
+    // several ranks: a slab's few tiles (3052 at C4 / W = 8) one per block -- 512 blocks of ~6 tiles
+    // measured 0.246 vs 0.214 ms per slab (profiles/r04/final4/)
+    hipLaunchKernelGGL(k_fb_fold<false>, dim3(std::min<uint32_t>(a.nb2, (uint32_t)grid * 256 / FBF_THREADS)),
+                       dim3(FBF_THREADS), 0, st, a, round);
     return hipGetLastError();
 }
 
