@@ -45,6 +45,7 @@ VARIANTS = {  # name -> extra -D flags for gp_round.hip
     "prio3v3": ["-DGP_SETPRIO=3", "-DGP_PRIO=3"],
     "ng2m4": ["-DGP_NG=2", "-DGP_MINB=4"],
     "steal": ["-DGP_STEAL=1"],
+    "sched0": ["-DGP_SETPRIO=0", "-DGP_STEAL=0"],
     "minb6p": ["-DGP_MINB=6"],
 }
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-DGP_EXPERIMENTS"]
