@@ -865,7 +865,9 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                         }
                         // next-round direction drawn below, one Philox batch for the thread's nodes
                         pend[k >> 1] |= (mask | (active && deg > 0 ? 64u : 0u) | ((flags >> 3) << 7)) << (16 * (k & 1));
+                        if (GP_SETPRIO >= 5) __builtin_amdgcn_s_setprio(GP_PRIO);
                         st_stream(swn + j, make_double2(acc_s, acc_w));
+                        if (GP_SETPRIO >= 5) __builtin_amdgcn_s_setprio(0);
                     }
                 }
             }

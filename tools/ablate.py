@@ -41,6 +41,7 @@ VARIANTS = {  # name -> extra -D flags for gp_round.hip
     "prio2": ["-DGP_SETPRIO=2"],
     "prio3": ["-DGP_SETPRIO=3"],
     "prio4": ["-DGP_SETPRIO=4"],
+    "prio5": ["-DGP_SETPRIO=5"],
     "prio3v1": ["-DGP_SETPRIO=3", "-DGP_PRIO=1"],
     "prio3v3": ["-DGP_SETPRIO=3", "-DGP_PRIO=3"],
     "ng2m4": ["-DGP_NG=2", "-DGP_MINB=4"],
