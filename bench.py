@@ -94,8 +94,11 @@ def cpu_baseline(args):
     does what a steady-state round does, every node sends.  Small samples (--cpu-nodes,
     or a host without memory for ~70 B/node) run the real pre-roll instead."""
     from tests.oracle_ctypes import Oracle
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    threads = min(threads, os.cpu_count() or threads)
+    # every core this process may run on (SURVEY.md §8(d): OpenMP over all host cores), not the
+    # box's OMP_NUM_THREADS (16 on the GPU boxes) -- unless --cpu-threads asks for a count
+    sched = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp_env = os.environ.get("OMP_NUM_THREADS")
+    threads = args.cpu_threads or sched
     n = args.cpu_nodes or args.nodes
     note = ""
     try:
@@ -135,7 +138,9 @@ def cpu_baseline(args):
         "kind": "port",
         "sample": f"SRS v1 C oracle (oracle/srs_oracle.c, OpenMP), {args.topology} {args.algorithm} "
                   f"n={n} (P={P}), {rounds} steady-state round(s) {pre}, {t:.1f} s timed "
-                  f"({t_setup:.1f} s setup untimed){note}",
+                  f"({t_setup:.1f} s setup untimed){note}; {threads} OpenMP threads "
+                  f"({'--cpu-threads' if args.cpu_threads else 'all scheduler cores'}: {sched} available, "
+                  f"OMP_NUM_THREADS={omp_env if omp_env is not None else 'unset'} in the environment)",
     }
 
 
@@ -182,6 +187,8 @@ def main():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-nodes", type=int, default=0, help="CPU-baseline sample size (0: --nodes)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU-baseline OpenMP threads (0: every core in the scheduler affinity mask)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--converge", action="store_true", help="also run a fresh simulation to convergence")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 HBM-traffic passes")

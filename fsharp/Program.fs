@@ -95,6 +95,7 @@ let private launchRanks (argv: string[]) (gpus: int) (rehearsal: bool) =
     // this program again: the apphost, or `dotnet <the assembly>` under dotnet run
     let host = Process.GetCurrentProcess().MainModule.FileName
     let pre = if IO.Path.GetFileNameWithoutExtension host = "dotnet" then [| Environment.GetCommandLineArgs().[0] |] else [||]
+    let nonce = Guid.NewGuid().ToString("N")
     let procs =
         [| for r in 0 .. gpus - 1 ->
                let psi = ProcessStartInfo(host)
@@ -106,6 +107,7 @@ let private launchRanks (argv: string[]) (gpus: int) (rehearsal: bool) =
                psi.Environment.["GOSSIP_RANK"] <- string r
                psi.Environment.["GOSSIP_WORLD"] <- string gpus
                psi.Environment.["GOSSIP_RDV"] <- rdv
+               psi.Environment.["GOSSIP_RDV_NONCE"] <- nonce   // gp_rendezvous_id: this launch's file only
                if rehearsal then
                    psi.Environment.["NCCL_HOSTID"] <- sprintf "gossip-rehearsal-%d-%d" (Process.GetCurrentProcess().Id) r
                    psi.Environment.["NCCL_SOCKET_IFNAME"] <- "lo"

@@ -32,17 +32,32 @@ def main(argv=None):
     if a.gpus < 1:
         print("--gpus / GOSSIP_GPUS must be >= 1", file=sys.stderr)
         return 2
-    if a.gpus > 1 and not os.environ.get("GOSSIP_LAUNCHED"):
+    # ranks started by a launcher: ours (GOSSIP_LAUNCHED) or an external one such as
+    # torch.distributed.run (WORLD_SIZE / RANK in the environment) -- never launch again
+    external = "WORLD_SIZE" in os.environ and not os.environ.get("GOSSIP_LAUNCHED")
+    if external and int(os.environ["WORLD_SIZE"]) != a.gpus:
+        print(f"--gpus {a.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}: refusing to run another GPU count",
+              file=sys.stderr)
+        return 2
+    if a.gpus > 1 and not os.environ.get("GOSSIP_LAUNCHED") and not external:
         from .launch import rehearsal_env, run_ranks
         extra = (lambda r: rehearsal_env(r)) if a.device is not None else None
         return run_ranks([sys.executable, "-m", "gossipprotocol_amd"] + argv, a.gpus, env_for_rank=extra,
                          ok_codes=(0, 3))
     from .sim import Simulation
     rank = int(os.environ.get("RANK", "0")) if a.gpus > 1 else 0
-    device = a.device if a.device is not None else rank
+    local_rank = int(os.environ.get("LOCAL_RANK", str(rank))) if a.gpus > 1 else 0
+    device = a.device if a.device is not None else local_rank
+    dist = None
+    if a.gpus > 1 and not os.environ.get("GOSSIP_RDV"):
+        # external launcher without our rendezvous file: the RCCL id travels through a
+        # gloo group on its MASTER_ADDR / MASTER_PORT (host side only)
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=a.gpus)
     try:
         sim = Simulation(a.num_nodes, a.topology, a.algorithm, seed=a.seed, max_rounds=a.max_rounds,
-                         device=device, rank=rank, world=a.gpus, rendezvous=os.environ.get("GOSSIP_RDV"))
+                         device=device, rank=rank, world=a.gpus, dist=dist,
+                         rendezvous=os.environ.get("GOSSIP_RDV"))
     except L.GossipError as e:
         print(f"[rank {rank}/{a.gpus}] {e}", file=sys.stderr)
         return 2 if e.code == -1 else 1
@@ -50,6 +65,8 @@ def main(argv=None):
         print("Gossip Starts" if a.algorithm == "gossip" else "Push Sum Starts", flush=True)
     res = sim.run()
     sim.close()
+    if dist is not None:
+        dist.destroy_process_group()
     if res.status == L.GP_STATUS_CONVERGED:
         if rank == 0:
             print("Convergence Time: %f ms" % res.elapsed_ms, flush=True)

@@ -130,6 +130,9 @@ int launch(const Args& a) {
     }
     const std::string rdv = dir + "/rccl_id";
     const pid_t launcher = getpid();
+    // this launch's rendezvous nonce (gp_rendezvous_id): the ranks inherit it through fork
+    const std::string nonce = std::to_string((long long)launcher) + "-" + dir.substr(dir.size() - 6);
+    setenv("GOSSIP_RDV_NONCE", nonce.c_str(), 1);
     std::fflush(stdout);
     std::fflush(stderr);
     std::vector<pid_t> pids;

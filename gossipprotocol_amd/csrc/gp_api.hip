@@ -1255,7 +1255,17 @@ int gp_rendezvous_id(int32_t rank, const char* path, int32_t timeout_ms, uint8_t
         return GP_EINVAL;
     }
     const size_t N = 128;
+    // GOSSIP_RDV_NONCE (set by the launchers, one value per launch): rank 0 writes it after
+    // the id and readers accept only a file that carries theirs, so a file a crashed run
+    // left at a caller-chosen path is never read as this run's id
+    const char* nv = std::getenv("GOSSIP_RDV_NONCE");
+    const std::string nonce = nv ? std::string(nv).substr(0, 64) : std::string();
     if (rank == 0) {  // publish: write a private name, then rename (readers never see a partial id)
+        struct stat st;
+        if (::stat(path, &st) == 0) {
+            set_err("gp_rendezvous_id: '%s' already exists (left by an earlier run?); the path must be fresh", path);
+            return GP_ESTATE;
+        }
         int rc = gp_get_unique_id(unique_id);
         if (rc) return rc;
         const std::string tmp = std::string(path) + ".tmp." + std::to_string((long long)getpid());
@@ -1264,7 +1274,9 @@ int gp_rendezvous_id(int32_t rank, const char* path, int32_t timeout_ms, uint8_t
             set_err("gp_rendezvous_id: cannot create '%s': %s", tmp.c_str(), std::strerror(errno));
             return GP_EINVAL;
         }
-        const bool ok = ::write(fd, unique_id, N) == (ssize_t)N && ::fsync(fd) == 0;
+        std::string blob(reinterpret_cast<const char*>(unique_id), N);
+        blob += nonce;
+        const bool ok = ::write(fd, blob.data(), blob.size()) == (ssize_t)blob.size() && ::fsync(fd) == 0;
         ::close(fd);
         if (!ok || ::rename(tmp.c_str(), path) != 0) {
             set_err("gp_rendezvous_id: cannot publish '%s': %s", path, std::strerror(errno));
@@ -1274,18 +1286,27 @@ int gp_rendezvous_id(int32_t rank, const char* path, int32_t timeout_ms, uint8_t
         return GP_OK;
     }
     const auto t0 = std::chrono::steady_clock::now();
-    for (;;) {  // wait for rank 0's file
+    for (;;) {  // wait for rank 0's file (with this launch's nonce)
         const int fd = ::open(path, O_RDONLY | O_CLOEXEC);
         if (fd >= 0) {
-            const ssize_t got = ::read(fd, unique_id, N);
+            char buf[128 + 65];
+            const ssize_t got = ::read(fd, buf, sizeof buf);
             ::close(fd);
-            if (got == (ssize_t)N) return GP_OK;
-            set_err("gp_rendezvous_id: '%s' holds %zd bytes, expected %zu", path, got, N);
-            return GP_EINVAL;
+            if (got < (ssize_t)N) {
+                set_err("gp_rendezvous_id: '%s' holds %zd bytes, expected %zu", path, got, N);
+                return GP_EINVAL;
+            }
+            if (std::string(buf + N, (size_t)got - N) == nonce) {
+                std::memcpy(unique_id, buf, N);
+                return GP_OK;
+            }
+            // another launch's file: keep waiting for ours (rank 0 refuses to overwrite it,
+            // so this ends at the timeout with the error below)
         }
         const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         if (timeout_ms >= 0 && ms >= timeout_ms) {
-            set_err("gp_rendezvous_id: rank %d waited %d ms for rank 0's id at '%s'", rank, timeout_ms, path);
+            set_err("gp_rendezvous_id: rank %d waited %d ms for rank 0's id at '%s'%s", rank, timeout_ms, path,
+                    fd >= 0 ? " (the file there carries another launch's nonce)" : "");
             return GP_ESTATE;
         }
         std::this_thread::sleep_for(std::chrono::milliseconds(5));

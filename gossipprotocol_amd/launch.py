@@ -68,13 +68,14 @@ def run_ranks(cmd, world: int, env_for_rank=None, log=None, poll_s: float = 0.2,
     log = log or (lambda *a: print(*a, file=sys.stderr, flush=True))
     rdv_dir = tempfile.mkdtemp(prefix="gossip_rdv_", dir=os.environ.get("TMPDIR", "/tmp"))
     port = free_port()
+    nonce = os.urandom(8).hex()  # this launch's rendezvous nonce (gp_rendezvous_id)
     procs = []
     failed = None
     try:
         for r in range(world):
             env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
                        MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GOSSIP_RDV=os.path.join(rdv_dir, "rccl_id"),
-                       GOSSIP_LAUNCHED="1")
+                       GOSSIP_RDV_NONCE=nonce, GOSSIP_LAUNCHED="1")
             if env_for_rank is not None:
                 env.update(env_for_rank(r))
             procs.append(subprocess.Popen(cmd, env=env, start_new_session=True))

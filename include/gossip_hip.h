@@ -128,7 +128,11 @@ int gp_create_rank(const gp_config* cfg, int32_t rank, int32_t world, const uint
  * private name, then renamed, so a reader never sees a partial id); every other
  * rank waits for the file (at most timeout_ms; < 0 waits forever) and reads it.
  * Then every rank calls gp_create_rank with the same id.  The launcher removes
- * the file afterwards. */
+ * the file afterwards.  The path must be fresh: rank 0 fails with GP_ESTATE when
+ * a file is already there.  If GOSSIP_RDV_NONCE is set in the environment (the
+ * launchers set one value per launch), rank 0 appends it to the id and readers
+ * accept only a file carrying the same nonce, so a file left at a reused path by
+ * a crashed run is never taken for this run's id. */
 int gp_rendezvous_id(int32_t rank, const char* path, int32_t timeout_ms, uint8_t unique_id[128]);
 
 /* Replaces the message loop Program.fs:84-131,141-163 plus the scheduler

@@ -20,5 +20,5 @@ for rep in 1 2; do
     echo "$v: $(grep -o 'k_[a-z_+<>A-Z0-9]*: [0-9.]* ms/round kernel, wall [0-9.]* ms/round' $O/perf_$v.$rep.log)"
   done
 done
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_inbox -o kt -- env GP_INBOX=1 GP_EXP=1 python3 tools/perf_round.py 1000000000 Imp3D push-sum 10 > $O/kt_inbox.log 2>&1 || { tail -5 $O/kt_inbox.log; exit 1; }
+GP_INBOX=1 GP_EXP=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_inbox -o kt -- python3 tools/perf_round.py 1000000000 Imp3D push-sum 10 > $O/kt_inbox.log 2>&1 || { tail -5 $O/kt_inbox.log; exit 1; }
 python3 tools/kt_steady.py $O/kt_inbox k_ps --last 20

@@ -1,7 +1,7 @@
 """Generate tests/golden/runs_1e8.json: whole runs to convergence at BASELINE.json's
 1e8 sizes, from the C oracle (oracle/srs_oracle.c, OpenMP).
 
-    python tests/golden/make_golden_runs.py [case ...]     # cases: c4 c5_1e8 (default: both)
+    python tests/golden/make_golden_runs.py [case ...]     # cases: c2 c4 c5_1e8 (default: all)
 
 Per case: the per-round alert counts of the whole run (the scheduler's Alert
 stream, Program.fs:51-56, under SRS v1), the convergence round, and an xxh3-128
@@ -13,6 +13,7 @@ per run) inside the GPU suite.  Fixtures of the build's own oracle: the
 reference produces no vectors, so parity with it stays
 "parity unpinned".
 
+C2: push-sum, 3D lattice, n = 1e6 (g = 100, P = 1,000,000), seed 1.
 C4: push-sum, full topology, n = 1e8 (P = 100,000,001), seed 1.
 C5@1e8: push-sum, Imp3D, n = 1e8 (g = 465, P = 100,544,625), seed 1.
 """
@@ -27,7 +28,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 from tests.oracle_ctypes import Oracle  # noqa: E402
 
-CASES = {"c4": (10**8, "full", "push-sum", 1), "c5_1e8": (10**8, "Imp3D", "push-sum", 1)}
+CASES = {"c2": (10**6, "3D", "push-sum", 1), "c4": (10**8, "full", "push-sum", 1), "c5_1e8": (10**8, "Imp3D", "push-sum", 1)}
 OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "runs_1e8.json")
 
 

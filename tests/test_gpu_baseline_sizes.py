@@ -16,8 +16,9 @@ progress while it goes; a failing segment stops the run (-x).
       and then steady-state rounds, i.e. the headline kernel's all-active path
       (sender Philox redraw, compact in-edge messages) at the 1e8 scale.
       The 1e9 size itself is covered by tests/test_gpu_parity.py::
-      test_full_size_imp3d_pushsum_1e9_rounds: four rounds (activation, steady
-      state, the alert peak at round 533, the converged tail at round 700)
+      test_full_size_1e9_* (one shared run, five segments): four checked rounds
+      (activation, steady state, the alert peak at round 533, the converged tail
+      at round 700)
       recomputed by the oracle for ~1.1e6 sampled receivers, bit-exact (a whole
       oracle run at 1e9 would need ~70 GB and ~20 min).
 """
@@ -155,7 +156,7 @@ def test_c4_converged(c4):
 GOLDEN_RUNS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "runs_1e8.json")
 
 
-@pytest.mark.parametrize("case", ["c4", "c5_1e8"])
+@pytest.mark.parametrize("case", ["c2", "c4", "c5_1e8"])
 def test_run_to_convergence_matches_oracle_record(case):
     """The product run to convergence at a BASELINE size reproduces the C oracle's
     recorded run (tests/golden/make_golden_runs.py): every round's alert count

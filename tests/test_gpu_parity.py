@@ -349,11 +349,17 @@ def test_kernel_variant_parity(kernel, n, topo, alg, seed, rounds, chk, xsegs, m
     1024-thread x 1 node build (tile1, GP_WIDE=1, gp_round_wide.hip)."""
     if kernel == "col" and alg == "push-sum":
         pytest.skip("the column march runs lattice gossip only")
+    if kernel == "tile1" and (alg != "push-sum" or topo == "Imp3D"):
+        # GP_WIDE only selects among the line / 3D push-sum size classes (choose_kernel)
+        pytest.skip("the 1024-thread build runs line / 3D push-sum only")
     monkeypatch.setenv("GP_KERNEL", "tile" if kernel.startswith("tile") else kernel)
     if kernel in ("tile4", "tile1"):
         monkeypatch.setenv("GP_WIDE", "1" if kernel == "tile1" else "0")
     monkeypatch.setenv("GP_XSEGS", xsegs)
     sim, orc = Sim(n, topo, alg, seed=seed, experimental=True), Oracle(n, topo, alg, seed)
+    name = sim.kernel_stats()[2]
+    if kernel in ("tile4", "tile1"):  # the size class the case claims to cover really runs
+        assert name.startswith("wide::") == (kernel == "tile1"), name
     done = 0
     while done < rounds:
         k = min(chk, rounds - done)
@@ -441,6 +447,10 @@ def test_tile_unstaged_path_parity(cap, wide, monkeypatch):
     with more in-edges than the cap take the unstaged path (per-edge decisions and
     gathers from HBM) -- all of them at 0, a mix at 1000 / 1024 (mean in-degree
     1024 per tile).  At the default cap (1216) that path runs for ~1e-9 of tiles."""
+    if wide == "1":
+        # the Imp3D push-sum kernel has one size class (its in-edge pass spills at 8 waves);
+        # GP_WIDE does not reach it (choose_kernel), so wide=1 would repeat wide=0
+        pytest.skip("Imp3D push-sum runs the 256 x 4 build only")
     monkeypatch.setenv("GP_KERNEL", "tile")
     monkeypatch.setenv("GP_WIDE", wide)
     monkeypatch.setenv("GP_STAGE_CAP", cap)

@@ -101,3 +101,30 @@ def test_bench_world_mismatch_refused():
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--no-cpu", "--no-traffic"], cwd=ROOT,
                        capture_output=True, text=True, timeout=120, env=dict(os.environ, WORLD_SIZE="1"))
     assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
+
+
+def test_rendezvous_stale_file_and_nonce(tmp_path, monkeypatch):
+    """A reused rendezvous path: rank 0 refuses to publish over a file already there,
+    and with GOSSIP_RDV_NONCE set (the launchers set one per launch) a reader takes
+    only a file carrying its nonce -- a stale id from a crashed run is never read."""
+    lib = L.lib()
+    path = tmp_path / "rccl_id"
+    path.write_bytes(bytes(128) + b"old-launch")
+    uid = C.create_string_buffer(128)
+    assert lib.gp_rendezvous_id(0, str(path).encode(), 50, uid) == -5
+    assert b"already exists" in lib.gp_last_error()
+    monkeypatch.setenv("GOSSIP_RDV_NONCE", "this-launch")
+    assert lib.gp_rendezvous_id(1, str(path).encode(), 100, uid) == -5
+    assert b"nonce" in lib.gp_last_error()
+    want = bytes(range(128))
+    path.write_bytes(want + b"this-launch")
+    assert lib.gp_rendezvous_id(1, str(path).encode(), 100, uid) == 0 and uid.raw == want
+
+
+def test_python_cli_world_mismatch_refused():
+    """python -m gossipprotocol_amd under an external launcher (WORLD_SIZE set) runs as that
+    rank instead of launching again, and refuses a --gpus that disagrees with WORLD_SIZE."""
+    r = subprocess.run([sys.executable, "-m", "gossipprotocol_amd", "1000", "Imp3D", "push-sum", "--gpus", "2"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, WORLD_SIZE="4", RANK="0"))
+    assert r.returncode == 2 and "WORLD_SIZE" in r.stderr
