@@ -95,8 +95,23 @@ struct Slab {
     std::vector<uint32_t> cap_out, cap_in;           // [h * W + b]: region h of the buffer to / from rank b
     std::vector<size_t> soff, sbytes, roff, rbytes;
     unsigned int* overflow = nullptr;  // device flag
-    // full topology over several ranks (gp_full.hip)
+    // Imp3D push-sum over several ranks: sender-ordered lists (gp_xchg.hpp)
+    bool lists = false;
+    uint32_t nt = 0, tsplit = 0;       // the slab's tiles; first tile of region 1
+    uint32_t* gw = nullptr;            // [tile * W + d]: first header word of the tile's segment
+    uint32_t* xcnt = nullptr;          // [h * W + d]: reservation counters of the send chunks
+    std::vector<size_t> lhdr, lval;    // send buffer: byte offsets of chunk (h, d)'s header words / slots
+    std::vector<size_t> rhdr, rval;    // receive buffer: byte offsets of chunk (h, p)'s header words / slots
+    std::vector<uint32_t> vbase;       // [h * W + d]: index of my chunk's first slot in d's vals region
+    // Imp3D gossip (column kernel) over several ranks: random-edge sends as bitmaps (gp_xchg.hpp)
+    bool bits = false;
+    uint32_t* rbits_in = nullptr;      // receive bitmap: source a's chunk at bit ro[a]
+    uint32_t* tgt = nullptr;           // local target of every receive-bitmap bit
+    uint32_t nbits_out = 0, nbits_in = 0;  // bitmap sizes (multiples of BITS_ALIGN)
+    std::vector<uint32_t> bo, bn, ro, rn;  // [peer]: chunk bit offset / bits, send and receive side
 };
+
+constexpr uint32_t BITS_ALIGN = 1024;  // bitmap chunks start on 128-byte boundaries
 
 size_t xbuf_bytes(uint32_t cap, bool push) {
     if (!cap) return 0;
@@ -142,8 +157,12 @@ struct gp_sim {
     // exchange buffers per rank pair: xhalves regions (2: full-topology push-sum, whose exchange runs
     // in two halves of each rank's senders on xstream, overlapped with the send / coarse passes)
     int xhalves = 1;
+    // Imp3D push-sum lists: header words of chunk (h, a -> b) at [(a * xhalves + h) * world + b],
+    // every slab's (each rank computes the whole table from the global random edges)
+    std::vector<uint32_t> list_nw;
     hipStream_t xstream = nullptr;
     hipEvent_t ev_send[2] = {nullptr, nullptr}, ev_xfer[2] = {nullptr, nullptr};
+    BlockPlan bplan{};  // KERNEL_BLOCK
 };
 
 namespace {
@@ -283,6 +302,12 @@ int alloc_slab(gp_sim* s, Slab& sl, int r) {
     S.base = S.ext_lo & ~3u;  // 4-aligned: the tile kernels move node bytes as words
     S.rtag = nullptr;
     S.rmsg = nullptr;
+    S.rk = nullptr;
+    S.rtg = nullptr;
+    S.sbits = nullptr;
+    S.xhdr = nullptr;
+    S.xvals = nullptr;
+    S.xnv = 0;
     int rc;
     const size_t next = (size_t)(S.ext_hi - S.base) + 1024;  // node arrays (+ word-I/O padding)
     const size_t nl = S.nloc;
@@ -347,6 +372,231 @@ int alloc_slab(gp_sim* s, Slab& sl, int r) {
         if ((rc = dev_alloc_t(s, &S.rbits[0], S.rbits_words)) || (rc = dev_alloc_t(s, &S.rbits[1], S.rbits_words)))
             return rc;
     }
+    return GP_OK;
+}
+
+// Exchange regions of a slab's senders: push-sum runs two (one's transfer overlaps the
+// other's packing), gossip one.  Imp3D push-sum cuts them at a tile boundary (the lists'
+// tiles); the full topology at the slab's middle id.
+int exchange_regions(const gp_sim* s) {
+    int NH = s->cfg.algorithm == GP_PUSHSUM ? 2 : 1;
+#ifdef GP_EXPERIMENTS
+    if (const char* e = std::getenv("GP_XHALVES")) NH = std::max(1, std::min(2, std::atoi(e)));
+#endif
+    return NH;
+}
+
+uint32_t slab_tiles(uint32_t lo, uint32_t nloc) {
+    return (uint32_t)(((uint64_t)lo + nloc + XTILE - 1) / XTILE - lo / XTILE);
+}
+
+// Local sender ids [s_lo, s_hi) of region h.
+void xregion(const Slab& sl, int NH, int h, uint32_t& s_lo, uint32_t& s_hi) {
+    const DevState& S = sl.S;
+    uint32_t split = S.nloc / 2;
+    if (sl.lists) {  // tiles [0, tsplit) | [tsplit, nt)
+        const int64_t b = (int64_t)(S.lo / XTILE + sl.tsplit) * XTILE - S.lo;
+        split = (uint32_t)std::min<int64_t>(S.nloc, std::max<int64_t>(0, b));
+    }
+    s_lo = NH == 1 || h == 0 ? 0u : split;
+    s_hi = NH == 1 || h == 1 ? S.nloc : split;
+}
+
+// Header-word offset of chunk (h, a) in rank b's header region, and slot offset of chunk
+// (h, a) in b's vals region: chunks in (h, a) order, a != b (every rank lays out its
+// receive buffer this way, and every sender addresses it this way).
+uint32_t list_hw(const gp_sim* s, int b, int h, int a) {
+    const int W = s->world, NH = s->xhalves;
+    uint64_t o = 0;
+    for (int hh = 0; hh < NH; ++hh)
+        for (int aa = 0; aa < W; ++aa) {
+            if (aa == b) continue;
+            if (hh == h && aa == a) return (uint32_t)o;
+            o += s->list_nw[((size_t)aa * NH + hh) * W + b];
+        }
+    return (uint32_t)o;
+}
+
+// Imp3D push-sum over several ranks: the static list plan (gp_xchg.hpp) of every slab
+// from the global random edges, the header-word counts of every chunk, and for this
+// rank's slabs the tile table gw and every remote in-edge's list key (rk).  kk: a
+// P-word scratch array; src: senders in receiver order (global); edge0: first global
+// in-edge of every rank.
+int build_lists(gp_sim* s, const uint32_t* rnd_all, uint32_t* kk, const uint32_t* src,
+                const std::vector<uint32_t>& edge0) {
+    const int W = s->world;
+    const int NH = s->xhalves = exchange_regions(s);
+    s->list_nw.assign((size_t)W * NH * W, 0);
+    std::vector<std::vector<uint32_t>> gw_all(W);
+    std::vector<uint32_t> tsplit(W);
+    Scratch tmp_mem;
+    for (int a = 0; a < W; ++a) {
+        const uint32_t lo = s->bounds[a], nloc = s->bounds[a + 1] - lo;
+        const uint32_t nt = slab_tiles(lo, nloc);
+        tsplit[a] = NH == 2 ? nt / 2 : nt;
+        uint32_t* cnt = nullptr;
+        HIP_TRY(tmp_mem.alloc(&cnt, (size_t)nt * W + 1));
+        ListCountArgs ca{};
+        ca.rnd = rnd_all;
+        ca.lo = lo;
+        ca.nloc = nloc;
+        ca.W = W;
+        ca.a = a;
+        for (int w = 0; w <= W; ++w) ca.bounds[w] = s->bounds[w];
+        ca.cnt = cnt;
+        HIP_TRY(launch_list_count(ca, s->stream));
+        std::vector<uint32_t> hc((size_t)nt * W);
+        HIP_TRY(hipMemcpyAsync(hc.data(), cnt, sizeof(uint32_t) * hc.size(), hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(hipStreamSynchronize(s->stream));
+        std::vector<uint32_t>& gw = gw_all[a];
+        gw.assign((size_t)nt * W, 0);
+        for (int d = 0; d < W; ++d) {
+            uint64_t run[2] = {0, 0};
+            for (uint32_t t = 0; t < nt; ++t) {
+                const int h = t < tsplit[a] ? 0 : 1;
+                gw[(size_t)t * W + d] = (uint32_t)run[h];
+                run[h] += (hc[(size_t)t * W + d] + 63u) / 64u;
+            }
+            for (int h = 0; h < NH; ++h) {
+                if (run[h] >= (1ull << 26)) {
+                    set_err("internal: random-edge list %d -> %d has %llu header words (limit 2^26)", a, d,
+                            (unsigned long long)run[h]);
+                    return GP_EINVAL;
+                }
+                s->list_nw[((size_t)a * NH + h) * W + d] = (uint32_t)run[h];
+            }
+        }
+    }
+    // every sender's key at its destination, then this rank's in-edges' keys
+    for (int a = 0; a < W; ++a) {
+        const uint32_t lo = s->bounds[a], nloc = s->bounds[a + 1] - lo;
+        uint32_t* gw = nullptr;
+        HIP_TRY(tmp_mem.alloc(&gw, gw_all[a].size() + 1));
+        HIP_TRY(hipMemcpyAsync(gw, gw_all[a].data(), sizeof(uint32_t) * gw_all[a].size(), hipMemcpyHostToDevice,
+                               s->stream));
+        ListKeyArgs ka{};
+        ka.rnd = rnd_all;
+        ka.gw = gw;
+        ka.lo = lo;
+        ka.nloc = nloc;
+        ka.tsplit = tsplit[a];
+        ka.W = W;
+        ka.a = a;
+        for (int w = 0; w <= W; ++w) ka.bounds[w] = s->bounds[w];
+        for (int h = 0; h < NH; ++h)
+            for (int b = 0; b < W; ++b) ka.hw[h][b] = b == a ? 0u : list_hw(s, b, h, a);
+        ka.key = kk;
+        HIP_TRY(launch_list_key(ka, s->stream));
+        HIP_TRY(hipStreamSynchronize(s->stream));  // (gw is freed at scope end; keep it simple)
+    }
+    int rc;
+    for (Slab& sl : s->slab) {
+        DevState& S = sl.S;
+        const int r = sl.rank;
+        sl.lists = true;
+        sl.nt = slab_tiles(S.lo, S.nloc);
+        sl.tsplit = tsplit[r];
+        if ((rc = dev_alloc_t(s, &sl.gw, gw_all[r].size() + 1))) return rc;
+        HIP_TRY(hipMemcpyAsync(sl.gw, gw_all[r].data(), sizeof(uint32_t) * gw_all[r].size(), hipMemcpyHostToDevice,
+                               s->stream));
+        const uint32_t ne = edge0[r + 1] - edge0[r];
+        if ((rc = dev_alloc_t(s, &S.rk, (size_t)ne + 4))) return rc;
+        HIP_TRY(launch_gather_keys(kk, src + edge0[r], ne, S.rk, s->grid, s->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    return GP_OK;
+}
+
+// Imp3D gossip on the column kernel over several ranks: the bitmap plan (gp_xchg.hpp).
+// For every source slab a, the edges with a sender on a get their rank among the
+// same receiver slab's edges from a (exclusive scan of a flag over the global
+// receiver order); this rank's senders learn their bit (rtg) and its receivers
+// the target of every received bit (tgt).  flag / scan / pos: P + 1 words of scratch.
+int build_bits(gp_sim* s, const uint32_t* src, const uint32_t* recv, const uint32_t* inv,
+               const std::vector<uint32_t>& edge0, uint32_t* flag, uint32_t* scan, uint32_t* pos) {
+    const int W = s->world;
+    const uint32_t P = (uint32_t)s->P;
+    Scratch tmp_mem;
+    size_t scan_bytes = 0;
+    HIP_TRY(exclusive_scan_u32(nullptr, scan_bytes, flag, scan, P + 1, s->stream));
+    uint8_t* scan_tmp = nullptr;
+    HIP_TRY(tmp_mem.alloc(&scan_tmp, scan_bytes ? scan_bytes : 4));
+    std::vector<std::vector<uint32_t>> n(W, std::vector<uint32_t>(W, 0));  // edges a -> b
+    for (int a = 0; a < W; ++a) {
+        HIP_TRY(launch_src_flag(src, P, s->bounds.data(), W, a, flag, s->grid, s->stream));
+        HIP_TRY(exclusive_scan_u32(scan_tmp, scan_bytes, flag, scan, P + 1, s->stream));
+        BitsSetupArgs ba{};
+        ba.src = src;
+        ba.recv = recv;
+        ba.scan = scan;
+        ba.pos = pos;
+        ba.n = P;
+        ba.W = W;
+        ba.a = a;
+        for (int w = 0; w <= W; ++w) {
+            ba.bounds[w] = s->bounds[w];
+            ba.edge0[w] = edge0[w];
+        }
+        HIP_TRY(launch_bits_pos(ba, s->grid, s->stream));
+        std::vector<uint32_t> at(W + 1);
+        for (int b = 0; b <= W; ++b)
+            HIP_TRY(hipMemcpyAsync(&at[b], scan + edge0[b], sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(hipStreamSynchronize(s->stream));
+        for (int b = 0; b < W; ++b) n[a][b] = a == b ? 0u : at[b + 1] - at[b];
+    }
+    auto pad = [](uint64_t x) { return (x + BITS_ALIGN - 1) / BITS_ALIGN * BITS_ALIGN; };
+    int rc;
+    for (Slab& sl : s->slab) {
+        DevState& S = sl.S;
+        const int me = sl.rank;
+        sl.bits = true;
+        sl.bo.assign(W, 0);
+        sl.bn.assign(W, 0);
+        sl.ro.assign(W, 0);
+        sl.rn.assign(W, 0);
+        uint64_t so = 0, ri = 0;
+        for (int d = 0; d < W; ++d) {
+            if (d == me) continue;
+            sl.bo[d] = (uint32_t)so;
+            sl.bn[d] = n[me][d];
+            so += pad(n[me][d]);
+            sl.ro[d] = (uint32_t)ri;
+            sl.rn[d] = n[d][me];
+            ri += pad(n[d][me]);
+        }
+        if (so >= (1ull << 31) || ri >= (1ull << 31)) {
+            set_err("internal: random-edge bitmaps beyond 2^31 bits");
+            return GP_EINVAL;
+        }
+        sl.nbits_out = (uint32_t)so;
+        sl.nbits_in = (uint32_t)ri;
+        if ((rc = dev_alloc_t(s, &S.rtg, (size_t)S.nloc + 64)) || (rc = dev_alloc_t(s, &S.sbits, so / 32 + 1)) ||
+            (rc = dev_alloc_t(s, &sl.rbits_in, ri / 32 + 1)) || (rc = dev_alloc_t(s, &sl.tgt, ri + 1)))
+            return rc;
+        HIP_TRY(hipMemsetAsync(S.sbits, 0, (so / 32 + 1) * 4, s->stream));
+        HIP_TRY(hipMemsetAsync(sl.rbits_in, 0, (ri / 32 + 1) * 4, s->stream));
+        BitsEndsArgs ea{};
+        ea.rnd = S.rnd;
+        ea.inv = inv;
+        ea.src = src;
+        ea.recv = recv;
+        ea.pos = pos;
+        ea.rtg = S.rtg;
+        ea.tgt = sl.tgt;
+        ea.lo = S.lo;
+        ea.nloc = S.nloc;
+        ea.e0 = edge0[me];
+        ea.e1 = edge0[me + 1];
+        ea.W = W;
+        ea.me = me;
+        for (int w = 0; w <= W; ++w) ea.bounds[w] = s->bounds[w];
+        for (int w = 0; w < W; ++w) {
+            ea.bo[w] = sl.bo[w];
+            ea.ro[w] = sl.ro[w];
+        }
+        HIP_TRY(launch_bits_ends(ea, s->grid, s->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(s->stream));
     return GP_OK;
 }
 
@@ -433,12 +683,12 @@ int build_imp3d(gp_sim* s) {
 #endif
             HIP_TRY(launch_pack_ind4(S, wide_at, s->grid, s->stream));
         }
-        if (W > 1) {
-            // counts (gossip column kernel) carry the target's local id: no slots, no tags
-            const bool slots = !col_gossip_counts(S);
+        if (W > 1 && !col_gossip_counts(S)) {  // (the gossip column kernel's bitmaps: build_bits)
+            // push-sum: sender-ordered lists (build_lists), no slots or tags; gossip tile kernel:
+            // {slot} entries and round tags (k_pack / k_unpack)
+            const bool slots = S.alg != PUSHSUM;
             if ((rc = dev_alloc_t(s, &sl.xdst, (size_t)S.nloc + 64))) return rc;
-            if (slots && ((rc = dev_alloc_t(s, &sl.pos, S.nloc)) || (rc = dev_alloc_t(s, &S.rtag, ne)) ||
-                          (S.alg == PUSHSUM && (rc = dev_alloc_t(s, &S.rmsg, ne)))))
+            if (slots && ((rc = dev_alloc_t(s, &sl.pos, S.nloc)) || (rc = dev_alloc_t(s, &S.rtag, ne))))
                 return rc;
             if (slots) HIP_TRY(hipMemsetAsync(S.rtag, 0xFF, sizeof(uint32_t) * (ne ? ne : 1), s->stream));
             PosArgs pa{};
@@ -455,6 +705,12 @@ int build_imp3d(gp_sim* s) {
             HIP_TRY(launch_make_pos(pa, s->grid, s->stream));
         }
     }
+    // (iota, the sort's value input, is free again: the lists' key scratch)
+    if (W > 1 && s->cfg.algorithm == GP_PUSHSUM && (rc = build_lists(s, rnd_all, iota, src_sorted, edge0))) return rc;
+    // (counts, off_all -- copied into the slabs' in_off -- and iota are free again: the bitmaps'
+    // scratch, in stream order after those copies)
+    if (W > 1 && col_gossip_counts(S0) && (rc = build_bits(s, src_sorted, keys_sorted, inv, edge0, counts, off_all, iota)))
+        return rc;
     HIP_TRY(hipStreamSynchronize(s->stream));
     return GP_OK;
 }
@@ -471,10 +727,12 @@ int setup_exchange(gp_sim* s) {
     const int W = s->world;
     const bool push = s->cfg.algorithm == GP_PUSHSUM;
     const bool full = s->cfg.topology == GP_FULL;
-    int NH = push ? 2 : 1;
-#ifdef GP_EXPERIMENTS
-    if (const char* e = std::getenv("GP_XHALVES")) NH = std::max(1, std::min(2, std::atoi(e)));
-#endif
+    if (!s->slab.empty() && s->slab[0].bits) {  // gossip column kernel: fixed-size bitmaps (build_bits)
+        s->xhalves = 1;
+        for (Slab& sl : s->slab) sl.overflow = &sl.S.ctl->overflow;
+        return GP_OK;
+    }
+    const int NH = exchange_regions(s);
     s->xhalves = NH;
     std::vector<uint32_t> caps((size_t)NH * W * W, 0);  // caps[(h * W + a) * W + b]: a -> b, region h
     Scratch tmp_mem;
@@ -512,8 +770,7 @@ int setup_exchange(gp_sim* s) {
             ea.rnd = S.rnd;
             ea.lo = S.lo;
             ea.nloc = S.nloc;
-            ea.s_lo = NH == 1 || h == 0 ? 0u : S.nloc / 2;
-            ea.s_hi = NH == 1 || h == 1 ? S.nloc : S.nloc / 2;
+            xregion(sl, NH, h, ea.s_lo, ea.s_hi);
             ea.W = W;
             ea.me = sl.rank;
             for (int w = 0; w <= W; ++w) ea.bounds[w] = s->bounds[w];
@@ -553,7 +810,69 @@ int setup_exchange(gp_sim* s) {
         }
     }
     int rc;
+    if (!s->slab.empty() && s->slab[0].lists) {  // Imp3D push-sum: sender-ordered lists (gp_xchg.hpp)
+        auto cap = [&](int h, int a, int b) { return caps[((size_t)h * W + a) * W + b]; };
+        auto nw = [&](int h, int a, int b) { return s->list_nw[((size_t)a * NH + h) * W + b]; };
+        // slot offset of chunk (h, a) in rank b's vals region (the order of list_hw)
+        auto vo = [&](int b, int h, int a) {
+            uint64_t o = 0;
+            for (int hh = 0; hh < NH; ++hh)
+                for (int aa = 0; aa < W; ++aa) {
+                    if (aa == b) continue;
+                    if (hh == h && aa == a) return o;
+                    o += cap(hh, aa, b);
+                }
+            return o;
+        };
+        for (Slab& sl : s->slab) {
+            const int a = sl.rank;
+            const size_t R = (size_t)NH * W;
+            sl.cap_out.assign(R, 0);
+            sl.cap_in.assign(R, 0);
+            sl.lhdr.assign(R, 0);
+            sl.lval.assign(R, 0);
+            sl.rhdr.assign(R, 0);
+            sl.rval.assign(R, 0);
+            sl.vbase.assign(R, 0);
+            size_t so = 0, hdr_in = 0;
+            uint64_t nv_in = 0;
+            for (int h = 0; h < NH; ++h)
+                for (int b = 0; b < W; ++b) {
+                    if (b == a) continue;
+                    const size_t i = (size_t)h * W + b;
+                    sl.cap_out[i] = cap(h, a, b);
+                    sl.cap_in[i] = cap(h, b, a);
+                    sl.lhdr[i] = so;
+                    so += (size_t)nw(h, a, b) * 16;
+                    sl.lval[i] = so;
+                    so += (size_t)sl.cap_out[i] * 16;
+                    sl.rhdr[i] = (size_t)list_hw(s, a, h, b) * 16;
+                    hdr_in += (size_t)nw(h, b, a) * 16;
+                    nv_in += sl.cap_in[i];
+                    const uint64_t vb = vo(b, h, a);
+                    if (vb >= (1ull << 32) || nv_in >= (1ull << 32)) {
+                        set_err("internal: exchange vals region beyond 2^32 slots");
+                        return GP_EINVAL;
+                    }
+                    sl.vbase[i] = (uint32_t)vb;
+                }
+            for (int h = 0; h < NH; ++h)
+                for (int b = 0; b < W; ++b)
+                    if (b != a) sl.rval[(size_t)h * W + b] = hdr_in + (size_t)vo(a, h, b) * 16;
+            const size_t ro = hdr_in + (size_t)nv_in * 16;
+            if ((rc = dev_alloc_t(s, &sl.xsend, so)) || (rc = dev_alloc_t(s, &sl.xrecv, ro)) ||
+                (rc = dev_alloc_t(s, &sl.xcnt, R)))
+                return rc;
+            HIP_TRY(hipMemsetAsync(sl.xsend, 0, so ? so : 16, s->stream));
+            HIP_TRY(hipMemsetAsync(sl.xrecv, 0, ro ? ro : 16, s->stream));
+            sl.S.xhdr = reinterpret_cast<const XHdr*>(sl.xrecv);
+            sl.S.xvals = reinterpret_cast<const double2*>(sl.xrecv + hdr_in);
+            sl.S.xnv = (uint32_t)std::max<uint64_t>(1, nv_in);
+            sl.overflow = &sl.S.ctl->overflow;
+        }
+    }
     for (Slab& sl : s->slab) {
+        if (sl.lists) break;
         const int a = sl.rank;
         const size_t R = (size_t)NH * W;
         sl.cap_out.assign(R, 0);
@@ -752,12 +1071,13 @@ int launch_round_full_multi(gp_sim* s, uint32_t r, hipEvent_t e0, hipEvent_t e1)
 
 // Halo refresh + Imp3D random-edge exchange for round `rn`, whose state the
 // previous round kernel has just written to buffers rn & 1.  Push-sum moves the
-// random-edge messages in two regions (s->xhalves): the senders' first half is
-// packed and handed to the exchange stream, whose transfer (with the halo planes)
-// overlaps the second half's packing; the first half is unpacked while the second
-// is in flight.  Events order the streams, so every rank issues its RCCL groups in
-// one order (region 0, region 1), before the finalize all-reduce on the compute
-// stream.
+// random-edge messages as sender-ordered lists (k_list_pack: header words + compacted
+// messages, read in place by the next round kernel -- no unpack) in two regions
+// (s->xhalves): region 0 is packed and handed to the exchange stream, whose transfer
+// (with the halo planes) overlaps region 1's packing.  Gossip packs {slot} or {count}
+// entries and unpacks them (k_pack / k_unpack).  Events order the streams, so every
+// rank issues its RCCL groups in one order (region 0, region 1), before the finalize
+// all-reduce on the compute stream.
 int exchange(gp_sim* s, uint32_t rn) {
     const int W = s->world;
     if (W == 1 || s->cfg.topology == GP_FULL) return GP_OK;  // full: the exchange is inside the round
@@ -785,10 +1105,39 @@ int exchange(gp_sim* s, uint32_t rn) {
             }
         }
     }
+    const bool lists = imp && push && s->slab[0].lists;
+    const bool bits = imp && s->slab[0].bits;
     for (int h = 0; h < NH; ++h) {
-        if (imp) {
+        if (imp && !bits) {  // (bitmaps: set by the round kernel itself)
             for (Slab& sl : s->slab) {
                 DevState& S = sl.S;
+                if (lists) {  // header words + compacted messages of region h (k_list_pack)
+                    HIP_TRY(hipMemsetAsync(sl.xcnt + (size_t)h * W, 0, sizeof(uint32_t) * W, s->stream));
+                    ListPackArgs la{};
+                    la.nbn = S.nb[b];
+                    la.swn = S.sw[b];
+                    la.xdst = sl.xdst;
+                    la.gw = sl.gw;
+                    la.lo = S.lo;
+                    la.nloc = S.nloc;
+                    la.base = S.base;
+                    la.t0 = h == 0 ? 0u : sl.tsplit;
+                    la.t1 = NH == 1 || h == 1 ? sl.nt : sl.tsplit;
+                    la.W = W;
+                    la.me = sl.rank;
+                    for (int d = 0; d < W; ++d) {
+                        if (d == sl.rank) continue;
+                        const size_t i = (size_t)h * W + d;
+                        la.peer[d].hdr = reinterpret_cast<XHdr*>(sl.xsend + sl.lhdr[i]);
+                        la.peer[d].vals = reinterpret_cast<double2*>(sl.xsend + sl.lval[i]);
+                        la.peer[d].cnt = sl.xcnt + i;
+                        la.peer[d].cap = sl.cap_out[i];
+                        la.peer[d].vbase = sl.vbase[i];
+                    }
+                    la.overflow = sl.overflow;
+                    HIP_TRY(launch_list_pack(la, s->stream));
+                    continue;
+                }
                 ZeroArgs z{};
                 PackArgs pa{};
                 pa.nbn = S.nb[b];
@@ -822,7 +1171,26 @@ int exchange(gp_sim* s, uint32_t rn) {
             HIP_TRY(hipStreamWaitEvent(xs, s->ev_send[h], 0));
         }
         if (s->mode == MODE_VIRTUAL) {
-            if (imp) {
+            if (bits) {
+                for (Slab& a : s->slab)
+                    for (Slab& d : s->slab)
+                        if (&a != &d && a.bn[d.rank])
+                            HIP_TRY(hipMemcpyAsync(d.rbits_in + d.ro[a.rank] / 32, a.S.sbits + a.bo[d.rank] / 32,
+                                                   (size_t)(a.bn[d.rank] + 31) / 32 * 4, hipMemcpyDeviceToDevice, xs));
+            } else if (lists) {
+                for (Slab& a : s->slab)
+                    for (Slab& d : s->slab) {
+                        if (&a == &d) continue;
+                        const size_t i = (size_t)h * W + d.rank, j = (size_t)h * W + a.rank;
+                        const size_t hb = (size_t)s->list_nw[((size_t)a.rank * NH + h) * W + d.rank] * 16;
+                        if (hb)
+                            HIP_TRY(hipMemcpyAsync(d.xrecv + d.rhdr[j], a.xsend + a.lhdr[i], hb,
+                                                   hipMemcpyDeviceToDevice, xs));
+                        if (a.cap_out[i])
+                            HIP_TRY(hipMemcpyAsync(d.xrecv + d.rval[j], a.xsend + a.lval[i], (size_t)a.cap_out[i] * 16,
+                                                   hipMemcpyDeviceToDevice, xs));
+                    }
+            } else if (imp) {
                 int rc = transfer_xbufs(s, h, xs);
                 if (rc) return rc;
             }
@@ -847,7 +1215,27 @@ int exchange(gp_sim* s, uint32_t rn) {
                     NCCL_TRY(ncclRecv(S.sw[b] + (sl.hi - S.base), H * 16, ncclUint8, r + 1, s->comm, xs));
                 }
             }
-            if (imp)
+            if (bits)
+                for (int p = 0; p < W; ++p) {  // the bitmap chunks, each way
+                    if (p == r) continue;
+                    const size_t ob = (size_t)(sl.bn[p] + 31) / 32 * 4, ib = (size_t)(sl.rn[p] + 31) / 32 * 4;
+                    if (ob) NCCL_TRY(ncclSend(S.sbits + sl.bo[p] / 32, ob, ncclUint8, p, s->comm, xs));
+                    if (ib) NCCL_TRY(ncclRecv(sl.rbits_in + sl.ro[p] / 32, ib, ncclUint8, p, s->comm, xs));
+                }
+            else if (lists)
+                for (int p = 0; p < W; ++p) {  // header words, then messages, each way
+                    if (p == r) continue;
+                    const size_t i = (size_t)h * W + p;
+                    const size_t ho = (size_t)s->list_nw[((size_t)r * NH + h) * W + p] * 16;
+                    const size_t hi = (size_t)s->list_nw[((size_t)p * NH + h) * W + r] * 16;
+                    if (ho) NCCL_TRY(ncclSend(sl.xsend + sl.lhdr[i], ho, ncclUint8, p, s->comm, xs));
+                    if (sl.cap_out[i])
+                        NCCL_TRY(ncclSend(sl.xsend + sl.lval[i], (size_t)sl.cap_out[i] * 16, ncclUint8, p, s->comm, xs));
+                    if (hi) NCCL_TRY(ncclRecv(sl.xrecv + sl.rhdr[i], hi, ncclUint8, p, s->comm, xs));
+                    if (sl.cap_in[i])
+                        NCCL_TRY(ncclRecv(sl.xrecv + sl.rval[i], (size_t)sl.cap_in[i] * 16, ncclUint8, p, s->comm, xs));
+                }
+            else if (imp)
                 for (int p = 0; p < W; ++p) {
                     if (p == r) continue;
                     const size_t i = (size_t)h * W + p;
@@ -858,7 +1246,15 @@ int exchange(gp_sim* s, uint32_t rn) {
         }
         if (xs != s->stream) HIP_TRY(hipEventRecord(s->ev_xfer[h], xs));
     }
-    if (imp) {
+    if (bits) {
+        if (xs != s->stream) HIP_TRY(hipStreamWaitEvent(s->stream, s->ev_xfer[NH - 1], 0));
+        for (Slab& sl : s->slab) {
+            // one rumour per received bit at its target, counted for round rn; then the send
+            // bitmap is cleared for the next round kernel
+            HIP_TRY(launch_apply_bits(sl.rbits_in, sl.nbits_in / 32, sl.tgt, sl.S.rq[rn & 1], sl.S.rq8, s->stream));
+            if (sl.nbits_out) HIP_TRY(hipMemsetAsync(sl.S.sbits, 0, (size_t)sl.nbits_out / 8, s->stream));
+        }
+    } else if (imp && !lists) {
         for (int h = 0; h < NH; ++h) {
             if (xs != s->stream) HIP_TRY(hipStreamWaitEvent(s->stream, s->ev_xfer[h], 0));
             for (Slab& sl : s->slab) {
@@ -928,6 +1324,14 @@ double alg_bytes(const gp_sim* s) {
         // in-list, and the random-edge message payload, 16 B for the ~1/7 of senders
         // that use the random edge -- a random gather, moved as a 128-B line)
         if (S.topo == IMP3D) return 38.5 + 16.0 / 7.0;
+        if (S.kernel == KERNEL_BLOCK) {
+            // LDS-resident: per round only the boxes' boundary layers move (17 B per face node,
+            // written once, read once by the neighbour), through L2 / Infinity Cache
+            const BlockPlan& p = S.bplan;
+            const double g = S.G.g;
+            const double faces = g * g * ((p.nbx - 1) + (p.nby - 1) + (p.nbz - 1)) * 2.0;
+            return 2.0 * 17.0 * faces / (double)S.G.P;
+        }
         if (S.topo != FULL) return 34.0;
         // send: byte 1 (sweep 1) + byte 1 + own (s, w) 16 + message write 20; split: sender
         // id 4 (sweep 1) + message r+w 40; fold: message 20 + own (s, w) r+w 32 + byte r+w 2
@@ -967,14 +1371,22 @@ void choose_kernel(gp_sim* s, int64_t nloc_max, int& kernel, uint32_t& col_xsegs
     const bool lattice = cfg->topology == GP_3D || cfg->topology == GP_IMP3D;
     const bool push = cfg->algorithm == GP_PUSHSUM;
     if (lattice && g >= 200 && !push) kernel = KERNEL_COL;
+    // 3D push-sum on one rank whose lattice fits the chip's LDS (C2: g = 100): one cooperative
+    // launch per batch, the state resident in LDS (gp_block.hip)
+    BlockPlan bp{};
+    const bool block_ok = cfg->topology == GP_3D && push && s->world == 1 && g >= 2 &&
+                          block_plan((uint32_t)g, prop.multiProcessorCount, bp);
+    if (block_ok) kernel = KERNEL_BLOCK;
 #ifdef GP_EXPERIMENTS
     if (const char* e = std::getenv("GP_KERNEL")) {
         if (!std::strcmp(e, "tile")) kernel = KERNEL_TILE;
         else if (!std::strcmp(e, "col") && lattice && !push) kernel = KERNEL_COL;
+        else if (!std::strcmp(e, "block") && block_ok) kernel = KERNEL_BLOCK;
     }
 #endif
+    s->bplan = bp;
     col_xsegs = 1;
-    if (cfg->topology != GP_FULL && kernel != KERNEL_TILE) {
+    if (cfg->topology != GP_FULL && kernel == KERNEL_COL) {
         // gossip: exactly the resident grid (a persistent sweep), a multiple of the 8 XCDs
         cap = (int64_t)prop.multiProcessorCount * col_blocks_per_cu(cfg->topology, cfg->algorithm);
         // x segments per patch: enough work items for every resident wave, >= 16 planes each
@@ -1064,6 +1476,13 @@ int build_sim(gp_sim* s) {
         // 0.40 ms/round at P = 2.7e7, profiles/r02/round_close.txt)
         sl.S.fuse_finalize = (s->mode == MODE_SINGLE && s->cfg.algorithm == GP_PUSHSUM &&
                               s->cfg.topology != GP_FULL) ? 2u : 0u;
+        sl.S.bplan = s->bplan;
+        sl.S.bface = sl.S.bscratch = nullptr;
+        if (kernel == KERNEL_BLOCK) {  // face exchange buffers + barrier / accumulator scratch
+            if ((rc = dev_alloc(s, &sl.S.bface, block_face_bytes(s->bplan))) || (rc = dev_alloc(s, &sl.S.bscratch, 64)))
+                return rc;
+            HIP_TRY(block_kernel_setup(s->bplan));
+        }
 #ifdef GP_EXPERIMENTS
         if (const char* e = std::getenv("GP_FUSE")) sl.S.fuse_finalize = sl.S.fuse_finalize ? (uint32_t)(e[0] - '0') : 0u;
         if (const char* e = std::getenv("GP_STAGE_CAP")) sl.S.tile_stage_cap = (uint32_t)std::max(0, std::atoi(e));
@@ -1350,12 +1769,29 @@ int64_t gp_step(gp_sim* s, int64_t nrounds, int64_t* alerts_out) {
         int64_t batch = std::min<int64_t>(nrounds - executed, BATCH);
         if (s->cfg.max_rounds > 0) batch = std::min<int64_t>(batch, s->cfg.max_rounds - s->rounds_done);
         if (batch <= 0) break;
-        for (int64_t k = 0; k < batch; ++k) {
-            const uint32_t r = (uint32_t)(s->rounds_done + k);
-            hipEvent_t e0 = s->timing ? s->ev[2 * k] : nullptr;
-            hipEvent_t e1 = s->timing ? s->ev[2 * k + 1] : nullptr;
-            int rc = launch_round(s, r, e0, e1);
-            if (rc) return rc;
+        const bool block = s->slab[0].S.kernel == KERNEL_BLOCK;
+        if (block) {  // the whole batch in one cooperative launch (gp_block.hip)
+            const DevState& S = s->slab[0].S;
+            if (s->timing) HIP_TRY(hipEventRecord(s->ev[0], s->stream));
+            HIP_TRY(launch_round_block(S, S.bplan, (uint32_t)s->rounds_done, (uint32_t)batch, S.bface, S.bscratch,
+                                       s->stream));
+            if (s->timing) HIP_TRY(hipEventRecord(s->ev[1], s->stream));
+            unsigned int flags[2] = {0, 0};
+            HIP_TRY(hipMemcpyAsync(flags, S.bscratch, sizeof flags, hipMemcpyDeviceToHost, s->stream));
+            HIP_TRY(hipStreamSynchronize(s->stream));
+            if (flags[1]) {
+                set_err("the LDS-resident round kernel's grid barrier timed out (a workgroup never arrived); "
+                        "the rounds of this batch are invalid");
+                return GP_ESTATE;
+            }
+        } else {
+            for (int64_t k = 0; k < batch; ++k) {
+                const uint32_t r = (uint32_t)(s->rounds_done + k);
+                hipEvent_t e0 = s->timing ? s->ev[2 * k] : nullptr;
+                hipEvent_t e1 = s->timing ? s->ev[2 * k + 1] : nullptr;
+                int rc = launch_round(s, r, e0, e1);
+                if (rc) return rc;
+            }
         }
         HIP_TRY(hipMemcpyAsync(s->host_ctl, s->slab[0].S.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, s->stream));
         HIP_TRY(hipStreamSynchronize(s->stream));
@@ -1385,7 +1821,12 @@ int64_t gp_step(gp_sim* s, int64_t nrounds, int64_t* alerts_out) {
             set_err("round bookkeeping mismatch (device %llu alerts, host %lld)", hc.alerts_total, (long long)cum);
             return GP_ESTATE;
         }
-        if (s->timing) {
+        if (s->timing && block) {  // one launch for the batch: its time over the rounds it ran
+            float ms = 0.f;
+            HIP_TRY(hipEventElapsedTime(&ms, s->ev[0], s->ev[1]));
+            s->kernel_ms += ms;
+            s->launches += ex;
+        } else if (s->timing) {
             for (int64_t k = 0; k < ex; ++k) {
                 float ms = 0.f;
                 HIP_TRY(hipEventElapsedTime(&ms, s->ev[2 * k], s->ev[2 * k + 1]));

@@ -1,0 +1,392 @@
+// gp_block.hip -- push-sum on a small 3D lattice held in LDS across rounds (gfx950).
+//
+// C2 (BASELINE config 2: 3D push-sum, n = 1e6, g = 100) is 17 bytes of state per
+// node, 17 MB in all -- less than the chip's LDS (256 CUs x 160 KiB).  A round of
+// the tile kernel re-streams that state through HBM and the Infinity Cache in a
+// fresh launch (20.7 us per round, bound by one tile's latency); here one
+// cooperative launch runs a whole batch of rounds with the lattice resident in LDS:
+//
+//   * the lattice is cut into NB = nbx * nby * nbz boxes (at most one per CU), one
+//     1024-thread workgroup each; a box's node bytes and (s, w) live in LDS;
+//   * per round a box writes its six boundary layers (node byte + (s, w)) to a
+//     face buffer in global memory, the grid meets at a barrier (release / acquire
+//     at agent scope), and every box reads its neighbours' facing layers into LDS
+//     halo arrays -- the only global traffic of a round (~28 KB per box at C2);
+//   * each node then folds exactly as the tile kernel (gp_round.hip) does: own half,
+//     lattice messages in the receiver's slot order (Program.fs:246-257), the ratio
+//     test of Program.fs:114-123 (SRS v1 B.4), the next direction by Philox -- with
+//     acc + m * 0.5, the oracle's own rounding;
+//   * the round's alert / newly-active counts go to a per-round accumulator; after
+//     the next barrier every box reads it, so every box knows the cumulative alert
+//     count and stops after the round that reaches T (Program.fs:51-56), and box 0
+//     records the round in the control block (hist, totals, done) for the host.
+//
+// At the end of the launch the state is written back to the round's (s, w) / node
+// byte buffers, so everything else (gp_read_state, the next batch) sees the usual
+// layout.  Every barrier wait has a time limit: a grid that is not co-resident
+// (hipLaunchCooperativeKernel refuses such a launch) or a lost block sets `err` and
+// every block leaves -- the batch fails loudly instead of hanging the device.
+#include <algorithm>
+
+#include "gp_internal.hpp"
+
+namespace gp {
+
+namespace {
+
+constexpr int BK_THREADS = 1024;
+constexpr int BK_NPT = 5;  // nodes per thread: boxes of at most 5120 nodes
+
+struct BlockArgs {
+    const double2* sw_in;   // round r0's state (id-indexed)
+    double2* sw_out;        // the state after the last executed round
+    double2* sw_alt;        // the other buffer (the state if the executed count is even)
+    const uint8_t* nb_in;
+    uint8_t* nb_out;
+    uint8_t* nb_alt;
+    uint8_t* fb;            // face bytes [2][NB][6][fmax]
+    double2* fs;            // face (s, w) [2][NB][6][fmax]
+    unsigned int* bar;      // barrier arrivals (zeroed before the launch)
+    unsigned long long* acc;  // [3][2]: per-round alerts, newly active (zeroed before the launch)
+    unsigned int* err;      // set by a barrier that timed out
+    Ctl* ctl;
+    Geom G;
+    uint32_t k0, k1;
+    uint32_t r0, nrounds;
+    uint32_t nbx, nby, nbz, fmax, vmax;
+};
+
+__device__ __forceinline__ uint32_t split(uint32_t g, uint32_t i, uint32_t n) {
+    return (uint32_t)((uint64_t)g * i / n);
+}
+
+__device__ __forceinline__ uint64_t now_10ns() { return __builtin_amdgcn_s_memrealtime(); }  // 100 MHz
+
+// Grid barrier k (k = 1, 2, ...): arrivals counted on one word (never reset inside a
+// launch); waits at most ~2 s.  Every thread releases its global writes and acquires
+// the others' at agent scope.
+__device__ __forceinline__ bool grid_sync(unsigned int* bar, unsigned int target, unsigned int* err) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __syncthreads();
+    __shared__ unsigned int ok;
+    if (threadIdx.x == 0) {
+        ok = 1u;
+        __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t t0 = now_10ns();
+        while (__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || now_10ns() - t0 > 200000000ull) {
+                __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = 0u;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    return ok != 0u;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(BK_THREADS) void k_ps_block(BlockArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const uint32_t g = a.G.g, g2 = a.G.g2, gm = g - 1u;
+    const uint32_t NB = gridDim.x;
+    const uint32_t b = blockIdx.x;
+    const uint32_t ix = b / (a.nby * a.nbz), iy = (b / a.nbz) % a.nby, iz = b % a.nbz;
+    const uint32_t x0 = split(g, ix, a.nbx), x1 = split(g, ix + 1, a.nbx);
+    const uint32_t y0 = split(g, iy, a.nby), y1 = split(g, iy + 1, a.nby);
+    const uint32_t z0 = split(g, iz, a.nbz), z1 = split(g, iz + 1, a.nbz);
+    const uint32_t dx = x1 - x0, dy = y1 - y0, dz = z1 - z0, dyz = dy * dz, V = dx * dyz;
+    const uint32_t F = a.fmax;
+    double2* swl = reinterpret_cast<double2*>(lds);         // [vmax]
+    double2* hsw = swl + a.vmax;                            // [6][fmax]
+    uint8_t* bl = reinterpret_cast<uint8_t*>(hsw + 6 * F);  // [vmax] node bytes of the round
+    uint8_t* bn = bl + a.vmax;                              // [vmax] the next round's (swapped per round)
+    uint8_t* hb = bn + a.vmax;                              // [6][fmax]
+    __shared__ uint32_t red[2][BK_THREADS / 64];
+    // face sizes and whether the neighbour in direction f exists (slot order: x-1, x+1, y+1, y-1, z+1, z-1)
+    const uint32_t fsz[6] = {dyz, dyz, dx * dz, dx * dz, dx * dy, dx * dy};
+    const bool has[6] = {ix > 0, ix + 1 < a.nbx, iy + 1 < a.nby, iy > 0, iz + 1 < a.nbz, iz > 0};
+    const uint32_t nbr_b[6] = {b - a.nby * a.nbz, b + a.nby * a.nbz, b + a.nbz, b - a.nbz, b + 1, b - 1};
+
+    // the box's state into LDS
+    for (uint32_t v = threadIdx.x; v < V; v += BK_THREADS) {
+        const uint32_t lx = v / dyz, ly = (v - lx * dyz) / dz, lz = v - lx * dyz - ly * dz;
+        const uint32_t j = (x0 + lx) * g2 + (y0 + ly) * g + (z0 + lz);
+        swl[v] = a.sw_in[j];
+        bl[v] = a.nb_in[j];
+    }
+    unsigned long long total = __hip_atomic_load(&a.ctl->alerts_total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long act = __hip_atomic_load(&a.ctl->active_total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t done_rounds = 0;  // rounds executed by this launch
+    bool stop = __hip_atomic_load(&a.ctl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+    __syncthreads();
+    for (uint32_t i = 0; i <= a.nrounds && !stop; ++i) {
+        const uint32_t r = a.r0 + i;
+        // (1) boundary layers of the current state -> face buffer (parity i & 1)
+        if (i < a.nrounds) {
+            const size_t fo = ((size_t)(i & 1u) * NB + b) * 6 * F;
+#pragma unroll
+            for (int f = 0; f < 6; ++f) {
+                if (!has[f]) continue;
+                for (uint32_t t = threadIdx.x; t < fsz[f]; t += BK_THREADS) {
+                    uint32_t v;
+                    if (f < 2) {  // x layer: t = ly * dz + lz
+                        v = (f == 0 ? 0u : dx - 1u) * dyz + t;
+                    } else if (f < 4) {  // y layer: t = lx * dz + lz
+                        const uint32_t lx = t / dz, lz = t - lx * dz;
+                        v = lx * dyz + (f == 2 ? dy - 1u : 0u) * dz + lz;
+                    } else {  // z layer: t = lx * dy + ly
+                        const uint32_t lx = t / dy, ly = t - lx * dy;
+                        v = lx * dyz + ly * dz + (f == 4 ? dz - 1u : 0u);
+                    }
+                    a.fb[fo + f * F + t] = bl[v];
+                    a.fs[fo + f * F + t] = swl[v];
+                }
+            }
+        }
+        // (2) barrier i + 1: faces of round r written, round r - 1's counts complete
+        if (NB > 1 && !grid_sync(a.bar, (i + 1u) * NB, a.err)) break;
+        if (NB == 1) __syncthreads();
+        // (3) close round r - 1 (every block: the same cumulative count)
+        if (i > 0) {
+            const unsigned long long* c = a.acc + 2 * ((r - 1u) % 3u);
+            const unsigned long long ra = __hip_atomic_load(&c[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long rn = __hip_atomic_load(&c[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            total += ra;
+            act += rn;
+            if (b == 0 && threadIdx.x == 0) {
+                Ctl* ctl = a.ctl;
+                ctl->hist[(r - 1u) % HIST] = ra;
+                __hip_atomic_store(&ctl->alerts_total, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&ctl->active_total, act, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (act >= a.G.P) __hip_atomic_store(&ctl->all_active, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (total >= a.G.T) __hip_atomic_store(&ctl->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                // the accumulator of round r + 1 (last read after barrier r - 1 + ... i - 1)
+                unsigned long long* z = a.acc + 2 * ((r + 1u) % 3u);
+                __hip_atomic_store(&z[0], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&z[1], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (total >= a.G.T) break;  // (the same decision in every block)
+        }
+        if (i == a.nrounds) break;
+        // (4) the neighbours' facing layers -> LDS halos
+        {
+            const size_t fp = (size_t)(i & 1u) * NB;
+#pragma unroll
+            for (int f = 0; f < 6; ++f) {
+                if (!has[f]) continue;
+                const size_t fo = ((fp + nbr_b[f]) * 6 + (f ^ 1)) * F;
+                for (uint32_t t = threadIdx.x; t < fsz[f]; t += BK_THREADS) {
+                    hb[f * F + t] = a.fb[fo + t];
+                    hsw[f * F + t] = a.fs[fo + t];
+                }
+            }
+        }
+        __syncthreads();
+        // (5) the round for this thread's nodes (results in registers)
+        uint32_t alerts = 0, newly = 0;
+        // the new (s, w) of node slot q in n[q] (named registers, selected by q: the slot loop
+        // is not unrolled -- unrolled, the compiler interleaved all slots and spilled); the
+        // new node bytes go straight to bn
+        double2 n0 = make_double2(0.0, 0.0), n1 = n0, n2 = n0, n3 = n0, n4 = n0;
+        static_assert(BK_NPT == 5, "one named register pair per node slot");
+#pragma unroll 1
+        for (int q = 0; q < BK_NPT; ++q) {
+            const uint32_t v = q * BK_THREADS + threadIdx.x;
+            if (v >= V) break;
+            const uint32_t lx = v / dyz, ly = (v - lx * dyz) / dz, lz = v - lx * dyz - ly * dz;
+            const uint32_t x = x0 + lx, y = y0 + ly, z = z0 + lz;
+            const uint32_t mask = mask_xyz(x, y, z, gm);
+            const uint32_t bt = bl[v];
+            const double2 sv = swl[v];
+            const bool active = (bt & B_ACTIVE) != 0;
+            const uint32_t deg = popc6(mask);
+            const bool halve = active && deg > 0;
+            double acc_s = halve ? sv.x * 0.5 : sv.x;
+            double acc_w = halve ? sv.y * 0.5 : sv.y;
+            bool recv = false;
+            // lattice slots in the receiver's order: x-1, x+1, y+1, y-1, z+1, z-1; the sender in
+            // direction d sends here iff its direction is d ^ 1
+#pragma unroll
+            for (int d = 0; d < 6; ++d) {
+                if (!((mask >> d) & 1u)) continue;
+                bool in;
+                uint32_t vn = 0, hn = 0;
+                switch (d) {
+                    case 0: in = lx > 0; vn = v - dyz; hn = ly * dz + lz; break;
+                    case 1: in = lx + 1 < dx; vn = v + dyz; hn = ly * dz + lz; break;
+                    case 2: in = ly + 1 < dy; vn = v + dz; hn = lx * dz + lz; break;
+                    case 3: in = ly > 0; vn = v - dz; hn = lx * dz + lz; break;
+                    case 4: in = lz + 1 < dz; vn = v + 1; hn = lx * dy + ly; break;
+                    default: in = lz > 0; vn = v - 1; hn = lx * dy + ly; break;
+                }
+                const uint32_t nb = in ? bl[vn] : hb[d * F + hn];
+                if ((nb & DIR_MASK) == (uint32_t)(d ^ 1)) {
+                    const double2 m = in ? swl[vn] : hsw[d * F + hn];
+                    acc_s = acc_s + m.x * 0.5;  // the oracle's rounding (no fused multiply-add)
+                    acc_w = acc_w + m.y * 0.5;
+                    recv = true;
+                }
+            }
+            uint32_t flags = bt & (B_ACTIVE | B_CONV | (3u << CNT_SHIFT));
+            bool act_n = active;
+            if (recv) {
+                if (!(bt & B_CONV)) {
+                    uint32_t c3 = (bt >> CNT_SHIFT) & 3u;
+                    c3 = ratio_moved(sv.x, sv.y, acc_s, acc_w) ? 0u : c3 + 1u;
+                    flags = (flags & ~(3u << CNT_SHIFT)) | (c3 << CNT_SHIFT);
+                    if (c3 == 3) {
+                        flags |= B_CONV;
+                        ++alerts;
+                    }
+                }
+                if (!active) {
+                    ++newly;
+                    flags |= B_ACTIVE;
+                    act_n = true;
+                }
+            }
+            uint32_t dir = DIR_NONE;
+            if (act_n && deg > 0) dir = slot_to_dir_fast(mask, uniform(a.k0, a.k1, S_PUSHSUM, x * g2 + y * g + z, r + 1, deg));
+            const double2 res = make_double2(acc_s, acc_w);
+            if (q == 0) n0 = res;
+            else if (q == 1) n1 = res;
+            else if (q == 2) n2 = res;
+            else if (q == 3) n3 = res;
+            else n4 = res;
+            bn[v] = (uint8_t)(flags | dir);
+        }
+        __syncthreads();  // every node has read the round-start state
+        // (6) the new state into LDS; the round's counts into its accumulator
+        {
+            const double2 nq[BK_NPT] = {n0, n1, n2, n3, n4};
+#pragma unroll
+            for (int q = 0; q < BK_NPT; ++q) {
+                const uint32_t v = q * BK_THREADS + threadIdx.x;
+                if (v < V) swl[v] = nq[q];
+            }
+        }
+        {
+            uint8_t* t = bl;
+            bl = bn;
+            bn = t;
+        }
+        uint32_t xa = alerts, xn = newly;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            xa += __shfl_xor(xa, o, 64);
+            xn += __shfl_xor(xn, o, 64);
+        }
+        if ((threadIdx.x & 63u) == 0) {
+            red[0][threadIdx.x >> 6] = xa;
+            red[1][threadIdx.x >> 6] = xn;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            xa = xn = 0;
+            for (int w = 0; w < BK_THREADS / 64; ++w) {
+                xa += red[0][w];
+                xn += red[1][w];
+            }
+            unsigned long long* c = a.acc + 2 * (r % 3u);
+            if (xa) __hip_atomic_fetch_add(&c[0], (unsigned long long)xa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (xn) __hip_atomic_fetch_add(&c[1], (unsigned long long)xn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        ++done_rounds;
+    }
+    // the state after the last executed round, into that round's buffers (the tile kernel's
+    // convention: round r writes buffer (r + 1) & 1)
+    __syncthreads();
+    double2* swo = (done_rounds & 1u) ? a.sw_out : a.sw_alt;
+    uint8_t* nbo = (done_rounds & 1u) ? a.nb_out : a.nb_alt;
+    for (uint32_t v = threadIdx.x; v < V; v += BK_THREADS) {
+        const uint32_t lx = v / dyz, ly = (v - lx * dyz) / dz, lz = v - lx * dyz - ly * dz;
+        const uint32_t j = (x0 + lx) * g2 + (y0 + ly) * g + (z0 + lz);
+        swo[j] = swl[v];
+        nbo[j] = bl[v];
+    }
+}
+
+// ---------------------------------------------------------------- host side
+// The box grid of a g^3 lattice for `cus` workgroups: the most boxes (at most one per
+// CU, a box of at most BK_NPT * 1024 nodes) with the smallest largest box, whose LDS
+// (17 bytes per node and per halo node) fits; false if none does.
+bool block_plan(uint32_t g, int cus, BlockPlan& p) {
+    bool found = false;
+    uint64_t best_v = ~0ull;
+    for (uint32_t nx = 1; nx <= g && nx <= (uint32_t)cus; ++nx)
+        for (uint32_t ny = 1; ny <= g && nx * ny <= (uint32_t)cus; ++ny)
+            for (uint32_t nz = 1; nz <= g && nx * ny * nz <= (uint32_t)cus; ++nz) {
+                const uint64_t bx = (g + nx - 1) / nx, by = (g + ny - 1) / ny, bz = (g + nz - 1) / nz;
+                const uint64_t v = bx * by * bz;
+                const uint64_t f = std::max(by * bz, std::max(bx * bz, bx * by));
+                const uint64_t lds = 16 * (v + 6 * f) + 2 * v + 6 * f + 64;
+                if (v > (uint64_t)BK_NPT * BK_THREADS || lds > 150 * 1024 || bx > 1023 || by > 1023 || bz > 1023)
+                    continue;
+                // estimated round time: node slots per thread (ceil(v / 1024)) plus a grid barrier
+                // (~3 slots) when there are several boxes; then the fewest boxes (less face traffic)
+                const uint64_t nbk = (uint64_t)nx * ny * nz;
+                const uint64_t key = (((v + BK_THREADS - 1) / BK_THREADS + (nbk > 1 ? 3 : 0)) << 32) | nbk;
+                if (!found || key < best_v) {
+                    found = true;
+                    best_v = key;
+                    p.nbx = nx;
+                    p.nby = ny;
+                    p.nbz = nz;
+                    p.vmax = (uint32_t)v;
+                    p.fmax = (uint32_t)f;
+                    p.lds = (uint32_t)lds;
+                }
+            }
+    return found;
+}
+
+size_t block_face_bytes(const BlockPlan& p) {
+    const size_t nb = (size_t)p.nbx * p.nby * p.nbz;
+    return 2 * nb * 6 * p.fmax * (16 + 1);
+}
+
+hipError_t launch_round_block(const DevState& S, const BlockPlan& p, uint32_t r0, uint32_t nrounds, void* face,
+                              void* scratch, hipStream_t st) {
+    BlockArgs a{};
+    const int cur = r0 & 1;
+    a.sw_in = S.sw[cur];
+    a.sw_out = S.sw[cur ^ 1];
+    a.sw_alt = S.sw[cur];
+    a.nb_in = S.nb[cur];
+    a.nb_out = S.nb[cur ^ 1];
+    a.nb_alt = S.nb[cur];
+    const size_t nb = (size_t)p.nbx * p.nby * p.nbz;
+    a.fs = static_cast<double2*>(face);
+    a.fb = reinterpret_cast<uint8_t*>(a.fs + 2 * nb * 6 * p.fmax);
+    // scratch: [0] barrier, [1] error flag, then 3 x 2 accumulators (8-byte aligned)
+    a.bar = static_cast<unsigned int*>(scratch);
+    a.err = a.bar + 1;
+    a.acc = reinterpret_cast<unsigned long long*>(a.bar + 2);
+    a.ctl = S.ctl;
+    a.G = S.G;
+    a.k0 = S.k0;
+    a.k1 = S.k1;
+    a.r0 = r0;
+    a.nrounds = nrounds;
+    a.nbx = p.nbx;
+    a.nby = p.nby;
+    a.nbz = p.nbz;
+    a.fmax = p.fmax;
+    a.vmax = p.vmax;
+    hipError_t e = hipMemsetAsync(scratch, 0, 8 + 6 * 8, st);
+    if (e != hipSuccess) return e;
+    void* args[] = {&a};
+    return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&k_ps_block), dim3((uint32_t)nb),
+                                      dim3(BK_THREADS), args, p.lds, st);
+}
+
+hipError_t block_kernel_setup(const BlockPlan& p) {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ps_block), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)p.lds);
+}
+
+}  // namespace gp

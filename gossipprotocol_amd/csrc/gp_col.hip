@@ -14,8 +14,9 @@
 // lattice costs no HBM traffic of its own.  Imp3D random-edge deliveries are
 // integer counts, so their order is free: a sender whose next direction is its
 // random edge counts the rumour at its target a round ahead (rq, an atomic) when
-// the target is on this rank; the exchange carries the others as counts to the
-// target's rank (k_pack / k_unpack, gp_xchg.hip).  No per-edge pass runs.
+// the target is on this rank; for a target on another rank it sets the edge's bit
+// in the send bitmap, and the target's rank adds the rumour (k_apply_bits,
+// gp_xchg.hip).  No per-edge pass runs.
 //
 // Work items (patch, x-segment) are dealt XCD-contiguously: the waves of one
 // XCD own one y-band of every plane, so y-halo rows come from the XCD's L2.
@@ -68,7 +69,9 @@ __device__ __forceinline__ uint32_t byte_of(uint32_t packed, int k) { return (pa
 // ---------------------------------------------------------------- gossip
 // Deliveries to j = lattice senders pointing here + Imp3D random-edge senders
 // + the injector; all dropped if j was converged at round start (Program.fs:87).
-template <int TOPO>
+// REMOTE (Imp3D slabs of a multi-rank run): a random-edge target on another rank gets
+// its rumour through the send bitmap (a.rtg names the bit, gp_xchg.hpp).
+template <int TOPO, bool REMOTE>
 __global__ __launch_bounds__(BULK_THREADS, GP_COL_MINW(TOPO)) void k_gossip_col(WaveArgs a, uint32_t r) {
     Ctl* ctl = a.ctl;
     if (ld_agent(&ctl->done)) return;
@@ -144,7 +147,7 @@ __global__ __launch_bounds__(BULK_THREADS, GP_COL_MINW(TOPO)) void k_gossip_col(
                 if (TOPO == IMP3D) {
                     lrc[k] = a.rq8 ? (uint32_t)reinterpret_cast<const uint8_t*>(a.rq_cur)[px + yo[k] - lo]
                                    : a.rq_cur[px + yo[k] - lo];
-                    lrd[k] = a.rnd[px + yo[k] - lo];
+                    lrd[k] = REMOTE ? a.rtg[px + yo[k] - lo] : a.rnd[px + yo[k] - lo];
                 }
             }
             const bool hmv = zv && y0 > 0, hpv = zv && y0 + NR < g;
@@ -206,7 +209,14 @@ __global__ __launch_bounds__(BULK_THREADS, GP_COL_MINW(TOPO)) void k_gossip_col(
                         if (a.rq8) reinterpret_cast<uint8_t*>(a.rq_cur)[j - lo] = 0u;
                         else a.rq_cur[j - lo] = 0u;
                     }
-                    if (dir == DIR_RANDOM && lrd[k] - lo < a.nloc) rq_add(a.rq_next, a.rq8, lrd[k] - lo);
+                    if (REMOTE) {  // local target (t - lo), or the edge's bit of the send bitmap
+                        if (dir == DIR_RANDOM) {
+                            if (lrd[k] & 0x80000000u) atomicOr(&a.sbits[(lrd[k] & 0x7FFFFFFFu) >> 5], 1u << (lrd[k] & 31u));
+                            else rq_add(a.rq_next, a.rq8, lrd[k]);
+                        }
+                    } else if (dir == DIR_RANDOM && lrd[k] - lo < a.nloc) {
+                        rq_add(a.rq_next, a.rq8, lrd[k] - lo);
+                    }
                 }
             }
             pb = cb;
@@ -223,13 +233,19 @@ __global__ __launch_bounds__(BULK_THREADS, GP_COL_MINW(TOPO)) void k_gossip_col(
 __global__ void k_col_seed_init(WaveArgs a, const uint8_t* nb0) {
     const uint32_t i = a.seed_node;
     if (i - a.lo >= a.nloc || (nb0[i - a.base] & DIR_MASK) != DIR_RANDOM) return;
+    if (a.rtg) {  // several ranks: a remote target's bit travels with round 0's exchange
+        const uint32_t e = a.rtg[i - a.lo];
+        if (e & 0x80000000u) atomicOr(&a.sbits[(e & 0x7FFFFFFFu) >> 5], 1u << (e & 31u));
+        else rq_add(a.rq_cur, a.rq8, e);
+        return;
+    }
     const uint32_t t = a.rnd[i - a.lo] - a.lo;
     if (t < a.nloc) rq_add(a.rq_cur, a.rq8, t);
 }
 
 int col_blocks_per_cu(int topo, int alg) {
     (void)alg;
-    const void* f = topo == GRID3D ? (const void*)k_gossip_col<GRID3D> : (const void*)k_gossip_col<IMP3D>;
+    const void* f = topo == GRID3D ? (const void*)k_gossip_col<GRID3D, false> : (const void*)k_gossip_col<IMP3D, false>;
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, BULK_THREADS, 0) != hipSuccess || n < 1) n = 1;
     return n;
@@ -241,10 +257,11 @@ hipError_t launch_round_col(const WaveArgs& a, int topo, int alg, uint32_t round
         return hipErrorInvalidValue;  // (push-sum: the tile kernel)
     } else {
         if (topo == GRID3D) {
-            hipLaunchKernelGGL(k_gossip_col<GRID3D>, g, b, 0, st, a, round);
+            hipLaunchKernelGGL((k_gossip_col<GRID3D, false>), g, b, 0, st, a, round);
         } else {
             if (!a.rq_cur || !a.rq_next || !a.rnd) return hipErrorInvalidValue;
-            hipLaunchKernelGGL(k_gossip_col<IMP3D>, g, b, 0, st, a, round);
+            if (a.rtg) hipLaunchKernelGGL((k_gossip_col<IMP3D, true>), g, b, 0, st, a, round);
+            else hipLaunchKernelGGL((k_gossip_col<IMP3D, false>), g, b, 0, st, a, round);
         }
     }
     return hipGetLastError();
@@ -275,6 +292,8 @@ WaveArgs make_wave_args(const DevState& S, uint32_t round) {
     a.rq_next = S.rq[(round + 1) & 1];
     a.rq8 = S.rq8;
     a.rnd = S.rnd;
+    a.rtg = S.rtg;
+    a.sbits = S.sbits;
     a.ctl = S.ctl;
     a.G = S.G;
     a.k0 = S.k0;

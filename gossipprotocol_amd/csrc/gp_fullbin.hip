@@ -585,6 +585,9 @@ constexpr int FBF_THREADS = GP_FBF_THREADS;
 // (reusing the fold's arrays), one reservation per (tile, bin), coalesced runs.
 // The next round then starts at B: no send pass re-reads the state (18 B/node).
 constexpr uint32_t FBF_MAXB1 = 1024;  // coarse bins the fused send can bin into (LDS reservation slots)
+#ifndef GP_FB_PF
+#define GP_FB_PF 1  // fused fold: the next tile's messages loaded during this tile's send phase
+#endif
 
 template <bool SEND>
 __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t r) {
@@ -609,17 +612,12 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
     uint32_t alerts = 0, newly = 0;
     for (uint32_t v = threadIdx.x; v < TILE; v += FBF_THREADS) cnt[v] = 0u;
     __syncthreads();
-    for (uint32_t f = blockIdx.x; f < a.nb2; f += gridDim.x) {
-        const uint32_t n = min(ld_agent(&a.cnt2[f]), (uint32_t)a.cap2);
+    // the tile's messages (sender ids, payloads) -- with GP_FB_PF, the next tile's are
+    // loaded while this tile's messages of round r+1 are scattered and written out
+    uint32_t snd[FQ];
+    double ps[FQ], pw[FQ];  // (two scalar arrays: a double2 array here went to scratch)
+    auto load_msgs = [&](uint32_t f, uint32_t n) {
         const size_t base = (size_t)f * a.cap2;
-        // every load of the tile in flight at once (indices clamped, validity at use)
-        uint32_t snd[FQ], x[FQ], y[FQ], vr[FQ], rk[FQ];
-        double ps[FQ], pw[FQ];  // (two scalar arrays: a double2 array here went to scratch)
-        uint8_t bk[NPT];
-        double2 svk[NPT];
-        uint32_t nfl[NPT];  // fused send: active in round r+1, and the half it sends
-        double2 nsw[NPT];
-        fb_prio_fold_loads<2>();
 #pragma unroll
         for (int k = 0; k < FQ; ++k) {
             const uint32_t q = min((uint32_t)(k * FBF_THREADS + threadIdx.x), n > 0 ? n - 1 : 0u);
@@ -628,6 +626,26 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
             ps[k] = m.x;
             pw[k] = m.y;
         }
+    };
+    uint32_t n_pf = 0;
+    if (GP_FB_PF && SEND && blockIdx.x < a.nb2) {
+        n_pf = min(ld_agent(&a.cnt2[blockIdx.x]), (uint32_t)a.cap2);
+        load_msgs(blockIdx.x, n_pf);
+    }
+    for (uint32_t f = blockIdx.x; f < a.nb2; f += gridDim.x) {
+        const bool pf = GP_FB_PF && SEND;
+        const uint32_t n = pf ? n_pf : min(ld_agent(&a.cnt2[f]), (uint32_t)a.cap2);
+        // the next tile's message count, early (a scalar load; its messages are loaded later)
+        const uint32_t fn = f + gridDim.x;
+        if (pf) n_pf = fn < a.nb2 ? min(ld_agent(&a.cnt2[fn]), (uint32_t)a.cap2) : 0u;
+        // every load of the tile in flight at once (indices clamped, validity at use)
+        uint32_t x[FQ], y[FQ], vr[FQ], rk[FQ];
+        uint8_t bk[NPT];
+        double2 svk[NPT];
+        uint32_t nfl[NPT];  // fused send: active in round r+1, and the half it sends
+        double2 nsw[NPT];
+        fb_prio_fold_loads<2>();
+        if (!pf) load_msgs(f, n);
 #pragma unroll
         for (int k = 0; k < NPT; ++k) {
             const uint32_t j = min(f * TILE + k * FBF_THREADS + threadIdx.x, a.nloc - 1);
@@ -748,6 +766,13 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
             if (q0 < a.nb1) {
                 const uint32_t n = (q0 + 1 < a.nb1 ? cnt[q0 + 1] : total) - cnt[q0];
                 if (n) res = atomicAdd(&a.cnt1[q0], n);
+            }
+            // the next tile's messages, issued after the reservation (so that waiting for its
+            // result does not wait for them) and in flight through the scatter and write-out
+            if (GP_FB_PF && fn < a.nb2) {
+                fb_prio<2>();
+                load_msgs(fn, n_pf);
+                fb_prio<0>();
             }
 #pragma unroll
             for (int k = 0; k < NPT; ++k) {

@@ -128,6 +128,22 @@ __device__ inline void rq_add(uint32_t* rq, uint32_t rq8, uint32_t t) {
     else atomicAdd(&rq[t], 1u);
 }
 
+// Imp3D push-sum across ranks (gp_xchg.hpp, sender-ordered lists): one header word
+// of a received list, 64 entries.
+struct XHdr {
+    unsigned long long mask;   // bit: the entry's sender used its random edge this round
+    uint32_t base;             // vals index of the word's first used entry (this rank's vals region)
+    uint32_t pad;
+};
+static_assert(sizeof(XHdr) == 16, "header words move as 16-byte loads");
+
+// KERNEL_BLOCK (gp_block.hip): the lattice cut into nbx * nby * nbz boxes, one per workgroup.
+struct BlockPlan {
+    uint32_t nbx, nby, nbz;  // boxes per axis
+    uint32_t vmax, fmax;     // largest box (nodes) and largest face
+    uint32_t lds;            // dynamic LDS bytes per workgroup
+};
+
 // Node state in HBM (structure of arrays, single GPU / one slab).
 struct DevState {
     Geom G;
@@ -146,6 +162,11 @@ struct DevState {
     // k_unpack) and read (then zeroed) by the receiver
     uint32_t* rq[2];
     uint32_t rq8;         // rq holds one byte per node (four per word) instead of one word
+    // gossip column kernel across ranks (gp_xchg.hpp, bitmaps): per local sender its
+    // random edge's local target (t - lo) or 0x80000000 | its bit in sbits, the send
+    // bitmap of the round being prepared
+    uint32_t* rtg;
+    uint32_t* sbits;
     // Imp3D: bit i of rbits[b] = node i sends on its random edge in the round
     // of buffer b (ballot-packed by the round kernel)
     uint64_t* rbits[2];
@@ -178,6 +199,13 @@ struct DevState {
     // round tag (the round the message was delivered for) and the message
     uint32_t* rtag;
     double2* rmsg;
+    // Imp3D push-sum across ranks (sender-ordered lists, gp_xchg.hpp): per local in-edge
+    // whose sender lives on another rank, its list key (64 * header word + bit) in this
+    // rank's received header region; the received headers and messages of the round
+    uint32_t* rk;
+    const XHdr* xhdr;
+    const double2* xvals;
+    uint32_t xnv;  // message slots in the vals region
     int kernel;  // KERNEL_* below
     // column kernels: x segments per patch (set at create from the resident grid)
     uint32_t col_xsegs;
@@ -185,6 +213,9 @@ struct DevState {
     uint32_t tile_wx;    // RoundArgs::wx
     uint32_t tile_stage_cap;  // RoundArgs::stage_cap (experiments build only; default: no limit)
     uint32_t fuse_finalize;   // the round kernel closes its own round (single rank push-sum)
+    BlockPlan bplan;          // KERNEL_BLOCK (gp_block.hip): boxes, face buffer, barrier scratch
+    void* bface;
+    void* bscratch;
     uint32_t tile_wide;       // KERNEL_TILE: the 1024-thread size class (gp_round_wide.hip)
     // Imp3D: the rank's in-edge count
     uint32_t nedges;
@@ -210,8 +241,12 @@ struct RoundArgs {
     const uint32_t* in_src;
     const uint32_t* in_srcd; // in_src with the sender's deg - 4 in bits 30-31, or null
     const uint8_t* ind4;     // nibble in-degrees (DevState::ind4), offset so that ind4 + j / 2 is node j's byte
-    const uint32_t* rtag;    // per local in-edge: round of the delivered remote message
+    const uint32_t* rtag;    // per local in-edge: round of the delivered remote message (gossip)
     const double2* rmsg;
+    const uint32_t* rk;      // push-sum: per local in-edge, the remote sender's list key (DevState::rk)
+    const XHdr* xhdr;        // push-sum: the received header words / messages of the round
+    const double2* xvals;
+    uint32_t xnv;
     int32_t* c;              // indexed by global id
     Ctl* ctl;
     Geom G;
@@ -228,7 +263,17 @@ struct RoundArgs {
     uint32_t* tq_next;   // walk 3: the next round's counters, zeroed by block 0 this round
 };
 
-enum KernelVariant : int { KERNEL_TILE = 1, KERNEL_COL = 2 };
+enum KernelVariant : int { KERNEL_TILE = 1, KERNEL_COL = 2, KERNEL_BLOCK = 3 };
+
+// ---- LDS-resident push-sum on a small 3D lattice (gp_block.hip): one cooperative launch
+// per batch of rounds (BlockPlan above DevState)
+bool block_plan(uint32_t g, int cus, BlockPlan& p);
+size_t block_face_bytes(const BlockPlan& p);
+hipError_t block_kernel_setup(const BlockPlan& p);
+// rounds [r0, r0 + nrounds) (fewer once the cumulative alerts reach T); scratch: 64 bytes,
+// word 1 is set if a grid barrier timed out
+hipError_t launch_round_block(const struct DevState& S, const BlockPlan& p, uint32_t r0, uint32_t nrounds, void* face,
+                              void* scratch, hipStream_t st);
 
 // Arguments of the column-march gossip kernels (gp_col.hip).
 struct WaveArgs {
@@ -247,6 +292,8 @@ struct WaveArgs {
     uint32_t* rq_next;       // next round's, counted by local senders with atomics (remote ones: k_unpack)
     uint32_t rq8;            // byte counters (DevState::rq8)
     const uint32_t* rnd;     // random edge of each local sender (id - lo)
+    const uint32_t* rtg;     // several ranks: local target or send-bitmap bit of it (DevState::rtg)
+    uint32_t* sbits;
     Ctl* ctl;
     Geom G;
     uint32_t k0, k1, seed_node;

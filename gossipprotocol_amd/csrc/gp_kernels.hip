@@ -401,6 +401,7 @@ const char* bulk_kernel_name(const DevState& S) {
                                    {"k_gossip_tile<LINE>", "k_full_gossip_send+recv", "k_gossip_col<GRID3D>",
                                     "k_gossip_col<IMP3D>"}};
     if (S.topo == FULL && S.alg == PUSHSUM && S.fb_fused) return "k_fb_split+fold<send>";  // one rank, fused
+    if (S.kernel == KERNEL_BLOCK) return "k_ps_block<GRID3D>";  // LDS-resident, one launch per batch
     const int v = S.kernel == KERNEL_COL ? 1 : 0;
     if (v == 0 && S.tile_wide && S.topo != FULL) {  // the 1024-thread size class (gp_round_wide.hip)
         static const char* w[2][4] = {{"wide::k_gossip_tile<LINE>", "", "wide::k_gossip_tile<GRID3D>",

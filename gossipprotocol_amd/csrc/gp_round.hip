@@ -82,6 +82,9 @@ namespace wide {
 #ifndef GP_NG
 #define GP_NG 1          // push-sum tile kernel: node slots whose loads are in flight together
 #endif
+#ifndef GP_RK_EARLY
+#define GP_RK_EARLY 0    // REMOTE push-sum: list keys loaded with the in-edge senders (before the draws)
+#endif
 #ifndef GP_MINB
 #define GP_MINB 5  // __launch_bounds__ minimum waves per SIMD (= resident 256-thread blocks per CU):
                    // the LDS tile allows 5, so keep VGPRs <= 96 to not lose the fifth
@@ -464,8 +467,20 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                     const uint32_t q = threadIdx.x + m * TPB;
                     raw[m] = q < cnt ? __builtin_nontemporal_load(srcp + e_lo + q) : 0u;
                 }
+                uint32_t rkv[REMOTE ? FU : 1];
+#if GP_RK_EARLY
+                // REMOTE: the list keys of the tile's in-edges (meaningful for remote senders),
+                // streamed with the senders
+                if constexpr (REMOTE) {
+#pragma unroll
+                    for (int m = 0; m < FU; ++m) {
+                        const uint32_t q = threadIdx.x + m * TPB;
+                        rkv[m] = q < cnt ? __builtin_nontemporal_load(a.rk + e_lo + q) : 0u;
+                    }
+                }
+#endif
                 uint32_t isrc[FU];
-                bool sent[FU];
+                bool sent[FU], pick[FU];
 #pragma unroll
                 for (int m = 0; m < FU; ++m) isrc[m] = packed ? raw[m] & 0x3FFFFFFFu : raw[m];
                 if (all_active) {
@@ -499,7 +514,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                     for (int m = 0; m < FU; ++m) {
                         const uint32_t q = threadIdx.x + m * TPB;
                         const uint32_t di = packed ? (raw[m] >> 30) + 4u : popc6(present_mask<IMP3D>(isrc[m], G)) + 1u;
-                        sent[m] = q < cnt && uniform_from(x[m], y[m], di) == di - 1u;
+                        sent[m] = pick[m] = q < cnt && uniform_from(x[m], y[m], di) == di - 1u;
                     }
                 } else {
                     // activation: the sender sends on its random edge iff its draw picks
@@ -511,33 +526,63 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                     // picks first, then every pick's bitmap word in flight together: loads
                     // unconditional (non-picks read the slab's first word, one shared line),
                     // since under a branch each load was waited on at once
-                    bool pick[FU];
+                    bool lpick[FU];
 #pragma unroll
                     for (int m = 0; m < FU; ++m) {
                         const uint32_t q = threadIdx.x + m * TPB;
                         const uint32_t i = isrc[m];
                         const uint32_t di = packed ? (raw[m] >> 30) + 4u : popc6(present_mask<IMP3D>(i, G)) + 1u;
-                        pick[m] = q < cnt && (!REMOTE || i - a.lo < a.nloc) && uniform_from(x[m], y[m], di) == di - 1u;
+                        pick[m] = q < cnt && uniform_from(x[m], y[m], di) == di - 1u;
+                        lpick[m] = pick[m] && (!REMOTE || i - a.lo < a.nloc);
                     }
                     unsigned long long wbits[FU];
 #pragma unroll
-                    for (int m = 0; m < FU; ++m) wbits[m] = rbc[pick[m] ? (isrc[m] >> 6) - (a.lo >> 6) : 0u];
+                    for (int m = 0; m < FU; ++m) wbits[m] = rbc[lpick[m] ? (isrc[m] >> 6) - (a.lo >> 6) : 0u];
                     // (the asm consumes every loaded word, so no load can be sunk into a
                     // branch on pick; its memory clobber keeps all loads ahead of the first)
 #pragma unroll
                     for (int m = 0; m < FU; ++m) asm volatile("" : "+v"(wbits[m])::"memory");
 #pragma unroll
-                    for (int m = 0; m < FU; ++m) wbits[m] = pick[m] ? wbits[m] : 0ull;
+                    for (int m = 0; m < FU; ++m) wbits[m] = lpick[m] ? wbits[m] : 0ull;
 #pragma unroll
                     for (int m = 0; m < FU; ++m) sent[m] = (wbits[m] >> (isrc[m] & 63)) & 1ull;
                 }
-                // sender on another rank, activation phase: the exchange tagged its message
-                // (every node active: its Philox draw above decides, like a local sender's)
-                if (REMOTE && !all_active) {
+                // sender on another rank: its rank's list for this one says whether it used the
+                // edge (the header word's bit) and where its message is (the word's base +
+                // the used entries below it).  Only the drawn / picked edges (~1/7) read a
+                // header word; the others load word 0 (one shared line), unconditionally,
+                // so no load waits under a branch.
+                uint32_t ridx[REMOTE ? FU : 1];
+                if constexpr (REMOTE) {
+#if !GP_RK_EARLY
+                    // the list keys of the tile's in-edges (meaningful for remote senders), after
+                    // the draws: live across the Philox batch they cost spills
 #pragma unroll
                     for (int m = 0; m < FU; ++m) {
                         const uint32_t q = threadIdx.x + m * TPB;
-                        if (q < cnt && isrc[m] - a.lo >= a.nloc) sent[m] = a.rtag[e_lo + q] == r;
+                        rkv[m] = q < cnt ? __builtin_nontemporal_load(a.rk + e_lo + q) : 0u;
+                    }
+#endif
+                    uint2 hm[FU];
+                    uint32_t hb[FU];
+#pragma unroll
+                    for (int m = 0; m < FU; ++m) {
+                        const bool cand = pick[m] && isrc[m] - a.lo >= a.nloc;
+                        const XHdr* hp = a.xhdr + (cand ? rkv[m] >> 6 : 0u);
+                        hm[m] = *reinterpret_cast<const uint2*>(&hp->mask);
+                        hb[m] = hp->base;
+                    }
+#pragma unroll
+                    for (int m = 0; m < FU; ++m) asm volatile("" : "+v"(hm[m].x), "+v"(hm[m].y), "+v"(hb[m])::"memory");
+#pragma unroll
+                    for (int m = 0; m < FU; ++m) {
+                        ridx[m] = 0u;
+                        if (pick[m] && isrc[m] - a.lo >= a.nloc) {
+                            const unsigned long long mk = ((unsigned long long)hm[m].y << 32) | hm[m].x;
+                            const uint32_t bit = rkv[m] & 63u;
+                            sent[m] = (mk >> bit) & 1ull;
+                            ridx[m] = min(hb[m] + (uint32_t)__popcll(mk & ((1ull << bit) - 1ull)), a.xnv - 1u);
+                        }
                     }
                 }
                 if (GP_SETPRIO >= 2) __builtin_amdgcn_s_setprio(GP_PRIO);
@@ -546,12 +591,16 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                     const unsigned long long bal = __ballot(sent[m]);
                     if (lane == 0) L.bits[m * (TPB / 64) + wv] = bal;
                     if (sent[m]) {
-                        const uint32_t q = threadIdx.x + m * TPB;
-                        // (the edge index opaque: hoisted out of the tile loop, the five per-lane
-                        // rmsg + q addresses were spilled, and each reload waited vmcnt(0))
-                        uint32_t eq = e_lo + q;
-                        if (REMOTE) asm volatile("" : "+v"(eq));
-                        const double2* src = (REMOTE && isrc[m] - a.lo >= a.nloc) ? a.rmsg + eq : swc + isrc[m];
+                        const double2* src;
+                        if constexpr (REMOTE) {
+                            // (the index opaque: hoisted out of the tile loop, per-lane addresses
+                            // were spilled, and each reload waited vmcnt(0))
+                            uint32_t xi = ridx[m];
+                            asm volatile("" : "+v"(xi));
+                            src = isrc[m] - a.lo >= a.nloc ? a.xvals + xi : swc + isrc[m];
+                        } else {
+                            src = swc + isrc[m];
+                        }
                         __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(L.msg + (m * TPB + wv * 64)), 16,
                                                          0, DMA_ONCE);
                     }
@@ -830,15 +879,20 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                                     bool sent;
                                     double2 mi = make_double2(0.0, 0.0);
                                     const bool rem = REMOTE && i - a.lo >= a.nloc;
-                                    if (all_active) {
+                                    uint32_t xi = 0;
+                                    if (rem) {  // the sender's list entry (see the in-edge pass)
+                                        const uint32_t k = a.rk[e];
+                                        const XHdr h = a.xhdr[k >> 6];
+                                        sent = (h.mask >> (k & 63u)) & 1ull;
+                                        xi = min(h.base + (uint32_t)__popcll(h.mask & ((1ull << (k & 63u)) - 1ull)),
+                                                 a.xnv - 1u);
+                                    } else if (all_active) {
                                         const uint32_t di = popc6(present_mask<IMP3D>(i, G)) + 1u;
                                         sent = uniform(a.k0, a.k1, S_PUSHSUM, i, r, di) == di - 1u;
-                                    } else if (rem) {
-                                        sent = a.rtag[e] == r;
                                     } else {
                                         sent = (rbc[(i >> 6) - (a.lo >> 6)] >> (i & 63)) & 1ull;
                                     }
-                                    if (sent) mi = rem ? a.rmsg[e] : ld_sw(swc + i);
+                                    if (sent) mi = rem ? a.xvals[xi] : ld_sw(swc + i);
                                     if (sent) {
                                         fold(mi);
                                         recv = true;
@@ -1200,6 +1254,10 @@ RoundArgs make_round_args(const DevState& S, uint32_t round) {
     a.ind4 = S.ind4 ? S.ind4 - (S.lo / TILE) * (TILE / 2) : nullptr;
     a.rtag = S.rtag;
     a.rmsg = S.rmsg;
+    a.rk = S.rk;
+    a.xhdr = S.xhdr;
+    a.xvals = S.xvals;
+    a.xnv = S.xnv;
     a.c = S.c ? S.c - S.lo : nullptr;
     a.lo = S.lo;
     a.nloc = S.nloc;
@@ -1271,7 +1329,8 @@ int ps_tile_resident_blocks(int topo, bool remote, int device) {
 hipError_t launch_round_tile(const DevState& S, uint32_t round, int grid, hipStream_t st) {
     const RoundArgs a = make_round_args(S, round);
     const dim3 g(grid), b(TPB);
-    const bool remote = S.rtag != nullptr;  // Imp3D slabs of a multi-rank run
+    // Imp3D slabs of a multi-rank run (push-sum: received lists; gossip: tagged slots)
+    const bool remote = S.alg == PUSHSUM ? S.rk != nullptr : S.rtag != nullptr;
     if (S.alg == PUSHSUM && S.topo == IMP3D && !S.ind4) return hipErrorInvalidValue;
     if (S.alg == PUSHSUM) {
         switch (S.topo) {

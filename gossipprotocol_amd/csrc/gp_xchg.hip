@@ -31,6 +31,11 @@ __device__ __forceinline__ uint32_t owner_of(uint32_t t, const uint32_t* bounds,
     return (uint32_t)o;
 }
 
+struct SlabTable {
+    uint32_t v[XMAXW + 1];
+    int W;
+};
+
 }  // namespace
 
 // Range binning: a block owns PACK_RANGE consecutive senders.  Sweep 1 finds
@@ -206,6 +211,330 @@ __global__ __launch_bounds__(256) void k_unpack(UnpackArgs a, uint32_t round) {
     }
 }
 
+// ---------------------------------------------------------------- sender-ordered lists
+// (Imp3D push-sum across ranks, round 5; gp_xchg.hpp).  A tile is XTILE = 1024 ids on
+// a global multiple of XTILE, node slot k of thread t = id T + 256 k + t (the layout of
+// the push-sum tile kernel).
+namespace {
+
+__device__ __forceinline__ uint32_t lane_below(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+struct RankLds {
+    uint32_t c[4][4][XMAXW];  // [slot][wave][destination]: counts, then exclusive offsets
+    uint32_t tot[XMAXW];      // the tile's list entries per destination
+};
+
+// rho[k]: rank of node slot k among the tile's list entries with the same destination,
+// in id order; dst[k] < W, or XNONE for no entry.  256 threads; two barriers.
+__device__ __forceinline__ void tile_list_rank(const uint32_t (&dst)[4], uint32_t (&rho)[4], RankLds& R, int W) {
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        rho[k] = 0u;
+        for (int d = 0; d < W; ++d) {  // W is uniform
+            const unsigned long long m = __ballot(dst[k] == (uint32_t)d);
+            if (dst[k] == (uint32_t)d) rho[k] = lane_below(m);
+            if (lane == 0) R.c[k][wv][d] = (uint32_t)__popcll(m);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < (uint32_t)W) {
+        const uint32_t d = threadIdx.x;
+        uint32_t o = 0;
+        for (int k = 0; k < 4; ++k)
+            for (int w = 0; w < 4; ++w) {
+                const uint32_t c = R.c[k][w][d];
+                R.c[k][w][d] = o;
+                o += c;
+            }
+        R.tot[d] = o;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (dst[k] != XNONE) rho[k] += R.c[k][wv][dst[k]];
+}
+
+struct TileSpan {
+    uint32_t T, j0, j1;
+};
+__device__ __forceinline__ TileSpan tile_span(uint32_t lo, uint32_t nloc, uint32_t t) {
+    TileSpan s;
+    s.T = (lo / XTILE + t) * XTILE;
+    s.j0 = max(lo, s.T);
+    s.j1 = min(lo + nloc, s.T + XTILE);
+    return s;
+}
+
+}  // namespace
+
+// Setup, slab a: list entries per (tile, destination).  One block per tile.
+__global__ __launch_bounds__(256) void k_list_count(ListCountArgs a) {
+    __shared__ uint32_t c[XMAXW];
+    if (threadIdx.x < XMAXW) c[threadIdx.x] = 0u;
+    __syncthreads();
+    const TileSpan sp = tile_span(a.lo, a.nloc, blockIdx.x);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t j = sp.T + k * 256u + threadIdx.x;
+        if (j >= sp.j0 && j < sp.j1) {
+            const uint32_t d = owner_of(a.rnd[j], a.bounds, a.W);
+            if (d != (uint32_t)a.a) atomicAdd(&c[d], 1u);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < (uint32_t)a.W) a.cnt[(size_t)blockIdx.x * a.W + threadIdx.x] = c[threadIdx.x];
+}
+
+// Setup, slab a: key[i] = 64 * (header word of i's list entry in its destination's header
+// region) + its bit, for every sender i of the slab whose random edge leaves the slab.
+__global__ __launch_bounds__(256) void k_list_key(ListKeyArgs a) {
+    __shared__ RankLds R;
+    const uint32_t t = blockIdx.x;
+    const TileSpan sp = tile_span(a.lo, a.nloc, t);
+    uint32_t dst[4], rho[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t j = sp.T + k * 256u + threadIdx.x;
+        dst[k] = XNONE;
+        if (j >= sp.j0 && j < sp.j1) {
+            const uint32_t d = owner_of(a.rnd[j], a.bounds, a.W);
+            if (d != (uint32_t)a.a) dst[k] = d;
+        }
+    }
+    tile_list_rank(dst, rho, R, a.W);
+    const int h = t < a.tsplit ? 0 : 1;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (dst[k] != XNONE)
+            a.key[sp.T + k * 256u + threadIdx.x] =
+                (a.hw[h][dst[k]] + a.gw[(size_t)t * a.W + dst[k]]) * 64u + rho[k];
+}
+
+// One round, one region: the header words and the compacted messages of every
+// destination.  A block of LP_TILES waves takes LP_TILES consecutive tiles (8192
+// senders), one per wave, walked as 16 slots of 64 consecutive ids: a node's rank among the
+// tile's entries of its destination is the wave's running count (scalar) plus the
+// lanes below in the slot's ballot -- no LDS table, no barrier per tile.  The used
+// entries' bits go into the wave's LDS words, the wave scans the words' counts; then,
+// for all the block's tiles at once, ONE reservation per destination (a reservation
+// per tile queued ~60 k returning atomics on each of a C5 slab's 14 counters per
+// round: 0.73 ms per region at W = 8), the header words and the messages in list
+// order.  Two barriers per block.
+constexpr int LIST_LW = XTILE / 64 + XMAXW;  // LDS words of one tile's segments (<= 16 full + 1 partial each)
+constexpr int LP_TILES = 8;                  // = waves per block
+constexpr int LP_WT = 1;                     // tiles per wave
+constexpr int LP_THREADS = 64 * LP_TILES / LP_WT;
+constexpr int LP_SLOTS = XTILE / 64;         // 64-id slots per tile
+__global__ __launch_bounds__(LP_THREADS) void k_list_pack(ListPackArgs a) {
+    __shared__ uint32_t mk[LP_TILES][2 * LIST_LW];  // the segments' bitmaps, 64 bits per word
+    __shared__ uint32_t wb[LP_TILES][LIST_LW];      // used entries before the word in its tile's run
+    __shared__ uint32_t lw[LP_TILES][XMAXW + 1];    // first LDS word of each destination's segment
+    __shared__ uint32_t tn[LP_TILES][XMAXW];        // used entries per (tile, destination), then run offsets
+    __shared__ uint32_t off[XMAXW];                 // the block's reserved run in each destination's chunk
+    __shared__ double2* ovals[XMAXW];
+    __shared__ uint32_t ocap[XMAXW];
+    const uint32_t tb = a.t0 + blockIdx.x * LP_TILES;
+    if (tb >= a.t1) return;
+    const int ntl = (int)min((uint32_t)LP_TILES, a.t1 - tb);
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t me = (uint32_t)a.me;
+    const int W = a.W;
+    for (uint32_t q = threadIdx.x; q < LP_TILES * 2 * LIST_LW; q += LP_THREADS) (&mk[0][0])[q] = 0u;
+    if (threadIdx.x < (uint32_t)W) {
+        ovals[threadIdx.x] = a.peer[threadIdx.x].vals;
+        ocap[threadIdx.x] = a.peer[threadIdx.x].cap;
+    }
+    __syncthreads();
+    // per tile of this wave and slot pair: used ? 0x8000 | d << 11 | rho : 0 (rho < 1024), 16 bits a slot
+    uint32_t st[LP_WT][LP_SLOTS / 2];
+#pragma unroll
+    for (int u = 0; u < LP_WT; ++u) {
+#pragma unroll
+        for (int q = 0; q < LP_SLOTS / 2; ++q) st[u][q] = 0u;
+        const int tt = (int)wv * LP_WT + u;
+        if (tt >= ntl) break;  // (wave-uniform)
+        const TileSpan sp = tile_span(a.lo, a.nloc, tb + tt);
+        uint8_t b[LP_SLOTS], x[LP_SLOTS];
+        xchg_prio<1>();
+#pragma unroll
+        for (int q = 0; q < LP_SLOTS; ++q) {  // unconditional (clamped) loads, all in flight
+            const uint32_t j = min(max(sp.T + q * 64u + lane, sp.j0), sp.j1 - 1u);
+            b[q] = a.nbn[j - a.base];
+            x[q] = a.xdst[j - a.lo];
+        }
+        xchg_prio<0>();
+        uint32_t run[XMAXW];  // the tile's entries per destination so far (wave-uniform)
+#pragma unroll
+        for (int d = 0; d < XMAXW; ++d) run[d] = 0u;
+#pragma unroll
+        for (int q = 0; q < LP_SLOTS; ++q) {
+            const uint32_t j = sp.T + q * 64u + lane;
+            const bool in = j >= sp.j0 && j < sp.j1 && x[q] != me;
+            const uint32_t dst = in ? (uint32_t)x[q] : XNONE;
+            uint32_t rho = 0;
+#pragma unroll
+            for (int d = 0; d < XMAXW; ++d)
+                if (d < W) {
+                    const unsigned long long m = __ballot(dst == (uint32_t)d);
+                    if (dst == (uint32_t)d) rho = run[d] + lane_below(m);
+                    run[d] += (uint32_t)__popcll(m);
+                }
+            if (in && (b[q] & DIR_MASK) == DIR_RANDOM) st[u][q >> 1] |= (0x8000u | (dst << 11) | rho) << (16 * (q & 1));
+        }
+        // the tile's segments: destination d's words from lw[tt][d] (ceil(entries / 64))
+        uint32_t w0 = 0;
+#pragma unroll
+        for (int d = 0; d < XMAXW; ++d)
+            if (d < W) {
+                if (lane == (uint32_t)d) lw[tt][d] = w0;
+                w0 += (run[d] + 63u) / 64u;
+            }
+        if (lane == 0) lw[tt][W] = w0;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int q = 0; q < LP_SLOTS; ++q) {
+            const uint32_t e = (st[u][q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
+            if (e & 0x8000u) {
+                const uint32_t d = (e >> 11) & 15u, rho = e & 0x7FFu;
+                const uint32_t w = lw[tt][d] + (rho >> 6);
+                atomicOr(&mk[tt][2 * w + ((rho >> 5) & 1u)], 1u << (rho & 31u));
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        // word prefixes within each destination's segment, and the tile's used entries per destination
+        const uint32_t nw = w0;  // <= LIST_LW <= 64: one wave-wide scan
+        const uint32_t l = lane;
+        uint32_t seg = 0;
+        for (int d = 1; d < W; ++d) seg += l >= lw[tt][d] ? 1u : 0u;
+        const unsigned long long m = l < nw ? ((unsigned long long)mk[tt][2 * l + 1] << 32) | mk[tt][2 * l] : 0ull;
+        const uint32_t p = (uint32_t)__popcll(m);
+        uint32_t incl = p;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t v = __shfl_up(incl, o, 64);
+            if (l >= (uint32_t)o) incl += v;
+        }
+        const uint32_t s0 = lw[tt][seg];
+        const uint32_t before = __shfl(incl, (int)(s0 > 0 ? s0 - 1 : 0), 64);
+        if (l < nw) wb[tt][l] = incl - p - (s0 > 0 ? before : 0u);
+        const uint32_t dl = min(l, (uint32_t)W - 1u);
+        const uint32_t e0 = lw[tt][dl], e1 = lw[tt][dl + 1];
+        const uint32_t a1 = __shfl(incl, (int)(e1 > 0 ? e1 - 1 : 0), 64);
+        const uint32_t a0 = __shfl(incl, (int)(e0 > 0 ? e0 - 1 : 0), 64);
+        if (l < (uint32_t)W) tn[tt][l] = e1 > e0 ? a1 - (e0 > 0 ? a0 : 0u) : 0u;
+    }
+    __syncthreads();
+    if (threadIdx.x < (uint32_t)W) {  // the block's run per destination: one reservation
+        const uint32_t d = threadIdx.x;
+        uint32_t r = 0;
+        for (int tt = 0; tt < ntl; ++tt) {
+            const uint32_t c = tn[tt][d];
+            tn[tt][d] = r;
+            r += c;
+        }
+        off[d] = d != me && r ? atomicAdd(a.peer[d].cnt, r) : 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < LP_WT; ++u) {
+        const int tt = (int)wv * LP_WT + u;
+        if (tt >= ntl) break;
+        const TileSpan sp = tile_span(a.lo, a.nloc, tb + tt);
+        {  // header words (lane = word)
+            const uint32_t l = lane;
+            if (l < lw[tt][W]) {
+                uint32_t seg = 0;
+                for (int d = 1; d < W; ++d) seg += l >= lw[tt][d] ? 1u : 0u;
+                XHdr h;
+                h.mask = ((unsigned long long)mk[tt][2 * l + 1] << 32) | mk[tt][2 * l];
+                h.base = a.peer[seg].vbase + off[seg] + tn[tt][seg] + wb[tt][l];
+                h.pad = 0u;
+                a.peer[seg].hdr[a.gw[(size_t)(tb + tt) * W + seg] + (l - lw[tt][seg])] = h;
+            }
+        }
+        // the used entries' (s, w): buffer loads over the tile's ids, past the end for the
+        // others (no memory touched, no load under a branch), four slots in flight
+        const __amdgpu_buffer_rsrc_t rs = buf_rsrc(a.swn + (sp.j0 - a.base), (sp.j1 - sp.j0) * 16u);
+#pragma unroll
+        for (int q0 = 0; q0 < LP_SLOTS; q0 += 4) {
+            double2 v[4];
+            xchg_prio<1>();
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                const int q = q0 + h;
+                const uint32_t j = sp.T + q * 64u + lane;
+                const bool used = (st[u][q >> 1] >> (16 * (q & 1))) & 0x8000u;
+                const auto w4 = __builtin_amdgcn_raw_buffer_load_b128(rs, used ? (j - sp.j0) * 16u : BUF_NONE, 0, 0);
+                v[h] = __builtin_bit_cast(double2, w4);
+            }
+            xchg_prio<0>();
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                const int q = q0 + h;
+                const uint32_t e = (st[u][q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
+                if (!(e & 0x8000u)) continue;
+                const uint32_t d = (e >> 11) & 15u, rho = e & 0x7FFu;
+                const uint32_t w = lw[tt][d] + (rho >> 6), bit = rho & 63u;
+                const unsigned long long m = ((unsigned long long)mk[tt][2 * w + 1] << 32) | mk[tt][2 * w];
+                const uint32_t idx = off[d] + tn[tt][d] + wb[tt][w] + (uint32_t)__popcll(m & ((1ull << bit) - 1ull));
+                if (idx < ocap[d]) ovals[d][idx] = v[h];
+                else atomicOr(a.overflow, 1u);
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_gather_keys(const uint32_t* __restrict__ key, const uint32_t* __restrict__ src,
+                                                     uint32_t n, uint32_t* __restrict__ out) {
+    for (uint32_t e = blockIdx.x * 256 + threadIdx.x; e < n; e += gridDim.x * 256) out[e] = key[src[e]];
+}
+
+// ---------------------------------------------------------------- gossip bitmaps (setup + apply)
+__global__ __launch_bounds__(256) void k_src_flag(const uint32_t* __restrict__ src, uint32_t n, SlabTable b, int a,
+                                                  uint32_t* __restrict__ flag) {
+    for (uint32_t q = blockIdx.x * 256 + threadIdx.x; q <= n; q += gridDim.x * 256)
+        flag[q] = q < n && owner_of(src[q], b.v, b.W) == (uint32_t)a ? 1u : 0u;
+}
+
+// pos[q] for the edges q whose sender is on slab a: their rank among the edges of the
+// same receiver slab with a sender on a, in receiver order.
+__global__ __launch_bounds__(256) void k_bits_pos(BitsSetupArgs a) {
+    for (uint32_t q = blockIdx.x * 256 + threadIdx.x; q < a.n; q += gridDim.x * 256) {
+        if (owner_of(a.src[q], a.bounds, a.W) != (uint32_t)a.a) continue;
+        const uint32_t b = owner_of(a.recv[q], a.bounds, a.W);
+        a.pos[q] = a.scan[q] - a.scan[a.edge0[b]];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_bits_ends(BitsEndsArgs a) {
+    for (uint32_t li = blockIdx.x * 256 + threadIdx.x; li < a.nloc; li += gridDim.x * 256) {
+        const uint32_t t = a.rnd[li];
+        const uint32_t d = owner_of(t, a.bounds, a.W);
+        a.rtg[li] = d == (uint32_t)a.me ? t - a.lo : 0x80000000u | (a.bo[d] + a.pos[a.inv[a.lo + li]]);
+    }
+    for (uint32_t q = a.e0 + blockIdx.x * 256 + threadIdx.x; q < a.e1; q += gridDim.x * 256) {
+        const uint32_t s = owner_of(a.src[q], a.bounds, a.W);
+        if (s != (uint32_t)a.me) a.tgt[a.ro[s] + a.pos[q]] = a.recv[q] - a.lo;
+    }
+}
+
+// One rumour for next round per set bit of the received bitmaps (Program.fs:84-89: the
+// sender's Tell to its random neighbour), at the bit's target.
+__global__ __launch_bounds__(256) void k_apply_bits(const uint32_t* __restrict__ bits, uint32_t nwords,
+                                                    const uint32_t* __restrict__ tgt, uint32_t* rq, uint32_t rq8) {
+    for (uint32_t w = blockIdx.x * 256 + threadIdx.x; w < nwords; w += gridDim.x * 256) {
+        uint32_t m = bits[w];
+        while (m) {
+            const uint32_t b = (uint32_t)__builtin_ctz(m);
+            m &= m - 1u;
+            rq_add(rq, rq8, tgt[w * 32u + b]);
+        }
+    }
+}
+
 __global__ void k_zero_counts(ZeroArgs z) {
     const int p = threadIdx.x;
     if (p < z.n && z.cnt[p]) *z.cnt[p] = 0u;
@@ -285,6 +614,48 @@ hipError_t launch_unpack(const UnpackArgs& a, uint32_t round, int grid, hipStrea
         if (p != a.me) cap = std::max(cap, a.peer[p].cap);
     const uint32_t blocks = (cap + UNP_BLOCK - 1) / UNP_BLOCK;
     if (blocks) hipLaunchKernelGGL(k_unpack, dim3(blocks, a.W), dim3(256), 0, st, a, round);
+    return hipGetLastError();
+}
+hipError_t launch_src_flag(const uint32_t* src, uint32_t n, const uint32_t* bounds, int W, int a, uint32_t* flag,
+                           int grid, hipStream_t st) {
+    SlabTable b{};
+    for (int w = 0; w <= W; ++w) b.v[w] = bounds[w];
+    b.W = W;
+    hipLaunchKernelGGL(k_src_flag, dim3(grid), dim3(256), 0, st, src, n, b, a, flag);
+    return hipGetLastError();
+}
+hipError_t launch_bits_pos(const BitsSetupArgs& a, int grid, hipStream_t st) {
+    hipLaunchKernelGGL(k_bits_pos, dim3(grid), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+hipError_t launch_bits_ends(const BitsEndsArgs& a, int grid, hipStream_t st) {
+    hipLaunchKernelGGL(k_bits_ends, dim3(grid), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+hipError_t launch_apply_bits(const uint32_t* bits, uint32_t nwords, const uint32_t* tgt, uint32_t* rq, uint32_t rq8,
+                             hipStream_t st) {
+    const uint32_t blocks = std::min<uint32_t>((nwords + 255) / 256, 4096u);
+    if (blocks) hipLaunchKernelGGL(k_apply_bits, dim3(blocks), dim3(256), 0, st, bits, nwords, tgt, rq, rq8);
+    return hipGetLastError();
+}
+hipError_t launch_list_count(const ListCountArgs& a, hipStream_t st) {
+    const uint32_t nt = (uint32_t)(((uint64_t)a.lo + a.nloc + XTILE - 1) / XTILE - a.lo / XTILE);
+    if (nt) hipLaunchKernelGGL(k_list_count, dim3(nt), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+hipError_t launch_list_key(const ListKeyArgs& a, hipStream_t st) {
+    const uint32_t nt = (uint32_t)(((uint64_t)a.lo + a.nloc + XTILE - 1) / XTILE - a.lo / XTILE);
+    if (nt) hipLaunchKernelGGL(k_list_key, dim3(nt), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+hipError_t launch_list_pack(const ListPackArgs& a, hipStream_t st) {
+    if (a.t1 > a.t0)
+        hipLaunchKernelGGL(k_list_pack, dim3((a.t1 - a.t0 + LP_TILES - 1) / LP_TILES), dim3(LP_THREADS), 0, st, a);
+    return hipGetLastError();
+}
+hipError_t launch_gather_keys(const uint32_t* key, const uint32_t* src, uint32_t n, uint32_t* out, int grid,
+                              hipStream_t st) {
+    if (n) hipLaunchKernelGGL(k_gather_keys, dim3(grid), dim3(256), 0, st, key, src, n, out);
     return hipGetLastError();
 }
 hipError_t launch_zero_counts(const ZeroArgs& z, hipStream_t st) {

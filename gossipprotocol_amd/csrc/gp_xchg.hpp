@@ -76,6 +76,104 @@ struct ExpectArgs {
     unsigned long long* n;    // [W] random edges to each rank
 };
 
+// ---- Imp3D push-sum: sender-ordered lists (round 5).  For each rank pair a -> b
+// the static list L_ab = a's senders whose random edge lands on b, in id order,
+// cut into the slab's 1024-id tiles (XTILE, the push-sum tile kernel's TILE) and
+// two regions (tiles [0, tsplit) and [tsplit, nt)); every (tile, b) segment starts
+// on a 64-entry boundary of the region's list (gw: its first header word).  Per
+// round the sender writes, per region and destination, one header word per 64
+// list entries -- the bitmap of the entries whose sender used its random edge and
+// the index of the first such message in the destination's vals region -- and the
+// used entries' (s, w) compacted in list order.  The receiver finds a used remote
+// in-edge's message at base + popcount(mask below its bit): no scatter, no slots.
+constexpr uint32_t XTILE = 1024;
+constexpr uint32_t XNONE = 0xFFu;  // "no list entry" (local target or no sender)
+
+struct ListPeer {              // send side: region h, destination d
+    XHdr* hdr;                 // NW header words
+    double2* vals;             // cap message slots
+    uint32_t* cnt;             // reservation counter (zeroed before the region's pack)
+    uint32_t cap;
+    uint32_t vbase;            // index of this chunk's first slot in d's vals region
+};
+
+struct ListPackArgs {
+    const uint8_t* nbn;        // node bytes of the round being prepared (local array, id - base)
+    const double2* swn;        // (s, w) of that round (local array, id - base)
+    const uint8_t* xdst;       // owner rank of each local sender's random-edge target (id - lo)
+    const uint32_t* gw;        // [tile * W + d]: first header word of the tile's segment in chunk (region, d)
+    uint32_t lo, nloc, base;
+    uint32_t t0, t1;           // the region's tiles (relative to lo / XTILE)
+    int W, me;
+    ListPeer peer[XMAXW];
+    unsigned int* overflow;
+};
+
+struct ListCountArgs {         // setup, slab a: list entries per (tile, destination)
+    const uint32_t* rnd;       // global random edges (rnd[i] for every id)
+    uint32_t lo, nloc;
+    int W, a;
+    uint32_t bounds[XMAXW + 1];
+    uint32_t* cnt;             // [tile * W + d]
+};
+
+struct ListKeyArgs {           // setup, slab a: every sender's list key at its destination
+    const uint32_t* rnd;       // global random edges
+    const uint32_t* gw;        // slab a's [tile * W + d]
+    uint32_t lo, nloc, tsplit;
+    int W, a;
+    uint32_t bounds[XMAXW + 1];
+    uint32_t hw[2][XMAXW];     // [h][b]: first header word of chunk (h, a) in b's header region
+    uint32_t* key;             // [global id]: 64 * header word + bit at the destination (local targets untouched)
+};
+
+// ---- Imp3D gossip on the column kernel across ranks: random-edge sends as bitmaps
+// (round 5).  For each rank pair a -> b the static list of edges from a's senders to
+// b's nodes, in b's receiver order (target, then sender), one bit per edge.  A sender
+// whose next direction is its random edge sets its edge's bit (k_gossip_col, an
+// atomicOr; rtg names the bit), the bitmaps travel (1 bit per remote edge instead of a
+// 4-byte entry per send, no pack pass), and the receiver adds one rumour per set bit
+// to its target's next-round count (k_apply_bits; tgt names the target of every bit).
+// Counts are integers, so the order of the additions is free.
+struct BitsSetupArgs {
+    const uint32_t* src;      // global senders in receiver order (the in-list sort)
+    const uint32_t* recv;     // their receivers (sorted random edges)
+    const uint32_t* scan;     // exclusive scan of [slab(src[q]) == a] (k_src_flag)
+    uint32_t* pos;            // out: for edges with a sender on slab a, the bit in its (a -> b) list
+    uint32_t n;               // edges (= P)
+    int W, a;
+    uint32_t bounds[XMAXW + 1];
+    uint32_t edge0[XMAXW + 1];  // first edge (global sorted position) of each receiver slab
+};
+
+struct BitsEndsArgs {         // this rank's encodings
+    const uint32_t* rnd;      // local senders' random edges (id - lo)
+    const uint32_t* inv;      // global sorted position of every sender's edge
+    const uint32_t* src;      // global senders in receiver order
+    const uint32_t* recv;     // their receivers
+    const uint32_t* pos;      // k_bits_pos's output for every edge
+    uint32_t* rtg;            // out [nloc]: local target (t - lo), or 0x80000000 | bit of the send bitmap
+    uint32_t* tgt;            // out: local receiver of every bit of the receive bitmap
+    uint32_t lo, nloc, e0, e1;  // this rank's ids and in-edges [e0, e1)
+    int W, me;
+    uint32_t bounds[XMAXW + 1];
+    uint32_t bo[XMAXW];       // bit offset of destination d's chunk in the send bitmap
+    uint32_t ro[XMAXW];       // bit offset of source a's chunk in the receive bitmap
+};
+
+hipError_t launch_src_flag(const uint32_t* src, uint32_t n, const uint32_t* bounds, int W, int a, uint32_t* flag,
+                           int grid, hipStream_t st);
+hipError_t launch_bits_pos(const BitsSetupArgs& a, int grid, hipStream_t st);
+hipError_t launch_bits_ends(const BitsEndsArgs& a, int grid, hipStream_t st);
+hipError_t launch_apply_bits(const uint32_t* bits, uint32_t nwords, const uint32_t* tgt, uint32_t* rq, uint32_t rq8,
+                             hipStream_t st);
+
+hipError_t launch_list_count(const ListCountArgs& a, hipStream_t st);
+hipError_t launch_list_key(const ListKeyArgs& a, hipStream_t st);
+hipError_t launch_list_pack(const ListPackArgs& a, hipStream_t st);
+hipError_t launch_gather_keys(const uint32_t* key, const uint32_t* src, uint32_t n, uint32_t* out, int grid,
+                              hipStream_t st);
+
 hipError_t launch_pack(const PackArgs& a, int grid, hipStream_t st);
 hipError_t launch_unpack(const UnpackArgs& a, uint32_t round, int grid, hipStream_t st);
 hipError_t launch_zero_counts(const ZeroArgs& z, hipStream_t st);

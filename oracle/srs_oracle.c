@@ -386,6 +386,37 @@ static int cmp_key_items(const or_sim* s, uint32_t a, uint32_t b) {
  *             against the round-start ratio (the reference's `difference` is
  *             always 0, Q11); D6 keeps converged nodes sending; D7 one test per
  *             round. */
+/* v[0..n) <- inclusive prefix sums, in nt contiguous slices (per-slice totals,
+ * their exclusive scan, then each slice's running sum) -- the serial scan over
+ * P = 1e9 counters was most of a round on a many-core host. */
+static void par_inclusive_scan_u32(uint32_t* v, int64_t n, int nt) {
+    uint64_t part[1025];
+    if (nt > 1024) nt = 1024;
+    #pragma omp parallel num_threads(nt)
+    {
+#ifdef _OPENMP
+        const int t = omp_get_thread_num(), T = omp_get_num_threads();
+#else
+        const int t = 0, T = 1;
+#endif
+        const int64_t a = n * t / T, b = n * (t + 1) / T;
+        uint64_t sum = 0;
+        for (int64_t i = a; i < b; ++i) sum += v[i];
+        part[t + 1] = sum;
+        #pragma omp barrier
+        #pragma omp single
+        {
+            part[0] = 0;
+            for (int q = 1; q <= T; ++q) part[q] += part[q - 1];
+        }
+        uint64_t run = part[t];
+        for (int64_t i = a; i < b; ++i) {
+            run += v[i];
+            v[i] = (uint32_t)run;
+        }
+    }
+}
+
 static int64_t pushsum_round(or_sim* s) {
     const int64_t P = s->P;
     const uint32_t r = (uint32_t)s->round;
@@ -408,7 +439,8 @@ static int64_t pushsum_round(or_sim* s) {
     }
     /* phase 2: bucket messages by receiver (counting sort; order inside a
      * bucket is fixed afterwards by sorting on the unique keys) */
-    memset(s->bcount, 0, sizeof(uint32_t) * (P + 1));
+    #pragma omp parallel for num_threads(nt) schedule(static)
+    for (int64_t j = 0; j <= P; ++j) s->bcount[j] = 0;
     #pragma omp parallel for num_threads(nt) schedule(static)
     for (int64_t i = 0; i < P; ++i) {
         uint32_t t = s->tgt[i];
@@ -417,8 +449,9 @@ static int64_t pushsum_round(or_sim* s) {
             s->bcount[t + 1] += 1;
         }
     }
-    for (int64_t j = 0; j < P; ++j) s->bcount[j + 1] += s->bcount[j];
-    memcpy(s->bcursor, s->bcount, sizeof(uint32_t) * P);
+    par_inclusive_scan_u32(s->bcount + 1, P, nt);
+    #pragma omp parallel for num_threads(nt) schedule(static)
+    for (int64_t j = 0; j < P; ++j) s->bcursor[j] = s->bcount[j];
     #pragma omp parallel for num_threads(nt) schedule(static)
     for (int64_t i = 0; i < P; ++i) {
         uint32_t t = s->tgt[i];

@@ -10,13 +10,14 @@ ranks only through the library's exchange plan:
     bytes -- here the direction / active fields -- and (s, w) goes to the
     neighbouring rank (gp_api.hip exchange, halo part);
   * random-edge messages: every sender whose next direction is its random edge
-    and whose target lives on another rank sends, for push-sum, {slot, s, w}
-    with `slot` = the message's position in the destination's receiver-sorted
-    in-edge array, computed from the global stable sort exactly like
-    build_imp3d / k_make_pos (the receiver tags rtag[slot] = round, gp_xchg.hip
-    k_pack / k_unpack); for gossip (the column kernel's counts mode) {target's
-    local id}, a rumour the receiver counts for the next round -- local senders
-    count theirs at the target directly (k_gossip_col);
+    and whose target lives on another rank sends.  Push-sum: sender-ordered lists
+    (ListPlan; gp_xchg.hpp k_list_pack) -- per region and destination one header
+    word {bitmap, base} per 64 entries of the static list and the used entries'
+    (s, w) compacted in list order; the receiver finds a remote in-edge's message
+    from its list key (64 * header word + bit, build_lists) as base + the used
+    entries below it.  Gossip (the column kernel's counts mode) {target's local
+    id}, a rumour the receiver counts for the next round -- local senders count
+    theirs at the target directly (k_gossip_col);
   * bookkeeping: {alerts, newly active, injector pick converged} summed over
     ranks (k_finalize_pre / all-reduce / k_finalize_post); the gossip
     injector's live list is replicated on every rank;
@@ -132,6 +133,89 @@ def slab_bounds(P, g, topo, W):
     return [(g * w // W) * g * g for w in range(W + 1)], g * g
 
 
+XTILE = 1024  # the lists' tiles: 1024 ids on global multiples (the push-sum tile kernel's TILE)
+
+
+class ListPlan:
+    """Imp3D push-sum over several ranks: the sender-ordered lists (gp_xchg.hpp,
+    gp_api.hip build_lists / setup_exchange).  List L_ab = slab a's senders whose
+    random edge lands on slab b, in id order, cut into the slab's tiles and two
+    regions (tiles [0, nt // 2) and the rest); every (tile, b) segment starts on a
+    64-entry boundary.  Computed from the global random edges, like every rank of
+    the library does for every slab."""
+
+    def __init__(self, P, g, W, bounds, rnd_all, geo, NH=2):
+        self.W, self.NH, self.bounds = W, NH, bounds
+        owner = np.searchsorted(np.array(bounds[1:-1]), rnd_all, side="right")
+        ids = np.arange(P)
+        slab = np.searchsorted(np.array(bounds[1:-1]), ids, side="right")
+        self.nw = np.zeros((W, NH, W), dtype=np.int64)        # header words of chunk (h, a -> b)
+        self.key_local = np.full(P, -1, dtype=np.int64)       # padded index of a sender in its chunk
+        self.region = np.zeros(P, dtype=np.int64)
+        mu = np.zeros((NH, W, W))
+        inv_deg = 1.0 / geo.degree(ids)
+        for a in range(W):
+            lo, hi = bounds[a], bounds[a + 1]
+            t_of = ids[lo:hi] // XTILE - lo // XTILE            # tile of each sender (relative)
+            nt = (hi + XTILE - 1) // XTILE - lo // XTILE
+            tsplit = nt // 2 if NH == 2 else nt
+            h_of = (t_of >= tsplit).astype(np.int64)
+            self.region[lo:hi] = h_of
+            np.add.at(mu, (h_of, a, owner[lo:hi]), inv_deg[lo:hi])
+            for b in range(W):
+                if b == a:
+                    continue
+                sel = np.nonzero(owner[lo:hi] == b)[0]          # the list, in id order
+                cnt = np.bincount(t_of[sel], minlength=nt)
+                words = (cnt + 63) // 64
+                gw = np.zeros(nt, dtype=np.int64)
+                for h in range(NH):
+                    in_h = (np.arange(nt) >= tsplit) == bool(h)
+                    gw[in_h] = np.cumsum(words[in_h]) - words[in_h]
+                    self.nw[a, h, b] = int(words[in_h].sum())
+                first = np.cumsum(cnt) - cnt  # list position of each tile's first entry
+                rho = np.arange(len(sel)) - first[t_of[sel]]
+                self.key_local[lo + sel] = gw[t_of[sel]] * 64 + rho
+        # capacities per (h, a -> b): expected messages + 12 sigma + 64, at most the edges
+        n_edges = np.zeros((NH, W, W))
+        for a in range(W):
+            lo, hi = bounds[a], bounds[a + 1]
+            np.add.at(n_edges, (self.region[lo:hi], a, owner[lo:hi]), 1)
+        self.cap = np.minimum(np.ceil(mu + 12.0 * np.sqrt(mu) + 64.0), n_edges).astype(np.int64)
+        for a in range(W):
+            self.cap[:, a, a] = 0
+        self.owner, self.slab = owner, slab
+
+    def hw(self, b, h, a):
+        """First header word of chunk (h, a) in b's header region (chunks in (h, a) order)."""
+        o = 0
+        for hh in range(self.NH):
+            for aa in range(self.W):
+                if aa == b:
+                    continue
+                if (hh, aa) == (h, a):
+                    return o
+                o += int(self.nw[aa, hh, b])
+        return o
+
+    def vo(self, b, h, a):
+        """First slot of chunk (h, a) in b's vals region (same order)."""
+        o = 0
+        for hh in range(self.NH):
+            for aa in range(self.W):
+                if aa == b:
+                    continue
+                if (hh, aa) == (h, a):
+                    return o
+                o += int(self.cap[hh, aa, b])
+        return o
+
+    def key(self, i):
+        """List key of sender i at its destination: 64 * header word + bit (build_lists)."""
+        a, b, h = self.slab[i], self.owner[i], self.region[i]
+        return np.array([self.hw(bb, hh, aa) * 64 for aa, bb, hh in zip(a, b, h)], dtype=np.int64) + self.key_local[i]
+
+
 def full_capacity(na, nb, P):
     """Per-pair message capacity of the full-topology exchange (gp_api.hip
     setup_exchange): messages a -> b are at most Binomial(na, nb / (P - 1))."""
@@ -204,6 +288,14 @@ class RankSim:
         ne = len(self.in_src)
         self.rtag = np.full(ne, -1, dtype=np.int64)
         self.rmsg = np.zeros((ne, 2))
+        self.plan = None
+        if self.alg == "push-sum" and self.W > 1:  # sender-ordered lists (build_lists)
+            self.plan = ListPlan(P, self.g, self.W, self.bounds, rnd_all, self.G)
+            src = self.in_src
+            remote = (src < self.lo) | (src >= self.hi)
+            self.rk = np.zeros(ne, dtype=np.int64)
+            if remote.any():
+                self.rk[remote] = self.plan.key(src[remote])
 
     def _local(self, ids):
         return ids - self.ext_lo
@@ -242,7 +334,9 @@ class RankSim:
             self.rq = np.zeros(self.hi - self.lo, dtype=np.int64)
             mine = (mydir == DIR_RANDOM) & (self.owner == self.rank)
             np.add.at(self.rq, self.rnd[mine] - self.lo, 1)
-        if self.topo == "Imp3D" and self.W > 1:
+        if self.topo == "Imp3D" and self.W > 1 and self.plan is not None:
+            self._exchange_lists()
+        elif self.topo == "Imp3D" and self.W > 1:
             mydir = self.dir[self._local(self.ids)]
             send = (mydir == DIR_RANDOM) & (self.owner != self.rank)
             packets = {}
@@ -267,6 +361,59 @@ class RankSim:
                     np.add.at(self.rq, msg[0], 1)
         _ = torch  # gloo transport via torch.distributed
 
+    def _exchange_lists(self):
+        """k_list_pack + the transfer: per region h and destination d, one header word
+        {mask, base} per 64 list entries and the used entries' (s, w) compacted in list
+        order (the library reserves each tile's run with an atomic, so runs land in any
+        order; the header's base says where -- here in tile order)."""
+        pl, me, W = self.plan, self.rank, self.W
+        mydir = self.dir[self._local(self.ids)]
+        used_all = (mydir == DIR_RANDOM) & (self.owner != me)
+        out = {}
+        for d in range(W):
+            if d == me:
+                continue
+            for h in range(pl.NH):
+                sel = np.nonzero((self.owner == d) & (pl.region[self.ids] == h))[0]
+                kl = pl.key_local[self.ids[sel]]
+                used = used_all[sel]
+                nw = int(pl.nw[me, h, d])
+                mask = np.zeros(nw, dtype=np.uint64)
+                np.bitwise_or.at(mask, kl[used] >> 6, np.left_shift(np.uint64(1), (kl[used] & 63).astype(np.uint64)))
+                per_word = np.bincount(kl[used] >> 6, minlength=nw)[:nw]
+                base = pl.vo(d, h, me) + (np.cumsum(per_word) - per_word).astype(np.int64)
+                order = np.argsort(kl[used], kind="stable")            # list order
+                li = self._local(self.ids[sel][used][order])
+                vals = np.stack([self.s[li], self.w[li]], axis=1) if len(li) else np.zeros((0, 2))
+                out[(d, h)] = (mask, base, vals)
+        got = [None] * W
+        self.dist.all_gather_object(got, out)
+        # this rank's receive region: header words and slots of every chunk (h, a), (h, a) order
+        hdr_mask, hdr_base, vals = [], [], []
+        for h in range(pl.NH):
+            for a in range(W):
+                if a == me:
+                    continue
+                m, b, v = got[a][(me, h)]
+                hdr_mask.append(m)
+                hdr_base.append(b)
+                slot = np.zeros((int(pl.cap[h, a, me]), 2))
+                slot[:len(v)] = v
+                vals.append(slot)
+        self.xmask = np.concatenate(hdr_mask) if hdr_mask else np.zeros(0, dtype=np.uint64)
+        self.xbase = np.concatenate(hdr_base) if hdr_base else np.zeros(0, dtype=np.int64)
+        self.xvals = np.concatenate(vals) if vals else np.zeros((0, 2))
+
+    def _list_lookup(self, k):
+        """Receiver side (the round kernel's in-edge pass): did the remote sender with list
+        key k use its edge, and where is its message?"""
+        w, bit = k >> 6, (k & 63).astype(np.uint64)
+        m = self.xmask[w]
+        sent = ((m >> bit) & np.uint64(1)) == 1
+        below = m & ((np.uint64(1) << bit) - np.uint64(1))
+        pc = np.array([bin(int(x)).count("1") for x in below], dtype=np.int64)
+        return sent, self.xbase[w] + pc
+
     def _allreduce(self, vals):
         import torch
         t = torch.tensor(vals, dtype=torch.int64)
@@ -281,7 +428,12 @@ class RankSim:
         local = (src >= self.lo) & (src < self.hi)
         sent = np.zeros(len(src), dtype=bool)
         sent[local] = self.dir[self._local(src[local])] == DIR_RANDOM
-        sent[~local] = self.rtag[~local] == r
+        if self.plan is not None:  # push-sum: the received lists
+            self.rslot = np.zeros(len(src), dtype=np.int64)
+            if (~local).any():
+                sent[~local], self.rslot[~local] = self._list_lookup(self.rk[~local])
+        else:
+            sent[~local] = self.rtag[~local] == r
         return sent, local
 
     def _pushsum_round(self):
@@ -308,7 +460,11 @@ class RankSim:
             val_w = np.zeros(len(sent))
             ls = self._local(self.in_src[local])
             val_s[local], val_w[local] = self.s[ls], self.w[ls]
-            val_s[~local], val_w[~local] = self.rmsg[~local, 0], self.rmsg[~local, 1]
+            if self.plan is not None:
+                rs = np.where(sent & ~local, self.rslot, 0)
+                val_s[~local], val_w[~local] = self.xvals[rs[~local], 0], self.xvals[rs[~local], 1]
+            else:
+                val_s[~local], val_w[~local] = self.rmsg[~local, 0], self.rmsg[~local, 1]
             indeg = np.diff(self.in_off)
             for k in range(int(indeg.max()) if len(indeg) else 0):
                 has = indeg > k

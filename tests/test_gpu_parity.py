@@ -496,3 +496,39 @@ def test_round_close_parity(fuse, n, topo, seed, rounds, chk, monkeypatch):
     assert sim.rounds == orc.rounds
     sim.close()
     orc.close()
+
+
+BLOCK_CASES = [  # (num_nodes, seed, rounds, checkpoint): 3D push-sum, the LDS-resident kernel
+    (1000, 3, 3000, 1000),        # one box, no grid barrier; through convergence
+    (27000, 5, 400, 100),         # several boxes
+    (1000000, 1, 300, 150),       # C2 (g = 100): one box per CU
+    (1030301, 2, 120, 60),        # g = 101: uneven boxes
+]
+
+
+@pytest.mark.parametrize("n,seed,rounds,chk", BLOCK_CASES, ids=lambda v: str(v))
+def test_block_kernel_parity(n, seed, rounds, chk, monkeypatch):
+    """3D push-sum on the LDS-resident kernel (gp_block.hip: one cooperative launch per batch,
+    boxes in LDS, faces through global memory at a grid barrier), forced with GP_KERNEL=block
+    (experiments build): per-round alerts and full state bit-exact vs the oracle at every
+    checkpoint (Program.fs:101-131, 238-257 via SRS v1 B.4), batches cut mid-run."""
+    monkeypatch.setenv("GP_KERNEL", "block")
+    sim, orc = Sim(n, "3D", "push-sum", seed=seed, experimental=True), Oracle(n, "3D", "push-sum", seed)
+    assert sim.kernel_stats()[2] == "k_ps_block<GRID3D>"
+    done = 0
+    while done < rounds and orc.alerts_total < orc.T:
+        k = min(chk, rounds - done)
+        ga, oa = sim.step(k), orc.step(k)
+        assert ga == oa, f"alerts differ in rounds {done}..{done + k}"
+        assert_same_state("push-sum", sim.state(), orc.state())
+        done += k
+    assert sim.rounds == orc.rounds
+    sim.close()
+    orc.close()
+
+
+def test_block_kernel_is_the_c2_default():
+    """The product picks the LDS-resident kernel for C2 (3D push-sum, n = 1e6, one GPU)."""
+    sim = Sim(10**6, "3D", "push-sum", seed=1)
+    assert sim.kernel_stats()[2] == "k_ps_block<GRID3D>"
+    sim.close()

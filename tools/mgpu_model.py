@@ -66,7 +66,11 @@ def run(n, topo, alg, W, rounds):
     s.close()
 
 
-def pair_bytes(n, topo, alg, W, halves=1):
+def per_slab_names(groups, short):
+    return {short(name) for grp in groups for name, _ in grp}
+
+
+def pair_bytes(n, topo, alg, W, halves=1, lists=True):
     """Bytes rank a sends rank b per round (fixed-capacity buffers incl. their 16-B count
     headers; full push-sum: `halves` regions, one per half of a's senders) and the halo
     bytes per neighbouring pair and direction."""
@@ -94,8 +98,19 @@ def pair_bytes(n, topo, alg, W, halves=1):
         if topo == "Imp3D":
             _, mu, _ = imp3d_pair_stats(P, g, W)
             for a in range(W):
+                na = bounds[a + 1] - bounds[a]
+                nt = na // 1024 + 1
                 for b in range(W):
-                    if b != a:  # push-sum: one region per half of the sender's slab
+                    if b == a:
+                        continue
+                    if push and lists:
+                        # sender-ordered lists (round 5): per region the header words (16 B per 64
+                        # list entries, a tile's segment padded to 64: ~half a word per tile) and the
+                        # message slots (16 B each, capacity per region)
+                        edges = na * (bounds[b + 1] - bounds[b]) / (P - 1)
+                        B[a][b] = int(16 * (edges / 64 + nt / 2)) + sum(16 * cap_of(mu[a, b] / halves)
+                                                                        for _ in range(halves))
+                    else:  # {slot, (s, w)} buffers (round 4) / gossip counts
                         B[a][b] = sum(xbuf(cap_of(mu[a, b] / halves)) for _ in range(halves))
     return P, bounds, B, halo
 
@@ -147,8 +162,13 @@ def model(tdir, n, topo, alg, W, rounds, out=None):
     # (full, gp_api.hip launch_round_full_multi) or the pack / unpack (Imp3D, exchange):
     # those kernels appear twice per slab
     halves = 2 if alg == "push-sum" and topo in ("full", "Imp3D") else 1
-    first_k, second_k = ("k_fbm_send", "k_fbm_coarse") if topo == "full" else ("k_pack", "k_unpack")
-    P, bounds, B, halo = pair_bytes(n, topo, alg, W, halves)
+    # (Imp3D push-sum since round 5: k_list_pack per region, no unpack -- the round kernel reads the
+    # received lists in place)
+    first_k, second_k = ("k_fbm_send", "k_fbm_coarse") if topo == "full" else ("k_list_pack", None)
+    legacy = topo != "full" and "k_unpack" in per_slab_names(groups, short)  # a round-4 build (A/B runs)
+    if legacy:
+        first_k, second_k = "k_pack", "k_unpack"
+    P, bounds, B, halo = pair_bytes(n, topo, alg, W, halves, lists=not legacy)
     kern = {k: [statistics.mean(x[s] for x in v) for s in range(W)] for k, v in per_slab.items()}
     comp = [statistics.mean(v) for v in rank_ms]
     t_comp = max(comp)
@@ -162,11 +182,12 @@ def model(tdir, n, topo, alg, W, rounds, out=None):
                 by.setdefault(short(name), []).append(ms)
             for nm in (first_k, second_k):
                 v = by.get(nm, [])
-                if len(v) == 2 * W:
+                if nm and len(v) == 2 * W:
                     hk.setdefault(nm, []).append(v)
-        if len(hk.get(first_k, [])) and len(hk.get(second_k, [])):
+        if len(hk.get(first_k, [])) and (second_k is None or len(hk.get(second_k, []))):
             s_h = [[statistics.mean(x[h * W + k] for x in hk[first_k]) for k in range(W)] for h in range(2)]
-            c_h = [[statistics.mean(x[h * W + k] for x in hk[second_k]) for k in range(W)] for h in range(2)]
+            c_h = ([[statistics.mean(x[h * W + k] for x in hk[second_k]) for k in range(W)] for h in range(2)]
+                   if second_k else [[0.0] * W, [0.0] * W])
             piped = {"send_half_ms": [max(v) for v in s_h], "coarse_half_ms": [max(v) for v in c_h],
                      "rest_ms": max(comp[k] - s_h[0][k] - s_h[1][k] - c_h[0][k] - c_h[1][k] for k in range(W))}
     res = {"workload": f"{alg} {topo} n={n} P={P}", "W": W, "rounds_measured": len(groups),
