@@ -99,6 +99,8 @@ struct Slab {
     bool lists = false;
     uint32_t nt = 0, tsplit = 0;       // the slab's tiles; first tile of region 1
     uint32_t* gw = nullptr;            // [tile * W + d]: first header word of the tile's segment
+    uint16_t* xdr = nullptr;           // [id - lo]: d << 10 | rank in the tile's list for d (static)
+    uint8_t* lwt = nullptr;            // [tile * (W + 1) + d]: the tile's LDS word layout in k_list_pack
     uint32_t* xcnt = nullptr;          // [h * W + d]: reservation counters of the send chunks
     std::vector<size_t> lhdr, lval;    // send buffer: byte offsets of chunk (h, d)'s header words / slots
     std::vector<size_t> rhdr, rval;    // receive buffer: byte offsets of chunk (h, p)'s header words / slots
@@ -303,6 +305,7 @@ int alloc_slab(gp_sim* s, Slab& sl, int r) {
     S.rtag = nullptr;
     S.rmsg = nullptr;
     S.rk = nullptr;
+    S.outbox = nullptr;
     S.rtg = nullptr;
     S.sbits = nullptr;
     S.xhdr = nullptr;
@@ -428,6 +431,7 @@ int build_lists(gp_sim* s, const uint32_t* rnd_all, uint32_t* kk, const uint32_t
     const int NH = s->xhalves = exchange_regions(s);
     s->list_nw.assign((size_t)W * NH * W, 0);
     std::vector<std::vector<uint32_t>> gw_all(W);
+    std::vector<std::vector<uint8_t>> lwt_all(W);
     std::vector<uint32_t> tsplit(W);
     Scratch tmp_mem;
     for (int a = 0; a < W; ++a) {
@@ -450,6 +454,16 @@ int build_lists(gp_sim* s, const uint32_t* rnd_all, uint32_t* kk, const uint32_t
         HIP_TRY(hipStreamSynchronize(s->stream));
         std::vector<uint32_t>& gw = gw_all[a];
         gw.assign((size_t)nt * W, 0);
+        std::vector<uint8_t>& lwt = lwt_all[a];  // per tile: prefix over d of its segments' words
+        lwt.assign((size_t)nt * (W + 1), 0);
+        for (uint32_t t = 0; t < nt; ++t) {
+            uint32_t w = 0;
+            for (int d = 0; d < W; ++d) {
+                lwt[(size_t)t * (W + 1) + d] = (uint8_t)w;
+                w += (hc[(size_t)t * W + d] + 63u) / 64u;
+            }
+            lwt[(size_t)t * (W + 1) + W] = (uint8_t)w;  // <= 16 + W words
+        }
         for (int d = 0; d < W; ++d) {
             uint64_t run[2] = {0, 0};
             for (uint32_t t = 0; t < nt; ++t) {
@@ -486,6 +500,13 @@ int build_lists(gp_sim* s, const uint32_t* rnd_all, uint32_t* kk, const uint32_t
         for (int h = 0; h < NH; ++h)
             for (int b = 0; b < W; ++b) ka.hw[h][b] = b == a ? 0u : list_hw(s, b, h, a);
         ka.key = kk;
+        ka.xdr = nullptr;
+        for (Slab& sl : s->slab) {
+            if (sl.rank != a) continue;
+            int rc;
+            if ((rc = dev_alloc_t(s, &sl.xdr, (size_t)nloc + 64))) return rc;
+            ka.xdr = sl.xdr;
+        }
         HIP_TRY(launch_list_key(ka, s->stream));
         HIP_TRY(hipStreamSynchronize(s->stream));  // (gw is freed at scope end; keep it simple)
     }
@@ -496,12 +517,20 @@ int build_lists(gp_sim* s, const uint32_t* rnd_all, uint32_t* kk, const uint32_t
         sl.lists = true;
         sl.nt = slab_tiles(S.lo, S.nloc);
         sl.tsplit = tsplit[r];
-        if ((rc = dev_alloc_t(s, &sl.gw, gw_all[r].size() + 1))) return rc;
+        if ((rc = dev_alloc_t(s, &sl.gw, gw_all[r].size() + 1)) || (rc = dev_alloc_t(s, &sl.lwt, lwt_all[r].size() + 16)))
+            return rc;
         HIP_TRY(hipMemcpyAsync(sl.gw, gw_all[r].data(), sizeof(uint32_t) * gw_all[r].size(), hipMemcpyHostToDevice,
                                s->stream));
+        HIP_TRY(hipMemcpyAsync(sl.lwt, lwt_all[r].data(), lwt_all[r].size(), hipMemcpyHostToDevice, s->stream));
         const uint32_t ne = edge0[r + 1] - edge0[r];
         if ((rc = dev_alloc_t(s, &S.rk, (size_t)ne + 4))) return rc;
         HIP_TRY(launch_gather_keys(kk, src + edge0[r], ne, S.rk, s->grid, s->stream));
+#ifdef GP_EXPERIMENTS
+        // GP_OUTBOX=1: the round kernel compacts its random-edge senders' (s, w) for the pack
+        if (const char* e = std::getenv("GP_OUTBOX"))
+            if (e[0] == '1' && (rc = dev_alloc_t(s, &S.outbox, (size_t)sl.nt * XTILE))) return rc;
+#endif
+
     }
     HIP_TRY(hipStreamSynchronize(s->stream));
     return GP_OK;
@@ -1116,7 +1145,9 @@ int exchange(gp_sim* s, uint32_t rn) {
                     ListPackArgs la{};
                     la.nbn = S.nb[b];
                     la.swn = S.sw[b];
-                    la.xdst = sl.xdst;
+                    la.xdr = sl.xdr;
+                    la.outbox = S.outbox;
+                    la.lwt = sl.lwt;
                     la.gw = sl.gw;
                     la.lo = S.lo;
                     la.nloc = S.nloc;
@@ -1479,7 +1510,7 @@ int build_sim(gp_sim* s) {
         sl.S.bplan = s->bplan;
         sl.S.bface = sl.S.bscratch = nullptr;
         if (kernel == KERNEL_BLOCK) {  // face exchange buffers + barrier / accumulator scratch
-            if ((rc = dev_alloc(s, &sl.S.bface, block_face_bytes(s->bplan))) || (rc = dev_alloc(s, &sl.S.bscratch, 64)))
+            if ((rc = dev_alloc(s, &sl.S.bface, block_face_bytes(s->bplan))) || (rc = dev_alloc(s, &sl.S.bscratch, BLOCK_SCRATCH_BYTES)))
                 return rc;
             HIP_TRY(block_kernel_setup(s->bplan));
         }

@@ -34,6 +34,9 @@ namespace gp {
 
 namespace {
 
+#ifndef GP_BK_ABL
+#define GP_BK_ABL 0  // experiments (wrong results): skip the node work, time the faces and barriers alone
+#endif
 constexpr int BK_THREADS = 1024;
 constexpr int BK_NPT = 5;  // nodes per thread: boxes of at most 5120 nodes
 
@@ -44,7 +47,7 @@ struct BlockArgs {
     const uint8_t* nb_in;
     uint8_t* nb_out;
     uint8_t* nb_alt;
-    uint8_t* fb;            // face bytes [2][NB][6][fmax]
+    uint32_t* fb;           // face node bytes, one word each [2][NB][6][fmax]
     double2* fs;            // face (s, w) [2][NB][6][fmax]
     unsigned int* bar;      // barrier arrivals (zeroed before the launch)
     unsigned long long* acc;  // [3][2]: per-round alerts, newly active (zeroed before the launch)
@@ -62,28 +65,46 @@ __device__ __forceinline__ uint32_t split(uint32_t g, uint32_t i, uint32_t n) {
 
 __device__ __forceinline__ uint64_t now_10ns() { return __builtin_amdgcn_s_memrealtime(); }  // 100 MHz
 
-// Grid barrier k (k = 1, 2, ...): arrivals counted on one word (never reset inside a
-// launch); waits at most ~2 s.  Every thread releases its global writes and acquires
-// the others' at agent scope.
-__device__ __forceinline__ bool grid_sync(unsigned int* bar, unsigned int target, unsigned int* err) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+// Grid barrier k (k = 1, 2, ...), in two halves (grid_arrive, grid_wait) so that the
+// box interior's nodes are computed while the barrier completes.  Faces are written and
+// read with device-coherent (agent-scope, relaxed atomic) stores and loads, so no cache
+// write-back or invalidate is needed: each wave waits for its face stores to be
+// performed (vmcnt) before the workgroup barrier, thread 0 then arrives.  Arrivals are
+// non-returning adds on one counter per group of blocks (blockIdx % 8: the blocks of one
+// XCD), so no word takes more than ~NB / 8 atomics per barrier (one word takes ~88 per
+// microsecond); the waiters poll the 8 counters at once; counters are never reset inside
+// a launch.  Waits at most ~2 s.  (Agent-scope release / acquire fences -- an L2
+// write-back and invalidate per block and barrier -- left a C2 round at 27 us of barrier
+// and face time, 37 us in all.)
+__device__ __forceinline__ void grid_arrive(unsigned int* bar, unsigned int k, unsigned int nb) {
+    (void)k;
+    (void)nb;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (threadIdx.x == 0)  // a non-returning add on this block group's counter (a 64-byte line each)
+        __hip_atomic_fetch_add(bar + 16u * (1u + (blockIdx.x & 7u)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool grid_wait(unsigned int* bar, unsigned int k, unsigned int nb, unsigned int* err) {
     __shared__ unsigned int ok;
-    if (threadIdx.x == 0) {
-        ok = 1u;
-        __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x < 64) {  // lane grp < 8 polls group grp's counter
+        const unsigned int grp = threadIdx.x;
+        const unsigned int want = grp < 8u ? k * ((nb + 7u - grp) / 8u) : 0u;
         const uint64_t t0 = now_10ns();
-        while (__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        bool fail = false;
+        for (;;) {
+            const unsigned int got =
+                grp < 8u ? __hip_atomic_load(bar + 16u * (1u + grp), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+            if (__ballot(got < want) == 0ull) break;
             if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || now_10ns() - t0 > 200000000ull) {
-                __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ok = 0u;
+                if (threadIdx.x == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                fail = true;
                 break;
             }
-            __builtin_amdgcn_s_sleep(2);
+            __builtin_amdgcn_s_sleep(1);
         }
+        if (threadIdx.x == 0) ok = fail ? 0u : 1u;
     }
     __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     return ok != 0u;
 }
 
@@ -100,11 +121,16 @@ __global__ __launch_bounds__(BK_THREADS) void k_ps_block(BlockArgs a) {
     const uint32_t z0 = split(g, iz, a.nbz), z1 = split(g, iz + 1, a.nbz);
     const uint32_t dx = x1 - x0, dy = y1 - y0, dz = z1 - z0, dyz = dy * dz, V = dx * dyz;
     const uint32_t F = a.fmax;
-    double2* swl = reinterpret_cast<double2*>(lds);         // [vmax]
-    double2* hsw = swl + a.vmax;                            // [6][fmax]
-    uint8_t* bl = reinterpret_cast<uint8_t*>(hsw + 6 * F);  // [vmax] node bytes of the round
-    uint8_t* bn = bl + a.vmax;                              // [vmax] the next round's (swapped per round)
-    uint8_t* hb = bn + a.vmax;                              // [6][fmax]
+    // LDS: (s, w) of the box, then of the six halos, then a zero sentinel (one array, so a
+    // neighbour is one index: in the box, in a halo, or the sentinel); node bytes likewise
+    // (sentinel DIR_NONE); the next round's node bytes; packed box coordinates
+    const uint32_t NS = a.vmax + 6 * F;  // the sentinel's index
+    double2* swl = reinterpret_cast<double2*>(lds);         // [NS + 1]
+    double2* hsw = swl + a.vmax;
+    uint8_t* bl = reinterpret_cast<uint8_t*>(swl + NS + 1);  // [NS + 1]
+    uint8_t* hb = bl + a.vmax;
+    uint8_t* bn = bl + ((NS + 1 + 3) & ~3u);                // [vmax]
+    uint32_t* ct = reinterpret_cast<uint32_t*>(bn + ((a.vmax + 3) & ~3u));  // [vmax] lx | ly << 10 | lz << 20
     __shared__ uint32_t red[2][BK_THREADS / 64];
     // face sizes and whether the neighbour in direction f exists (slot order: x-1, x+1, y+1, y-1, z+1, z-1)
     const uint32_t fsz[6] = {dyz, dyz, dx * dz, dx * dz, dx * dy, dx * dy};
@@ -117,12 +143,83 @@ __global__ __launch_bounds__(BK_THREADS) void k_ps_block(BlockArgs a) {
         const uint32_t j = (x0 + lx) * g2 + (y0 + ly) * g + (z0 + lz);
         swl[v] = a.sw_in[j];
         bl[v] = a.nb_in[j];
+        // (no divisions per node and round); bit 30: the node has a lattice neighbour outside the
+        // box (it reads a halo, so it is computed after the barrier)
+        const uint32_t x = x0 + lx, y = y0 + ly, z = z0 + lz;
+        const uint32_t mask = mask_xyz(x, y, z, gm);
+        const bool bnd = ((mask & 1u) && lx == 0) || ((mask & 2u) && lx + 1 == dx) || ((mask & 4u) && ly + 1 == dy) ||
+                         ((mask & 8u) && ly == 0) || ((mask & 16u) && lz + 1 == dz) || ((mask & 32u) && lz == 0);
+        ct[v] = lx | (ly << 10) | (lz << 20) | (bnd ? 1u << 30 : 0u);
+    }
+    if (threadIdx.x == 0) {
+        swl[NS] = make_double2(0.0, 0.0);
+        bl[NS] = DIR_NONE;
     }
     unsigned long long total = __hip_atomic_load(&a.ctl->alerts_total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned long long act = __hip_atomic_load(&a.ctl->active_total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint32_t done_rounds = 0;  // rounds executed by this launch
     bool stop = __hip_atomic_load(&a.ctl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
     __syncthreads();
+    // One node of round r: the tile kernel's fold (own half, the lattice messages in the
+    // receiver's slot order -- Program.fs:246-257 -- acc + m * 0.5, the oracle's rounding;
+    // a direction without a message adds +0.0, exact for the non-negative s and w), the
+    // ratio test (Program.fs:114-123), the next direction by Philox.  pass 0: only nodes
+    // whose neighbours are all in the box; pass 1: only the others (they read halos).
+    auto node = [&](uint32_t v, uint32_t r, int pass, double2& res, uint32_t& alerts, uint32_t& newly) {
+        const uint32_t c = ct[v];
+        if (((c >> 30) & 1u) != (uint32_t)pass) return false;
+        const uint32_t lx = c & 1023u, ly = (c >> 10) & 1023u, lz = (c >> 20) & 1023u;
+        const uint32_t x = x0 + lx, y = y0 + ly, z = z0 + lz;
+        const uint32_t mask = mask_xyz(x, y, z, gm);
+        const uint32_t bt = bl[v];
+        const double2 sv = swl[v];
+        const bool active = (bt & B_ACTIVE) != 0;
+        const uint32_t deg = popc6(mask);
+        const bool halve = active && deg > 0;
+        double acc_s = halve ? sv.x * 0.5 : sv.x;
+        double acc_w = halve ? sv.y * 0.5 : sv.y;
+        // every neighbour's byte first (in the box, in a halo, or the DIR_NONE sentinel), then the
+        // (s, w) of those that send here (direction d ^ 1), folded in slot order
+        const bool in[6] = {lx > 0, lx + 1 < dx, ly + 1 < dy, ly > 0, lz + 1 < dz, lz > 0};
+        const uint32_t vn[6] = {v - dyz, v + dyz, v + dz, v - dz, v + 1, v - 1};
+        const uint32_t hn[6] = {ly * dz + lz, ly * dz + lz, lx * dz + lz, lx * dz + lz, lx * dy + ly, lx * dy + ly};
+        uint32_t u[6], from = 0;
+#pragma unroll
+        for (int d = 0; d < 6; ++d) {
+            u[d] = !((mask >> d) & 1u) ? NS : in[d] ? vn[d] : a.vmax + d * F + hn[d];
+            from |= (bl[u[d]] & DIR_MASK) == (uint32_t)(d ^ 1) ? 1u << d : 0u;
+        }
+#pragma unroll
+        for (int d = 0; d < 6; ++d)
+            if ((from >> d) & 1u) {
+                const double2 m = swl[u[d]];
+                acc_s = acc_s + m.x * 0.5;  // the oracle's rounding (no fused multiply-add)
+                acc_w = acc_w + m.y * 0.5;
+            }
+        uint32_t flags = bt & (B_ACTIVE | B_CONV | (3u << CNT_SHIFT));
+        bool act_n = active;
+        if (from) {
+            if (!(bt & B_CONV)) {
+                uint32_t c3 = (bt >> CNT_SHIFT) & 3u;
+                c3 = ratio_moved(sv.x, sv.y, acc_s, acc_w) ? 0u : c3 + 1u;
+                flags = (flags & ~(3u << CNT_SHIFT)) | (c3 << CNT_SHIFT);
+                if (c3 == 3) {
+                    flags |= B_CONV;
+                    ++alerts;
+                }
+            }
+            if (!active) {
+                ++newly;
+                flags |= B_ACTIVE;
+                act_n = true;
+            }
+        }
+        uint32_t dir = DIR_NONE;
+        if (act_n && deg > 0) dir = slot_to_dir_fast(mask, uniform(a.k0, a.k1, S_PUSHSUM, x * g2 + y * g + z, r + 1, deg));
+        res = make_double2(acc_s, acc_w);
+        bn[v] = (uint8_t)(flags | dir);
+        return true;
+    };
     for (uint32_t i = 0; i <= a.nrounds && !stop; ++i) {
         const uint32_t r = a.r0 + i;
         // (1) boundary layers of the current state -> face buffer (parity i & 1)
@@ -142,137 +239,113 @@ __global__ __launch_bounds__(BK_THREADS) void k_ps_block(BlockArgs a) {
                         const uint32_t lx = t / dy, ly = t - lx * dy;
                         v = lx * dyz + ly * dz + (f == 4 ? dz - 1u : 0u);
                     }
-                    a.fb[fo + f * F + t] = bl[v];
-                    a.fs[fo + f * F + t] = swl[v];
+                    // device-coherent stores (agent-scope atomics: performed at the coherence
+                    // point, no L2 write-back needed before the barrier)
+                    const double2 mm = swl[v];
+                    unsigned long long* fp = reinterpret_cast<unsigned long long*>(a.fs + fo + f * F + t);
+                    __hip_atomic_store(&fp[0], __builtin_bit_cast(unsigned long long, mm.x), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(&fp[1], __builtin_bit_cast(unsigned long long, mm.y), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(&a.fb[fo + f * F + t], (uint32_t)bl[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
         }
-        // (2) barrier i + 1: faces of round r written, round r - 1's counts complete
-        if (NB > 1 && !grid_sync(a.bar, (i + 1u) * NB, a.err)) break;
-        if (NB == 1) __syncthreads();
-        // (3) close round r - 1 (every block: the same cumulative count)
-        if (i > 0) {
-            const unsigned long long* c = a.acc + 2 * ((r - 1u) % 3u);
-            const unsigned long long ra = __hip_atomic_load(&c[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const unsigned long long rn = __hip_atomic_load(&c[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            total += ra;
-            act += rn;
-            if (b == 0 && threadIdx.x == 0) {
-                Ctl* ctl = a.ctl;
-                ctl->hist[(r - 1u) % HIST] = ra;
-                __hip_atomic_store(&ctl->alerts_total, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&ctl->active_total, act, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (act >= a.G.P) __hip_atomic_store(&ctl->all_active, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (total >= a.G.T) __hip_atomic_store(&ctl->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                // the accumulator of round r + 1 (last read after barrier r - 1 + ... i - 1)
-                unsigned long long* z = a.acc + 2 * ((r + 1u) % 3u);
-                __hip_atomic_store(&z[0], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&z[1], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            if (total >= a.G.T) break;  // (the same decision in every block)
-        }
-        if (i == a.nrounds) break;
-        // (4) the neighbours' facing layers -> LDS halos
-        {
-            const size_t fp = (size_t)(i & 1u) * NB;
-#pragma unroll
-            for (int f = 0; f < 6; ++f) {
-                if (!has[f]) continue;
-                const size_t fo = ((fp + nbr_b[f]) * 6 + (f ^ 1)) * F;
-                for (uint32_t t = threadIdx.x; t < fsz[f]; t += BK_THREADS) {
-                    hb[f * F + t] = a.fb[fo + t];
-                    hsw[f * F + t] = a.fs[fo + t];
-                }
-            }
-        }
-        __syncthreads();
-        // (5) the round for this thread's nodes (results in registers)
+        // (2) arrive at barrier i + 1 (faces of round r written, round r - 1's counts added)
+        if (NB > 1) grid_arrive(a.bar, i + 1u, NB);
+        // (3) the box interior's nodes of round r while the barrier completes (in registers and
+        // bn only: nothing is committed before round r - 1 is known not to be the last)
         uint32_t alerts = 0, newly = 0;
         // the new (s, w) of node slot q in n[q] (named registers, selected by q: the slot loop
-        // is not unrolled -- unrolled, the compiler interleaved all slots and spilled); the
-        // new node bytes go straight to bn
+        // is not unrolled -- unrolled, the compiler interleaved all slots and spilled)
         double2 n0 = make_double2(0.0, 0.0), n1 = n0, n2 = n0, n3 = n0, n4 = n0;
         static_assert(BK_NPT == 5, "one named register pair per node slot");
-#pragma unroll 1
-        for (int q = 0; q < BK_NPT; ++q) {
-            const uint32_t v = q * BK_THREADS + threadIdx.x;
-            if (v >= V) break;
-            const uint32_t lx = v / dyz, ly = (v - lx * dyz) / dz, lz = v - lx * dyz - ly * dz;
-            const uint32_t x = x0 + lx, y = y0 + ly, z = z0 + lz;
-            const uint32_t mask = mask_xyz(x, y, z, gm);
-            const uint32_t bt = bl[v];
-            const double2 sv = swl[v];
-            const bool active = (bt & B_ACTIVE) != 0;
-            const uint32_t deg = popc6(mask);
-            const bool halve = active && deg > 0;
-            double acc_s = halve ? sv.x * 0.5 : sv.x;
-            double acc_w = halve ? sv.y * 0.5 : sv.y;
-            bool recv = false;
-            // lattice slots in the receiver's order: x-1, x+1, y+1, y-1, z+1, z-1; the sender in
-            // direction d sends here iff its direction is d ^ 1
-#pragma unroll
-            for (int d = 0; d < 6; ++d) {
-                if (!((mask >> d) & 1u)) continue;
-                bool in;
-                uint32_t vn = 0, hn = 0;
-                switch (d) {
-                    case 0: in = lx > 0; vn = v - dyz; hn = ly * dz + lz; break;
-                    case 1: in = lx + 1 < dx; vn = v + dyz; hn = ly * dz + lz; break;
-                    case 2: in = ly + 1 < dy; vn = v + dz; hn = lx * dz + lz; break;
-                    case 3: in = ly > 0; vn = v - dz; hn = lx * dz + lz; break;
-                    case 4: in = lz + 1 < dz; vn = v + 1; hn = lx * dy + ly; break;
-                    default: in = lz > 0; vn = v - 1; hn = lx * dy + ly; break;
+        bool quit = false;
+        for (int pass = 0; pass < 2; ++pass) {
+            if (pass == 1) {
+                // (4) the barrier; close round r - 1 (every block: the same cumulative count)
+                if (NB > 1 && !grid_wait(a.bar, i + 1u, NB, a.err)) {
+                    quit = true;
+                    break;
                 }
-                const uint32_t nb = in ? bl[vn] : hb[d * F + hn];
-                if ((nb & DIR_MASK) == (uint32_t)(d ^ 1)) {
-                    const double2 m = in ? swl[vn] : hsw[d * F + hn];
-                    acc_s = acc_s + m.x * 0.5;  // the oracle's rounding (no fused multiply-add)
-                    acc_w = acc_w + m.y * 0.5;
-                    recv = true;
-                }
-            }
-            uint32_t flags = bt & (B_ACTIVE | B_CONV | (3u << CNT_SHIFT));
-            bool act_n = active;
-            if (recv) {
-                if (!(bt & B_CONV)) {
-                    uint32_t c3 = (bt >> CNT_SHIFT) & 3u;
-                    c3 = ratio_moved(sv.x, sv.y, acc_s, acc_w) ? 0u : c3 + 1u;
-                    flags = (flags & ~(3u << CNT_SHIFT)) | (c3 << CNT_SHIFT);
-                    if (c3 == 3) {
-                        flags |= B_CONV;
-                        ++alerts;
+                if (NB == 1) __syncthreads();
+                if (i > 0) {
+                    const unsigned long long* cc = a.acc + 2 * ((r - 1u) % 3u);
+                    const unsigned long long ra = __hip_atomic_load(&cc[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const unsigned long long rn = __hip_atomic_load(&cc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    total += ra;
+                    act += rn;
+                    if (b == 0 && threadIdx.x == 0) {
+                        Ctl* ctl = a.ctl;
+                        ctl->hist[(r - 1u) % HIST] = ra;
+                        __hip_atomic_store(&ctl->alerts_total, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(&ctl->active_total, act, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (act >= a.G.P) __hip_atomic_store(&ctl->all_active, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (total >= a.G.T) __hip_atomic_store(&ctl->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        // the accumulator of round r + 1 (every block read it, for round r - 2, before
+                        // arriving at this barrier)
+                        unsigned long long* zz = a.acc + 2 * ((r + 1u) % 3u);
+                        __hip_atomic_store(&zz[0], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(&zz[1], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                    if (total >= a.G.T) {  // (the same decision in every block; round r is dropped)
+                        quit = true;
+                        break;
                     }
                 }
-                if (!active) {
-                    ++newly;
-                    flags |= B_ACTIVE;
-                    act_n = true;
+                if (i == a.nrounds) {
+                    quit = true;
+                    break;
                 }
+                // (5) the neighbours' facing layers -> LDS halos
+                {
+                    const size_t fp = (size_t)(i & 1u) * NB;
+        #pragma unroll
+                    for (int f = 0; f < 6; ++f) {
+                        if (!has[f]) continue;
+                        const size_t fo = ((fp + nbr_b[f]) * 6 + (f ^ 1)) * F;
+                        for (uint32_t t = threadIdx.x; t < fsz[f]; t += BK_THREADS) {
+                            // device-coherent loads (the other XCDs' faces, no L2 invalidate needed)
+                            unsigned long long* fq = reinterpret_cast<unsigned long long*>(a.fs + fo + t);
+                            const unsigned long long sx = __hip_atomic_load(&fq[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            const unsigned long long wx = __hip_atomic_load(&fq[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            hb[f * F + t] = (uint8_t)__hip_atomic_load(&a.fb[fo + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            hsw[f * F + t] = make_double2(__builtin_bit_cast(double, sx), __builtin_bit_cast(double, wx));
+                        }
+                    }
+                }
+                __syncthreads();
             }
-            uint32_t dir = DIR_NONE;
-            if (act_n && deg > 0) dir = slot_to_dir_fast(mask, uniform(a.k0, a.k1, S_PUSHSUM, x * g2 + y * g + z, r + 1, deg));
-            const double2 res = make_double2(acc_s, acc_w);
-            if (q == 0) n0 = res;
-            else if (q == 1) n1 = res;
-            else if (q == 2) n2 = res;
-            else if (q == 3) n3 = res;
-            else n4 = res;
-            bn[v] = (uint8_t)(flags | dir);
+            if (i == a.nrounds) continue;  // (the closing iteration: no node work)
+            // pass 0: the box interior's nodes, while the barrier completes (in registers and bn
+            // only: nothing is committed before round r - 1 is known not to be the last);
+            // pass 1: the nodes next to the box's faces, after the halos
+#pragma unroll 1
+            for (int q = 0; q < BK_NPT; ++q) {
+                const uint32_t v = q * BK_THREADS + threadIdx.x;
+                if (v >= V || GP_BK_ABL) break;  // (GP_BK_ABL: timing only, no node work)
+                double2 res;
+                if (!node(v, r, pass, res, alerts, newly)) continue;
+                if (q == 0) n0 = res;
+                else if (q == 1) n1 = res;
+                else if (q == 2) n2 = res;
+                else if (q == 3) n3 = res;
+                else n4 = res;
+            }
         }
+        if (quit) break;
         __syncthreads();  // every node has read the round-start state
-        // (6) the new state into LDS; the round's counts into its accumulator
+        // (7) commit: the new state into LDS; the round's counts into its accumulator
         {
             const double2 nq[BK_NPT] = {n0, n1, n2, n3, n4};
 #pragma unroll
             for (int q = 0; q < BK_NPT; ++q) {
                 const uint32_t v = q * BK_THREADS + threadIdx.x;
-                if (v < V) swl[v] = nq[q];
+                if (v < V) {
+                    swl[v] = nq[q];
+                    bl[v] = bn[v];
+                }
             }
-        }
-        {
-            uint8_t* t = bl;
-            bl = bn;
-            bn = t;
         }
         uint32_t xa = alerts, xn = newly;
 #pragma unroll
@@ -291,9 +364,9 @@ __global__ __launch_bounds__(BK_THREADS) void k_ps_block(BlockArgs a) {
                 xa += red[0][w];
                 xn += red[1][w];
             }
-            unsigned long long* c = a.acc + 2 * (r % 3u);
-            if (xa) __hip_atomic_fetch_add(&c[0], (unsigned long long)xa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (xn) __hip_atomic_fetch_add(&c[1], (unsigned long long)xn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            unsigned long long* cc = a.acc + 2 * (r % 3u);
+            if (xa) __hip_atomic_fetch_add(&cc[0], (unsigned long long)xa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (xn) __hip_atomic_fetch_add(&cc[1], (unsigned long long)xn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         ++done_rounds;
     }
@@ -323,7 +396,8 @@ bool block_plan(uint32_t g, int cus, BlockPlan& p) {
                 const uint64_t bx = (g + nx - 1) / nx, by = (g + ny - 1) / ny, bz = (g + nz - 1) / nz;
                 const uint64_t v = bx * by * bz;
                 const uint64_t f = std::max(by * bz, std::max(bx * bz, bx * by));
-                const uint64_t lds = 16 * (v + 6 * f) + 2 * v + 6 * f + 64;
+                const uint64_t ns = v + 6 * f + 1;
+                const uint64_t lds = 16 * ns + ((ns + 3) & ~3ull) + ((v + 3) & ~3ull) + 4 * v + 64;
                 if (v > (uint64_t)BK_NPT * BK_THREADS || lds > 150 * 1024 || bx > 1023 || by > 1023 || bz > 1023)
                     continue;
                 // estimated round time: node slots per thread (ceil(v / 1024)) plus a grid barrier
@@ -346,7 +420,7 @@ bool block_plan(uint32_t g, int cus, BlockPlan& p) {
 
 size_t block_face_bytes(const BlockPlan& p) {
     const size_t nb = (size_t)p.nbx * p.nby * p.nbz;
-    return 2 * nb * 6 * p.fmax * (16 + 1);
+    return 2 * nb * 6 * p.fmax * (16 + 4);
 }
 
 hipError_t launch_round_block(const DevState& S, const BlockPlan& p, uint32_t r0, uint32_t nrounds, void* face,
@@ -361,8 +435,9 @@ hipError_t launch_round_block(const DevState& S, const BlockPlan& p, uint32_t r0
     a.nb_alt = S.nb[cur];
     const size_t nb = (size_t)p.nbx * p.nby * p.nbz;
     a.fs = static_cast<double2*>(face);
-    a.fb = reinterpret_cast<uint8_t*>(a.fs + 2 * nb * 6 * p.fmax);
-    // scratch: [0] barrier, [1] error flag, then 3 x 2 accumulators (8-byte aligned)
+    a.fb = reinterpret_cast<uint32_t*>(a.fs + 2 * nb * 6 * p.fmax);
+    // scratch (words): [0] barrier (groups arrived), [1] error flag, [2..14) 3 x 2 accumulators,
+    // [16 (1 + grp)] the arrivals of block group grp (a 64-byte line each)
     a.bar = static_cast<unsigned int*>(scratch);
     a.err = a.bar + 1;
     a.acc = reinterpret_cast<unsigned long long*>(a.bar + 2);
@@ -377,7 +452,7 @@ hipError_t launch_round_block(const DevState& S, const BlockPlan& p, uint32_t r0
     a.nbz = p.nbz;
     a.fmax = p.fmax;
     a.vmax = p.vmax;
-    hipError_t e = hipMemsetAsync(scratch, 0, 8 + 6 * 8, st);
+    hipError_t e = hipMemsetAsync(scratch, 0, BLOCK_SCRATCH_BYTES, st);
     if (e != hipSuccess) return e;
     void* args[] = {&a};
     return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&k_ps_block), dim3((uint32_t)nb),

@@ -203,6 +203,7 @@ struct DevState {
     // whose sender lives on another rank, its list key (64 * header word + bit) in this
     // rank's received header region; the received headers and messages of the round
     uint32_t* rk;
+    double2* outbox;  // experiments (GP_OUTBOX=1): [tile * 1024 + rank] the tile's random-edge senders' (s, w)
     const XHdr* xhdr;
     const double2* xvals;
     uint32_t xnv;  // message slots in the vals region
@@ -244,6 +245,7 @@ struct RoundArgs {
     const uint32_t* rtag;    // per local in-edge: round of the delivered remote message (gossip)
     const double2* rmsg;
     const uint32_t* rk;      // push-sum: per local in-edge, the remote sender's list key (DevState::rk)
+    double2* outbox;         // experiments: the random-edge senders' next-round (s, w), per tile (DevState::outbox)
     const XHdr* xhdr;        // push-sum: the received header words / messages of the round
     const double2* xvals;
     uint32_t xnv;
@@ -270,8 +272,9 @@ enum KernelVariant : int { KERNEL_TILE = 1, KERNEL_COL = 2, KERNEL_BLOCK = 3 };
 bool block_plan(uint32_t g, int cus, BlockPlan& p);
 size_t block_face_bytes(const BlockPlan& p);
 hipError_t block_kernel_setup(const BlockPlan& p);
-// rounds [r0, r0 + nrounds) (fewer once the cumulative alerts reach T); scratch: 64 bytes,
-// word 1 is set if a grid barrier timed out
+// rounds [r0, r0 + nrounds) (fewer once the cumulative alerts reach T); scratch:
+// BLOCK_SCRATCH_BYTES, word 1 is set if a grid barrier timed out
+constexpr size_t BLOCK_SCRATCH_BYTES = 4 * 16 * 9;
 hipError_t launch_round_block(const struct DevState& S, const BlockPlan& p, uint32_t r0, uint32_t nrounds, void* face,
                               void* scratch, hipStream_t st);
 

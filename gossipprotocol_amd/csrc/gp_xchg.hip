@@ -307,22 +307,24 @@ __global__ __launch_bounds__(256) void k_list_key(ListKeyArgs a) {
     tile_list_rank(dst, rho, R, a.W);
     const int h = t < a.tsplit ? 0 : 1;
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-        if (dst[k] != XNONE)
-            a.key[sp.T + k * 256u + threadIdx.x] =
-                (a.hw[h][dst[k]] + a.gw[(size_t)t * a.W + dst[k]]) * 64u + rho[k];
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t j = sp.T + k * 256u + threadIdx.x;
+        if (dst[k] != XNONE) a.key[j] = (a.hw[h][dst[k]] + a.gw[(size_t)t * a.W + dst[k]]) * 64u + rho[k];
+        if (a.xdr && j >= sp.j0 && j < sp.j1)
+            a.xdr[j - a.lo] = dst[k] != XNONE ? (uint16_t)((dst[k] << 10) | rho[k]) : XDR_NONE;
+    }
 }
 
 // One round, one region: the header words and the compacted messages of every
 // destination.  A block of LP_TILES waves takes LP_TILES consecutive tiles (8192
-// senders), one per wave, walked as 16 slots of 64 consecutive ids: a node's rank among the
-// tile's entries of its destination is the wave's running count (scalar) plus the
-// lanes below in the slot's ballot -- no LDS table, no barrier per tile.  The used
-// entries' bits go into the wave's LDS words, the wave scans the words' counts; then,
-// for all the block's tiles at once, ONE reservation per destination (a reservation
-// per tile queued ~60 k returning atomics on each of a C5 slab's 14 counters per
-// round: 0.73 ms per region at W = 8), the header words and the messages in list
-// order.  Two barriers per block.
+// senders), one per wave, walked as 16 slots of 64 consecutive ids.  A sender's
+// destination and rank in its tile's list are static (xdr, k_list_key at create) and so
+// is the tile's LDS word layout (lwt): a used entry's bit is one LDS atomic, no ranking
+// per round (ballots per slot and destination made the pack VALU-bound: 0.60 -> ? ms per
+// C5 slab at W = 8).  The wave scans its words' counts; then, for all the block's tiles
+// at once, ONE reservation per destination (a reservation per tile queued ~60 k
+// returning atomics on each of a C5 slab's 14 counters per round: 0.73 ms per region),
+// the header words and the messages in list order.  Two barriers per block.
 constexpr int LIST_LW = XTILE / 64 + XMAXW;  // LDS words of one tile's segments (<= 16 full + 1 partial each)
 constexpr int LP_TILES = 8;                  // = waves per block
 constexpr int LP_WT = 1;                     // tiles per wave
@@ -347,65 +349,52 @@ __global__ __launch_bounds__(LP_THREADS) void k_list_pack(ListPackArgs a) {
         ovals[threadIdx.x] = a.peer[threadIdx.x].vals;
         ocap[threadIdx.x] = a.peer[threadIdx.x].cap;
     }
+    if (threadIdx.x < (uint32_t)(LP_TILES * (W + 1))) {  // the tiles' static LDS word layouts
+        const uint32_t tt = threadIdx.x / (W + 1), d = threadIdx.x - tt * (W + 1);
+        if ((int)tt < ntl) lw[tt][d] = a.lwt[(size_t)(tb + tt) * (W + 1) + d];
+    }
     __syncthreads();
-    // per tile of this wave and slot pair: used ? 0x8000 | d << 11 | rho : 0 (rho < 1024), 16 bits a slot
-    uint32_t st[LP_WT][LP_SLOTS / 2];
+    // per tile of this wave and slot: used ? 1 << 31 | d << 11 | rho : 0 (rho < 1024)
+    uint32_t st[LP_WT][LP_SLOTS];
 #pragma unroll
     for (int u = 0; u < LP_WT; ++u) {
 #pragma unroll
-        for (int q = 0; q < LP_SLOTS / 2; ++q) st[u][q] = 0u;
+        for (int q = 0; q < LP_SLOTS; ++q) st[u][q] = 0u;
         const int tt = (int)wv * LP_WT + u;
         if (tt >= ntl) break;  // (wave-uniform)
         const TileSpan sp = tile_span(a.lo, a.nloc, tb + tt);
-        uint8_t b[LP_SLOTS], x[LP_SLOTS];
+        uint8_t b[LP_SLOTS];
+        uint16_t x[LP_SLOTS];
         xchg_prio<1>();
 #pragma unroll
         for (int q = 0; q < LP_SLOTS; ++q) {  // unconditional (clamped) loads, all in flight
             const uint32_t j = min(max(sp.T + q * 64u + lane, sp.j0), sp.j1 - 1u);
             b[q] = a.nbn[j - a.base];
-            x[q] = a.xdst[j - a.lo];
+            x[q] = a.xdr[j - a.lo];
         }
         xchg_prio<0>();
-        uint32_t run[XMAXW];  // the tile's entries per destination so far (wave-uniform)
-#pragma unroll
-        for (int d = 0; d < XMAXW; ++d) run[d] = 0u;
+        uint32_t orun = 0;  // the tile's random-edge senders so far (outbox ranks, GP_OUTBOX)
 #pragma unroll
         for (int q = 0; q < LP_SLOTS; ++q) {
             const uint32_t j = sp.T + q * 64u + lane;
-            const bool in = j >= sp.j0 && j < sp.j1 && x[q] != me;
-            const uint32_t dst = in ? (uint32_t)x[q] : XNONE;
-            uint32_t rho = 0;
-#pragma unroll
-            for (int d = 0; d < XMAXW; ++d)
-                if (d < W) {
-                    const unsigned long long m = __ballot(dst == (uint32_t)d);
-                    if (dst == (uint32_t)d) rho = run[d] + lane_below(m);
-                    run[d] += (uint32_t)__popcll(m);
-                }
-            if (in && (b[q] & DIR_MASK) == DIR_RANDOM) st[u][q >> 1] |= (0x8000u | (dst << 11) | rho) << (16 * (q & 1));
-        }
-        // the tile's segments: destination d's words from lw[tt][d] (ceil(entries / 64))
-        uint32_t w0 = 0;
-#pragma unroll
-        for (int d = 0; d < XMAXW; ++d)
-            if (d < W) {
-                if (lane == (uint32_t)d) lw[tt][d] = w0;
-                w0 += (run[d] + 63u) / 64u;
+            const bool rnd = j >= sp.j0 && j < sp.j1 && (b[q] & DIR_MASK) == DIR_RANDOM;
+            uint32_t ord = 0;
+            if (a.outbox) {
+                const unsigned long long rb = __ballot(rnd);
+                ord = orun + lane_below(rb);
+                orun += (uint32_t)__popcll(rb);
             }
-        if (lane == 0) lw[tt][W] = w0;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-        for (int q = 0; q < LP_SLOTS; ++q) {
-            const uint32_t e = (st[u][q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
-            if (e & 0x8000u) {
-                const uint32_t d = (e >> 11) & 15u, rho = e & 0x7FFu;
+            const bool used = rnd && x[q] != XDR_NONE;
+            if (used) {
+                const uint32_t d = x[q] >> 10, rho = x[q] & 1023u;
+                st[u][q] = 0x80000000u | (ord << 15) | (d << 11) | rho;
                 const uint32_t w = lw[tt][d] + (rho >> 6);
                 atomicOr(&mk[tt][2 * w + ((rho >> 5) & 1u)], 1u << (rho & 31u));
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         // word prefixes within each destination's segment, and the tile's used entries per destination
-        const uint32_t nw = w0;  // <= LIST_LW <= 64: one wave-wide scan
+        const uint32_t nw = lw[tt][W];  // <= LIST_LW <= 64: one wave-wide scan
         const uint32_t l = lane;
         uint32_t seg = 0;
         for (int d = 1; d < W; ++d) seg += l >= lw[tt][d] ? 1u : 0u;
@@ -456,8 +445,13 @@ __global__ __launch_bounds__(LP_THREADS) void k_list_pack(ListPackArgs a) {
             }
         }
         // the used entries' (s, w): buffer loads over the tile's ids, past the end for the
-        // others (no memory touched, no load under a branch), four slots in flight
-        const __amdgpu_buffer_rsrc_t rs = buf_rsrc(a.swn + (sp.j0 - a.base), (sp.j1 - sp.j0) * 16u);
+        // others (no memory touched, no load under a branch), four slots in flight.  (A compacted
+        // outbox of the random-edge senders' (s, w), written by the round kernel, cut the pack's
+        // reads but cost the round kernel more than it saved: 0.60 -> 0.58 ms for the pack,
+        // 1.94 -> 2.24 ms for the round kernel at W = 8, profiles/r05/rejected/outbox.txt)
+        const bool obx = a.outbox != nullptr;
+        const __amdgpu_buffer_rsrc_t rs = obx ? buf_rsrc(a.outbox + (size_t)(tb + tt) * XTILE, XTILE * 16u)
+                                              : buf_rsrc(a.swn + (sp.j0 - a.base), (sp.j1 - sp.j0) * 16u);
 #pragma unroll
         for (int q0 = 0; q0 < LP_SLOTS; q0 += 4) {
             double2 v[4];
@@ -466,16 +460,17 @@ __global__ __launch_bounds__(LP_THREADS) void k_list_pack(ListPackArgs a) {
             for (int h = 0; h < 4; ++h) {
                 const int q = q0 + h;
                 const uint32_t j = sp.T + q * 64u + lane;
-                const bool used = (st[u][q >> 1] >> (16 * (q & 1))) & 0x8000u;
-                const auto w4 = __builtin_amdgcn_raw_buffer_load_b128(rs, used ? (j - sp.j0) * 16u : BUF_NONE, 0, 0);
+                const uint32_t e = st[u][q];
+                const uint32_t o = obx ? ((e >> 15) & 1023u) * 16u : (j - sp.j0) * 16u;
+                const auto w4 = __builtin_amdgcn_raw_buffer_load_b128(rs, (e & 0x80000000u) ? o : BUF_NONE, 0, 0);
                 v[h] = __builtin_bit_cast(double2, w4);
             }
             xchg_prio<0>();
 #pragma unroll
             for (int h = 0; h < 4; ++h) {
                 const int q = q0 + h;
-                const uint32_t e = (st[u][q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
-                if (!(e & 0x8000u)) continue;
+                const uint32_t e = st[u][q];
+                if (!(e & 0x80000000u)) continue;
                 const uint32_t d = (e >> 11) & 15u, rho = e & 0x7FFu;
                 const uint32_t w = lw[tt][d] + (rho >> 6), bit = rho & 63u;
                 const unsigned long long m = ((unsigned long long)mk[tt][2 * w + 1] << 32) | mk[tt][2 * w];

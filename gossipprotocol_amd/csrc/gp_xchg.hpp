@@ -100,7 +100,9 @@ struct ListPeer {              // send side: region h, destination d
 struct ListPackArgs {
     const uint8_t* nbn;        // node bytes of the round being prepared (local array, id - base)
     const double2* swn;        // (s, w) of that round (local array, id - base)
-    const uint8_t* xdst;       // owner rank of each local sender's random-edge target (id - lo)
+    const uint16_t* xdr;       // [id - lo]: d << 10 | the sender's rank in its tile's list for d (static), or XDR_NONE
+    const double2* outbox;     // experiments: [tile * XTILE + rank] the round kernel's random-edge senders' (s, w)
+    const uint8_t* lwt;        // [tile * (W + 1) + d]: first LDS word of d's segment in the tile (static)
     const uint32_t* gw;        // [tile * W + d]: first header word of the tile's segment in chunk (region, d)
     uint32_t lo, nloc, base;
     uint32_t t0, t1;           // the region's tiles (relative to lo / XTILE)
@@ -125,7 +127,9 @@ struct ListKeyArgs {           // setup, slab a: every sender's list key at its 
     uint32_t bounds[XMAXW + 1];
     uint32_t hw[2][XMAXW];     // [h][b]: first header word of chunk (h, a) in b's header region
     uint32_t* key;             // [global id]: 64 * header word + bit at the destination (local targets untouched)
+    uint16_t* xdr;             // optional, [id - lo]: d << 10 | rank in the tile's list for d, or XDR_NONE
 };
+constexpr uint16_t XDR_NONE = 0xFFFFu;
 
 // ---- Imp3D gossip on the column kernel across ranks: random-edge sends as bitmaps
 // (round 5).  For each rank pair a -> b the static list of edges from a's senders to

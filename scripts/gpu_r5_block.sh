@@ -12,4 +12,4 @@ c2() {
   echo "c2 $l: $(grep -o 'wall [0-9.]* ms/round' $O/c2_$l.log | head -1) $(grep -o '[0-9.]* ms/round kernel' $O/c2_$l.log | head -1) $(grep -o 'no events: wall [0-9.]* ms/round' $O/c2_$l.log | head -1)"
 }
 c2 block GP_X=0 && c2 tile GP_EXP=1 GP_KERNEL=tile && c2 block2 GP_X=0 || exit 1
-O=gpurun_out/r5_xchg bash scripts/gpu_r5_xchg.sh
+if [ -n "$WITH_XCHG" ]; then O=gpurun_out/r5_xchg bash scripts/gpu_r5_xchg.sh; fi

@@ -110,6 +110,11 @@ def pair_bytes(n, topo, alg, W, halves=1, lists=True):
                         edges = na * (bounds[b + 1] - bounds[b]) / (P - 1)
                         B[a][b] = int(16 * (edges / 64 + nt / 2)) + sum(16 * cap_of(mu[a, b] / halves)
                                                                         for _ in range(halves))
+                    elif not push and lists:
+                        # gossip (column kernel) since round 5: one bit per edge a -> b, chunks
+                        # padded to 1024 bits
+                        edges = na * (bounds[b + 1] - bounds[b]) / (P - 1)
+                        B[a][b] = int(math.ceil(edges / 1024) * 128)
                     else:  # {slot, (s, w)} buffers (round 4) / gossip counts
                         B[a][b] = sum(xbuf(cap_of(mu[a, b] / halves)) for _ in range(halves))
     return P, bounds, B, halo
@@ -165,7 +170,8 @@ def model(tdir, n, topo, alg, W, rounds, out=None):
     # (Imp3D push-sum since round 5: k_list_pack per region, no unpack -- the round kernel reads the
     # received lists in place)
     first_k, second_k = ("k_fbm_send", "k_fbm_coarse") if topo == "full" else ("k_list_pack", None)
-    legacy = topo != "full" and "k_unpack" in per_slab_names(groups, short)  # a round-4 build (A/B runs)
+    # a round-4 build (A/B runs): {slot} / {count} buffers with an unpack pass
+    legacy = topo != "full" and any("k_unpack" in k for k in per_slab_names(groups, short))
     if legacy:
         first_k, second_k = "k_pack", "k_unpack"
     P, bounds, B, halo = pair_bytes(n, topo, alg, W, halves, lists=not legacy)
