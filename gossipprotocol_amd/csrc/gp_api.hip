@@ -305,7 +305,6 @@ int alloc_slab(gp_sim* s, Slab& sl, int r) {
     S.rtag = nullptr;
     S.rmsg = nullptr;
     S.rk = nullptr;
-    S.outbox = nullptr;
     S.rtg = nullptr;
     S.sbits = nullptr;
     S.xhdr = nullptr;
@@ -525,11 +524,6 @@ int build_lists(gp_sim* s, const uint32_t* rnd_all, uint32_t* kk, const uint32_t
         const uint32_t ne = edge0[r + 1] - edge0[r];
         if ((rc = dev_alloc_t(s, &S.rk, (size_t)ne + 4))) return rc;
         HIP_TRY(launch_gather_keys(kk, src + edge0[r], ne, S.rk, s->grid, s->stream));
-#ifdef GP_EXPERIMENTS
-        // GP_OUTBOX=1: the round kernel compacts its random-edge senders' (s, w) for the pack
-        if (const char* e = std::getenv("GP_OUTBOX"))
-            if (e[0] == '1' && (rc = dev_alloc_t(s, &S.outbox, (size_t)sl.nt * XTILE))) return rc;
-#endif
 
     }
     HIP_TRY(hipStreamSynchronize(s->stream));
@@ -1146,7 +1140,6 @@ int exchange(gp_sim* s, uint32_t rn) {
                     la.nbn = S.nb[b];
                     la.swn = S.sw[b];
                     la.xdr = sl.xdr;
-                    la.outbox = S.outbox;
                     la.lwt = sl.lwt;
                     la.gw = sl.gw;
                     la.lo = S.lo;

@@ -65,44 +65,40 @@ __device__ __forceinline__ uint32_t split(uint32_t g, uint32_t i, uint32_t n) {
 
 __device__ __forceinline__ uint64_t now_10ns() { return __builtin_amdgcn_s_memrealtime(); }  // 100 MHz
 
-// Grid barrier k (k = 1, 2, ...), in two halves (grid_arrive, grid_wait) so that the
-// box interior's nodes are computed while the barrier completes.  Faces are written and
-// read with device-coherent (agent-scope, relaxed atomic) stores and loads, so no cache
-// write-back or invalidate is needed: each wave waits for its face stores to be
-// performed (vmcnt) before the workgroup barrier, thread 0 then arrives.  Arrivals are
-// non-returning adds on one counter per group of blocks (blockIdx % 8: the blocks of one
-// XCD), so no word takes more than ~NB / 8 atomics per barrier (one word takes ~88 per
-// microsecond); the waiters poll the 8 counters at once; counters are never reset inside
-// a launch.  Waits at most ~2 s.  (Agent-scope release / acquire fences -- an L2
-// write-back and invalidate per block and barrier -- left a C2 round at 27 us of barrier
-// and face time, 37 us in all.)
-__device__ __forceinline__ void grid_arrive(unsigned int* bar, unsigned int k, unsigned int nb) {
-    (void)k;
-    (void)nb;
+// Grid barrier k (k = 1, 2, ...).  Faces are written and read with device-coherent
+// (agent-scope, relaxed atomic) stores and loads, so no cache write-back or invalidate is
+// needed: each wave waits for its face stores to be performed (vmcnt) before the
+// workgroup barrier, thread 0 then arrives.  Arrivals are counted per group of blocks
+// (blockIdx % 8: the blocks of one XCD) and the last of a group arrives on the global
+// word, so no word takes more than ~NB / 8 returning atomics per barrier (one word takes
+// ~88 per microsecond); counters are never reset inside a launch.  Waits at most ~2 s.
+// Measured at C2 (profiles/r05/c2/): agent-scope release / acquire fences in every wave
+// (an L2 write-back and invalidate each) 133 us per round; one per block 37 us; this form
+// 19 us, of which 9.5 us is faces and barrier (no-node-work ablation).  Rejected: non-
+// returning arrivals with the waiters polling all 8 group counters (11.4 us ablation), and
+// computing the box interior while the barrier completes (22 us: the two passes over the
+// node slots cost more than the wait they hide).
+__device__ __forceinline__ bool grid_sync(unsigned int* bar, unsigned int k, unsigned int nb, unsigned int* err) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0)  // a non-returning add on this block group's counter (a 64-byte line each)
-        __hip_atomic_fetch_add(bar + 16u * (1u + (blockIdx.x & 7u)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ bool grid_wait(unsigned int* bar, unsigned int k, unsigned int nb, unsigned int* err) {
     __shared__ unsigned int ok;
-    if (threadIdx.x < 64) {  // lane grp < 8 polls group grp's counter
-        const unsigned int grp = threadIdx.x;
-        const unsigned int want = grp < 8u ? k * ((nb + 7u - grp) / 8u) : 0u;
+    if (threadIdx.x == 0) {
+        ok = 1u;
+        const unsigned int grp = blockIdx.x & 7u;
+        const unsigned int members = (nb - grp + 7u) / 8u;
+        const unsigned int groups = nb < 8u ? nb : 8u;
+        unsigned int* gc = bar + 16u * (1u + grp);  // a 64-byte line per group counter
+        const unsigned int prev = __hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev + 1u == k * members) __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint64_t t0 = now_10ns();
-        bool fail = false;
-        for (;;) {
-            const unsigned int got =
-                grp < 8u ? __hip_atomic_load(bar + 16u * (1u + grp), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-            if (__ballot(got < want) == 0ull) break;
+        while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < k * groups) {
             if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || now_10ns() - t0 > 200000000ull) {
-                if (threadIdx.x == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                fail = true;
+                __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = 0u;
                 break;
             }
             __builtin_amdgcn_s_sleep(1);
         }
-        if (threadIdx.x == 0) ok = fail ? 0u : 1u;
     }
     __syncthreads();
     return ok != 0u;
@@ -143,13 +139,7 @@ __global__ __launch_bounds__(BK_THREADS) void k_ps_block(BlockArgs a) {
         const uint32_t j = (x0 + lx) * g2 + (y0 + ly) * g + (z0 + lz);
         swl[v] = a.sw_in[j];
         bl[v] = a.nb_in[j];
-        // (no divisions per node and round); bit 30: the node has a lattice neighbour outside the
-        // box (it reads a halo, so it is computed after the barrier)
-        const uint32_t x = x0 + lx, y = y0 + ly, z = z0 + lz;
-        const uint32_t mask = mask_xyz(x, y, z, gm);
-        const bool bnd = ((mask & 1u) && lx == 0) || ((mask & 2u) && lx + 1 == dx) || ((mask & 4u) && ly + 1 == dy) ||
-                         ((mask & 8u) && ly == 0) || ((mask & 16u) && lz + 1 == dz) || ((mask & 32u) && lz == 0);
-        ct[v] = lx | (ly << 10) | (lz << 20) | (bnd ? 1u << 30 : 0u);
+        ct[v] = lx | (ly << 10) | (lz << 20);  // (no divisions per node and round)
     }
     if (threadIdx.x == 0) {
         swl[NS] = make_double2(0.0, 0.0);
@@ -163,12 +153,10 @@ __global__ __launch_bounds__(BK_THREADS) void k_ps_block(BlockArgs a) {
     // One node of round r: the tile kernel's fold (own half, the lattice messages in the
     // receiver's slot order -- Program.fs:246-257 -- acc + m * 0.5, the oracle's rounding;
     // a direction without a message adds +0.0, exact for the non-negative s and w), the
-    // ratio test (Program.fs:114-123), the next direction by Philox.  pass 0: only nodes
-    // whose neighbours are all in the box; pass 1: only the others (they read halos).
-    auto node = [&](uint32_t v, uint32_t r, int pass, double2& res, uint32_t& alerts, uint32_t& newly) {
+    // ratio test (Program.fs:114-123), the next direction by Philox.
+    auto node = [&](uint32_t v, uint32_t r, double2& res, uint32_t& alerts, uint32_t& newly) {
         const uint32_t c = ct[v];
-        if (((c >> 30) & 1u) != (uint32_t)pass) return false;
-        const uint32_t lx = c & 1023u, ly = (c >> 10) & 1023u, lz = (c >> 20) & 1023u;
+        const uint32_t lx = c & 1023u, ly = (c >> 10) & 1023u, lz = c >> 20;
         const uint32_t x = x0 + lx, y = y0 + ly, z = z0 + lz;
         const uint32_t mask = mask_xyz(x, y, z, gm);
         const uint32_t bt = bl[v];
@@ -218,7 +206,6 @@ __global__ __launch_bounds__(BK_THREADS) void k_ps_block(BlockArgs a) {
         if (act_n && deg > 0) dir = slot_to_dir_fast(mask, uniform(a.k0, a.k1, S_PUSHSUM, x * g2 + y * g + z, r + 1, deg));
         res = make_double2(acc_s, acc_w);
         bn[v] = (uint8_t)(flags | dir);
-        return true;
     };
     for (uint32_t i = 0; i <= a.nrounds && !stop; ++i) {
         const uint32_t r = a.r0 + i;
@@ -251,91 +238,70 @@ __global__ __launch_bounds__(BK_THREADS) void k_ps_block(BlockArgs a) {
                 }
             }
         }
-        // (2) arrive at barrier i + 1 (faces of round r written, round r - 1's counts added)
-        if (NB > 1) grid_arrive(a.bar, i + 1u, NB);
-        // (3) the box interior's nodes of round r while the barrier completes (in registers and
-        // bn only: nothing is committed before round r - 1 is known not to be the last)
-        uint32_t alerts = 0, newly = 0;
-        // the new (s, w) of node slot q in n[q] (named registers, selected by q: the slot loop
-        // is not unrolled -- unrolled, the compiler interleaved all slots and spilled)
-        double2 n0 = make_double2(0.0, 0.0), n1 = n0, n2 = n0, n3 = n0, n4 = n0;
-        static_assert(BK_NPT == 5, "one named register pair per node slot");
-        bool quit = false;
-        for (int pass = 0; pass < 2; ++pass) {
-            if (pass == 1) {
-                // (4) the barrier; close round r - 1 (every block: the same cumulative count)
-                if (NB > 1 && !grid_wait(a.bar, i + 1u, NB, a.err)) {
-                    quit = true;
-                    break;
-                }
-                if (NB == 1) __syncthreads();
-                if (i > 0) {
-                    const unsigned long long* cc = a.acc + 2 * ((r - 1u) % 3u);
-                    const unsigned long long ra = __hip_atomic_load(&cc[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const unsigned long long rn = __hip_atomic_load(&cc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    total += ra;
-                    act += rn;
-                    if (b == 0 && threadIdx.x == 0) {
-                        Ctl* ctl = a.ctl;
-                        ctl->hist[(r - 1u) % HIST] = ra;
-                        __hip_atomic_store(&ctl->alerts_total, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        __hip_atomic_store(&ctl->active_total, act, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        if (act >= a.G.P) __hip_atomic_store(&ctl->all_active, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        if (total >= a.G.T) __hip_atomic_store(&ctl->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        // the accumulator of round r + 1 (every block read it, for round r - 2, before
-                        // arriving at this barrier)
-                        unsigned long long* zz = a.acc + 2 * ((r + 1u) % 3u);
-                        __hip_atomic_store(&zz[0], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        __hip_atomic_store(&zz[1], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    }
-                    if (total >= a.G.T) {  // (the same decision in every block; round r is dropped)
-                        quit = true;
-                        break;
-                    }
-                }
-                if (i == a.nrounds) {
-                    quit = true;
-                    break;
-                }
-                // (5) the neighbours' facing layers -> LDS halos
-                {
-                    const size_t fp = (size_t)(i & 1u) * NB;
-        #pragma unroll
-                    for (int f = 0; f < 6; ++f) {
-                        if (!has[f]) continue;
-                        const size_t fo = ((fp + nbr_b[f]) * 6 + (f ^ 1)) * F;
-                        for (uint32_t t = threadIdx.x; t < fsz[f]; t += BK_THREADS) {
-                            // device-coherent loads (the other XCDs' faces, no L2 invalidate needed)
-                            unsigned long long* fq = reinterpret_cast<unsigned long long*>(a.fs + fo + t);
-                            const unsigned long long sx = __hip_atomic_load(&fq[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            const unsigned long long wx = __hip_atomic_load(&fq[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            hb[f * F + t] = (uint8_t)__hip_atomic_load(&a.fb[fo + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            hsw[f * F + t] = make_double2(__builtin_bit_cast(double, sx), __builtin_bit_cast(double, wx));
-                        }
-                    }
-                }
-                __syncthreads();
+        // (2) barrier i + 1: faces of round r written, round r - 1's counts complete
+        if (NB > 1 && !grid_sync(a.bar, i + 1u, NB, a.err)) break;
+        if (NB == 1) __syncthreads();
+        // (3) close round r - 1 (every block: the same cumulative count)
+        if (i > 0) {
+            const unsigned long long* cc = a.acc + 2 * ((r - 1u) % 3u);
+            const unsigned long long ra = __hip_atomic_load(&cc[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long rn = __hip_atomic_load(&cc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            total += ra;
+            act += rn;
+            if (b == 0 && threadIdx.x == 0) {
+                Ctl* ctl = a.ctl;
+                ctl->hist[(r - 1u) % HIST] = ra;
+                __hip_atomic_store(&ctl->alerts_total, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&ctl->active_total, act, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (act >= a.G.P) __hip_atomic_store(&ctl->all_active, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (total >= a.G.T) __hip_atomic_store(&ctl->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                // the accumulator of round r + 1 (every block read it, for round r - 2, before
+                // arriving at this barrier)
+                unsigned long long* zz = a.acc + 2 * ((r + 1u) % 3u);
+                __hip_atomic_store(&zz[0], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&zz[1], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            if (i == a.nrounds) continue;  // (the closing iteration: no node work)
-            // pass 0: the box interior's nodes, while the barrier completes (in registers and bn
-            // only: nothing is committed before round r - 1 is known not to be the last);
-            // pass 1: the nodes next to the box's faces, after the halos
-#pragma unroll 1
-            for (int q = 0; q < BK_NPT; ++q) {
-                const uint32_t v = q * BK_THREADS + threadIdx.x;
-                if (v >= V || GP_BK_ABL) break;  // (GP_BK_ABL: timing only, no node work)
-                double2 res;
-                if (!node(v, r, pass, res, alerts, newly)) continue;
-                if (q == 0) n0 = res;
-                else if (q == 1) n1 = res;
-                else if (q == 2) n2 = res;
-                else if (q == 3) n3 = res;
-                else n4 = res;
+            if (total >= a.G.T) break;  // (the same decision in every block)
+        }
+        if (i == a.nrounds) break;
+        // (4) the neighbours' facing layers -> LDS halos
+        {
+            const size_t fp = (size_t)(i & 1u) * NB;
+#pragma unroll
+            for (int f = 0; f < 6; ++f) {
+                if (!has[f]) continue;
+                const size_t fo = ((fp + nbr_b[f]) * 6 + (f ^ 1)) * F;
+                for (uint32_t t = threadIdx.x; t < fsz[f]; t += BK_THREADS) {
+                    // device-coherent loads (the other XCDs' faces, no L2 invalidate needed)
+                    unsigned long long* fq = reinterpret_cast<unsigned long long*>(a.fs + fo + t);
+                    const unsigned long long sx = __hip_atomic_load(&fq[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const unsigned long long wx = __hip_atomic_load(&fq[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    hb[f * F + t] = (uint8_t)__hip_atomic_load(&a.fb[fo + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    hsw[f * F + t] = make_double2(__builtin_bit_cast(double, sx), __builtin_bit_cast(double, wx));
+                }
             }
         }
-        if (quit) break;
+        __syncthreads();
+        // (5) the round for this thread's nodes: the new (s, w) of node slot q in n[q] (named
+        // registers, selected by q: the slot loop is not unrolled -- unrolled, the compiler
+        // interleaved all slots and spilled); the new node bytes go to bn
+        uint32_t alerts = 0, newly = 0;
+        double2 n0 = make_double2(0.0, 0.0), n1 = n0, n2 = n0, n3 = n0, n4 = n0;
+        static_assert(BK_NPT == 5, "one named register pair per node slot");
+#pragma unroll 1
+        for (int q = 0; q < BK_NPT; ++q) {
+            const uint32_t v = q * BK_THREADS + threadIdx.x;
+            if (v >= V || GP_BK_ABL) break;  // (GP_BK_ABL: timing only, no node work)
+            double2 res;
+            node(v, r, res, alerts, newly);
+            if (q == 0) n0 = res;
+            else if (q == 1) n1 = res;
+            else if (q == 2) n2 = res;
+            else if (q == 3) n3 = res;
+            else n4 = res;
+        }
         __syncthreads();  // every node has read the round-start state
-        // (7) commit: the new state into LDS; the round's counts into its accumulator
+        // (6) commit: the new state into LDS; the round's counts into its accumulator
         {
             const double2 nq[BK_NPT] = {n0, n1, n2, n3, n4};
 #pragma unroll

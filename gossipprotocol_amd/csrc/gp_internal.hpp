@@ -203,7 +203,6 @@ struct DevState {
     // whose sender lives on another rank, its list key (64 * header word + bit) in this
     // rank's received header region; the received headers and messages of the round
     uint32_t* rk;
-    double2* outbox;  // experiments (GP_OUTBOX=1): [tile * 1024 + rank] the tile's random-edge senders' (s, w)
     const XHdr* xhdr;
     const double2* xvals;
     uint32_t xnv;  // message slots in the vals region
@@ -245,7 +244,6 @@ struct RoundArgs {
     const uint32_t* rtag;    // per local in-edge: round of the delivered remote message (gossip)
     const double2* rmsg;
     const uint32_t* rk;      // push-sum: per local in-edge, the remote sender's list key (DevState::rk)
-    double2* outbox;         // experiments: the random-edge senders' next-round (s, w), per tile (DevState::outbox)
     const XHdr* xhdr;        // push-sum: the received header words / messages of the round
     const double2* xvals;
     uint32_t xnv;

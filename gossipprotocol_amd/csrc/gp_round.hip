@@ -136,7 +136,6 @@ struct TileLdsP {
     uint32_t out[TILE / 4];
     uint32_t red[2][TPB / 64];
     uint32_t qn[2];                   // walk 3: the block's next item, by iteration parity
-    uint32_t ocnt[NPT][TPB / 64];     // REMOTE with an outbox: random-edge senders per (node slot, wave)
     double2 zb[TPB / 64][NPT][2];     // GP_ZDPP: (s, w) across each wave's ends, slot k: [0] node - 1, [1] node + 64
 };
 
@@ -921,10 +920,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                         // next-round direction drawn below, one Philox batch for the thread's nodes
                         pend[k >> 1] |= (mask | (active && deg > 0 ? 64u : 0u) | ((flags >> 3) << 7)) << (16 * (k & 1));
                         if (GP_SETPRIO >= 5) __builtin_amdgcn_s_setprio(GP_PRIO);
-                        // (REMOTE with an outbox, experiments: plain stores, so that the outbox's
-                        // re-read of the random-edge senders' values below hits the L2)
-                        if (REMOTE && a.outbox) swn[j] = make_double2(acc_s, acc_w);
-                        else st_stream(swn + j, make_double2(acc_s, acc_w));
+                        st_stream(swn + j, make_double2(acc_s, acc_w));
                         if (GP_SETPRIO >= 5) __builtin_amdgcn_s_setprio(0);
                     }
                 }
@@ -951,34 +947,12 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                     if (lane == 0) {  // the slab's first tile may start below lo: no word there
                         const int64_t wi = (int64_t)((T + k * TPB + (threadIdx.x & ~63u)) >> 6) - (int64_t)(a.lo >> 6);
                         if (wi >= 0) a.rbn[wi] = bits;
-                        if (REMOTE) L.ocnt[k][wv] = (uint32_t)__popcll(bits);
                     }
                 }
             }
         }
         __syncthreads();
         GP_STAMP(t5);
-        if (REMOTE && a.outbox) {
-            // experiments (GP_OUTBOX=1): the (s, w) of the tile's senders that use their random edge
-            // next round, compacted in id order at outbox[tile * TILE + rank], for k_list_pack
-            double2* ob = a.outbox + (size_t)(T / TILE - a.lo / TILE) * TILE;
-            uint32_t run = 0;  // random-edge senders of the slots before k (wave-uniform)
-#pragma unroll
-            for (int k = 0; k < NPT; ++k) {
-                uint32_t kb = run;
-#pragma unroll
-                for (int w = 0; w < TPB / 64; ++w) {
-                    const uint32_t c = L.ocnt[k][w];
-                    kb += w < (int)wv ? c : 0u;
-                    run += c;
-                }
-                const uint32_t jl = k * TPB + threadIdx.x;
-                const uint32_t j = T + jl;
-                const bool rnd = j >= j0 && j < j1 && (lds_byte(L.out, jl) & DIR_MASK) == DIR_RANDOM;
-                const unsigned long long bits = __ballot(rnd);
-                if (rnd) ob[kb + mbcnt64(bits)] = swn[j];
-            }
-        }
         // node bytes out as words (allocations are padded past P)
         for (uint32_t w = threadIdx.x; w < (uint32_t)(TILE / 4); w += TPB) {
             const uint32_t jw = T + w * 4;
@@ -1281,7 +1255,6 @@ RoundArgs make_round_args(const DevState& S, uint32_t round) {
     a.rtag = S.rtag;
     a.rmsg = S.rmsg;
     a.rk = S.rk;
-    a.outbox = S.outbox;
     a.xhdr = S.xhdr;
     a.xvals = S.xvals;
     a.xnv = S.xnv;

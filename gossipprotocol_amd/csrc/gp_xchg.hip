@@ -320,7 +320,7 @@ __global__ __launch_bounds__(256) void k_list_key(ListKeyArgs a) {
 // senders), one per wave, walked as 16 slots of 64 consecutive ids.  A sender's
 // destination and rank in its tile's list are static (xdr, k_list_key at create) and so
 // is the tile's LDS word layout (lwt): a used entry's bit is one LDS atomic, no ranking
-// per round (ballots per slot and destination made the pack VALU-bound: 0.60 -> ? ms per
+// per round (ballots per slot and destination made the pack VALU-bound: 0.69 -> 0.52-0.60 ms per
 // C5 slab at W = 8).  The wave scans its words' counts; then, for all the block's tiles
 // at once, ONE reservation per destination (a reservation per tile queued ~60 k
 // returning atomics on each of a C5 slab's 14 counters per round: 0.73 ms per region),
@@ -373,21 +373,13 @@ __global__ __launch_bounds__(LP_THREADS) void k_list_pack(ListPackArgs a) {
             x[q] = a.xdr[j - a.lo];
         }
         xchg_prio<0>();
-        uint32_t orun = 0;  // the tile's random-edge senders so far (outbox ranks, GP_OUTBOX)
 #pragma unroll
         for (int q = 0; q < LP_SLOTS; ++q) {
             const uint32_t j = sp.T + q * 64u + lane;
-            const bool rnd = j >= sp.j0 && j < sp.j1 && (b[q] & DIR_MASK) == DIR_RANDOM;
-            uint32_t ord = 0;
-            if (a.outbox) {
-                const unsigned long long rb = __ballot(rnd);
-                ord = orun + lane_below(rb);
-                orun += (uint32_t)__popcll(rb);
-            }
-            const bool used = rnd && x[q] != XDR_NONE;
+            const bool used = j >= sp.j0 && j < sp.j1 && (b[q] & DIR_MASK) == DIR_RANDOM && x[q] != XDR_NONE;
             if (used) {
                 const uint32_t d = x[q] >> 10, rho = x[q] & 1023u;
-                st[u][q] = 0x80000000u | (ord << 15) | (d << 11) | rho;
+                st[u][q] = 0x80000000u | (d << 11) | rho;
                 const uint32_t w = lw[tt][d] + (rho >> 6);
                 atomicOr(&mk[tt][2 * w + ((rho >> 5) & 1u)], 1u << (rho & 31u));
             }
@@ -447,11 +439,9 @@ __global__ __launch_bounds__(LP_THREADS) void k_list_pack(ListPackArgs a) {
         // the used entries' (s, w): buffer loads over the tile's ids, past the end for the
         // others (no memory touched, no load under a branch), four slots in flight.  (A compacted
         // outbox of the random-edge senders' (s, w), written by the round kernel, cut the pack's
-        // reads but cost the round kernel more than it saved: 0.60 -> 0.58 ms for the pack,
-        // 1.94 -> 2.24 ms for the round kernel at W = 8, profiles/r05/rejected/outbox.txt)
-        const bool obx = a.outbox != nullptr;
-        const __amdgpu_buffer_rsrc_t rs = obx ? buf_rsrc(a.outbox + (size_t)(tb + tt) * XTILE, XTILE * 16u)
-                                              : buf_rsrc(a.swn + (sp.j0 - a.base), (sp.j1 - sp.j0) * 16u);
+        // reads but cost the round kernel more than it saved, with non-temporal or plain stores
+        // of the state: profiles/r05/rejected/outbox.txt)
+        const __amdgpu_buffer_rsrc_t rs = buf_rsrc(a.swn + (sp.j0 - a.base), (sp.j1 - sp.j0) * 16u);
 #pragma unroll
         for (int q0 = 0; q0 < LP_SLOTS; q0 += 4) {
             double2 v[4];
@@ -461,8 +451,8 @@ __global__ __launch_bounds__(LP_THREADS) void k_list_pack(ListPackArgs a) {
                 const int q = q0 + h;
                 const uint32_t j = sp.T + q * 64u + lane;
                 const uint32_t e = st[u][q];
-                const uint32_t o = obx ? ((e >> 15) & 1023u) * 16u : (j - sp.j0) * 16u;
-                const auto w4 = __builtin_amdgcn_raw_buffer_load_b128(rs, (e & 0x80000000u) ? o : BUF_NONE, 0, 0);
+                const auto w4 =
+                    __builtin_amdgcn_raw_buffer_load_b128(rs, (e & 0x80000000u) ? (j - sp.j0) * 16u : BUF_NONE, 0, 0);
                 v[h] = __builtin_bit_cast(double2, w4);
             }
             xchg_prio<0>();

@@ -101,7 +101,6 @@ struct ListPackArgs {
     const uint8_t* nbn;        // node bytes of the round being prepared (local array, id - base)
     const double2* swn;        // (s, w) of that round (local array, id - base)
     const uint16_t* xdr;       // [id - lo]: d << 10 | the sender's rank in its tile's list for d (static), or XDR_NONE
-    const double2* outbox;     // experiments: [tile * XTILE + rank] the round kernel's random-edge senders' (s, w)
     const uint8_t* lwt;        // [tile * (W + 1) + d]: first LDS word of d's segment in the tile (static)
     const uint32_t* gw;        // [tile * W + d]: first header word of the tile's segment in chunk (region, d)
     uint32_t lo, nloc, base;

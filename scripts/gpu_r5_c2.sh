@@ -12,3 +12,6 @@ c2() {
   echo "c2 $l: $(grep -o '[0-9.]* ms/round kernel' $O/c2_$l.log | head -1) $(grep -o 'no events: wall [0-9.]* ms/round' $O/c2_$l.log | head -1)"
 }
 c2 block GP_X=0 && c2 ablation GOSSIP_HIP_LIB_EXPERIMENT=build/ablate/lib_bkabl.so GP_KERNEL=block && c2 tile GP_EXP=1 GP_KERNEL=tile && c2 block2 GP_X=0 || exit 1
+# C2 to convergence on the product's kernel (the LDS-resident one): rounds and wall time
+timeout -k 10 300 python3 tools/converge.py 1000000 3D push-sum 1 $O/c2_converge.json > $O/c2_converge.log 2>&1 || { tail -5 $O/c2_converge.log; exit 1; }
+tail -2 $O/c2_converge.log

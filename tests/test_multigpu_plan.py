@@ -62,14 +62,21 @@ def cap_of(mu):
 
 
 def imp3d_rank_bytes(nloc, halo, nedges, W, caps_out, caps_in, P):
-    """Device bytes of one Imp3D push-sum rank (alloc_slab + build_imp3d +
-    setup_exchange), and the peak with build_imp3d's global temporaries."""
+    """Device bytes of one Imp3D push-sum rank (alloc_slab + build_imp3d + build_lists +
+    setup_exchange), and the peak with build_imp3d's global temporaries.  Since round 5 the
+    random-edge exchange is sender-ordered lists: per in-edge the list key rk (no slot, tag
+    or message arrays), per sender its static list rank xdr (2 B), and per pair and region
+    one 16-B header word per 64 list entries (about half a word of padding per tile) plus
+    the message slots, on both sides."""
     next_ = nloc + 2 * halo + 1024
     node = next_ * (2 * 16 + 2) + nloc * 4 + (nloc + 5) * 4 + 2 * (nloc // 64 + 64) * 8  # sw, nb, rnd, in_off, rbits
-    edges = (nedges + 4) * 4 * 2 + nedges * (4 + 4 + 16)                                # in_src, in_srcd, pos, rtag, rmsg
-    xbuf = sum(16 + 4 * c + 16 * c for c in caps_out) + sum(16 + 4 * c + 16 * c for c in caps_in)
+    node += nloc * (1 + 2)                                                               # xdst, xdr
+    edges = (nedges + 4) * 4 * 3                                                         # in_src, in_srcd, rk
+    tiles = nloc // 1024 + 2
+    hdr = 2 * 16 * (nedges / 64 + tiles * W / 2)                                         # header words, out and in
+    xbuf = hdr + sum(16 * c for c in caps_out) + sum(16 * c for c in caps_in)
     steady = node + edges + xbuf
-    temporaries = P * 4 * 7 + 64e6  # rnd_all, iota, keys, src_sorted, counts, off_all, inv + sort scratch
+    temporaries = P * 4 * 7 + 64e6  # rnd_all, iota (then the list keys), keys, src_sorted, counts, off_all, inv + sort scratch
     return steady, steady + temporaries
 
 
@@ -164,9 +171,12 @@ def test_realised_imp3d_counts_stay_below_capacity_world8():
     src_rank = np.searchsorted(np.array(bounds[1:-1]), ids, side="right")
     dst_rank = np.searchsorted(np.array(bounds[1:-1]), rnd, side="right")
     inv_deg = 1.0 / geo.degree(ids)
-    # push-sum exchange region of every sender: the half of its slab it lies in (setup_exchange)
+    # push-sum exchange region of every sender (setup_exchange / build_lists): its tile's half of
+    # the slab's 1024-id tiles (tiles on global multiples of 1024)
     b_arr = np.array(bounds)
-    half = ((ids - b_arr[src_rank]) >= (b_arr[src_rank + 1] - b_arr[src_rank]) // 2).astype(np.int64)
+    lo_t = b_arr[src_rank] // 1024
+    nt = (b_arr[src_rank + 1] + 1023) // 1024 - lo_t
+    half = ((ids // 1024 - lo_t) >= nt // 2).astype(np.int64)
     mu = np.zeros((2, W, W))
     np.add.at(mu, (half, src_rank, dst_rank), inv_deg)
     cap = np.vectorize(lambda m: min(cap_of(m), 10**9))(mu)
