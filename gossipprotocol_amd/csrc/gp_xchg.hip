@@ -326,7 +326,10 @@ __global__ __launch_bounds__(256) void k_list_key(ListKeyArgs a) {
 // returning atomics on each of a C5 slab's 14 counters per round: 0.73 ms per region),
 // the header words and the messages in list order.  Two barriers per block.
 constexpr int LIST_LW = XTILE / 64 + XMAXW;  // LDS words of one tile's segments (<= 16 full + 1 partial each)
-constexpr int LP_TILES = 8;                  // = waves per block
+#ifndef GP_LP_TILES
+#define GP_LP_TILES 8  // experiments: tiles per block (16: 0.52 -> 0.59 ms per C5 slab at W = 8, profiles/r05/rejected/pack_shapes.txt)
+#endif
+constexpr int LP_TILES = GP_LP_TILES;        // tiles per block, one per wave
 constexpr int LP_WT = 1;                     // tiles per wave
 constexpr int LP_THREADS = 64 * LP_TILES / LP_WT;
 constexpr int LP_SLOTS = XTILE / 64;         // 64-id slots per tile
