@@ -9,9 +9,10 @@
 //   * the lattice is cut into NB = nbx * nby * nbz boxes (at most one per CU), one
 //     1024-thread workgroup each; a box's node bytes and (s, w) live in LDS;
 //   * per round a box writes its six boundary layers (node byte + (s, w)) to a
-//     face buffer in global memory, the grid meets at a barrier (release / acquire
-//     at agent scope), and every box reads its neighbours' facing layers into LDS
-//     halo arrays -- the only global traffic of a round (~28 KB per box at C2);
+//     face buffer in global memory with device-coherent stores, the grid meets at a
+//     barrier (grid_sync), and every box reads its neighbours' facing layers into
+//     LDS halo arrays with device-coherent loads -- the only global traffic of a
+//     round (~28 KB per box at C2);
 //   * each node then folds exactly as the tile kernel (gp_round.hip) does: own half,
 //     lattice messages in the receiver's slot order (Program.fs:246-257), the ratio
 //     test of Program.fs:114-123 (SRS v1 B.4), the next direction by Philox -- with
