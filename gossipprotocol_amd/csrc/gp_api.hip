@@ -1399,7 +1399,8 @@ void choose_kernel(gp_sim* s, int64_t nloc_max, int& kernel, uint32_t& col_xsegs
     // launch per batch, the state resident in LDS (gp_block.hip)
     BlockPlan bp{};
     const bool block_ok = cfg->topology == GP_3D && push && s->world == 1 && g >= 2 &&
-                          block_plan((uint32_t)g, prop.multiProcessorCount, bp);
+                          block_plan((uint32_t)g, prop.multiProcessorCount, bp) &&
+                          block_plan_resident(bp, prop.multiProcessorCount);
     if (block_ok) kernel = KERNEL_BLOCK;
 #ifdef GP_EXPERIMENTS
     if (const char* e = std::getenv("GP_KERNEL")) {
@@ -1797,8 +1798,14 @@ int64_t gp_step(gp_sim* s, int64_t nrounds, int64_t* alerts_out) {
         if (block) {  // the whole batch in one cooperative launch (gp_block.hip)
             const DevState& S = s->slab[0].S;
             if (s->timing) HIP_TRY(hipEventRecord(s->ev[0], s->stream));
-            HIP_TRY(launch_round_block(S, S.bplan, (uint32_t)s->rounds_done, (uint32_t)batch, S.bface, S.bscratch,
-                                       s->stream));
+            const hipError_t le = launch_round_block(S, S.bplan, (uint32_t)s->rounds_done, (uint32_t)batch, S.bface,
+                                                     S.bscratch, s->stream);
+            if (le != hipSuccess) {
+                set_err("the LDS-resident round kernel's cooperative launch failed: %s (its %u workgroups must be "
+                        "resident on the device at once)",
+                        hipGetErrorString(le), S.bplan.nbx * S.bplan.nby * S.bplan.nbz);
+                return GP_EHIP;
+            }
             if (s->timing) HIP_TRY(hipEventRecord(s->ev[1], s->stream));
             unsigned int flags[2] = {0, 0};
             HIP_TRY(hipMemcpyAsync(flags, S.bscratch, sizeof flags, hipMemcpyDeviceToHost, s->stream));

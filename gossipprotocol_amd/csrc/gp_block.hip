@@ -431,4 +431,15 @@ hipError_t block_kernel_setup(const BlockPlan& p) {
                                (int)p.lds);
 }
 
+// Whether the plan's boxes can all be resident at once on `cus` CUs (the cooperative launch's
+// condition), from the runtime's occupancy for this LDS size; false also if the query fails.
+bool block_plan_resident(const BlockPlan& p, int cus) {
+    if (block_kernel_setup(p) != hipSuccess) return false;
+    int per = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&k_ps_block), BK_THREADS,
+                                                     p.lds) != hipSuccess)
+        return false;
+    return (uint64_t)p.nbx * p.nby * p.nbz <= (uint64_t)per * (uint64_t)cus;
+}
+
 }  // namespace gp

@@ -270,6 +270,7 @@ enum KernelVariant : int { KERNEL_TILE = 1, KERNEL_COL = 2, KERNEL_BLOCK = 3 };
 bool block_plan(uint32_t g, int cus, BlockPlan& p);
 size_t block_face_bytes(const BlockPlan& p);
 hipError_t block_kernel_setup(const BlockPlan& p);
+bool block_plan_resident(const BlockPlan& p, int cus);
 // rounds [r0, r0 + nrounds) (fewer once the cumulative alerts reach T); scratch:
 // BLOCK_SCRATCH_BYTES, word 1 is set if a grid barrier timed out
 constexpr size_t BLOCK_SCRATCH_BYTES = 4 * 16 * 9;
