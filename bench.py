@@ -11,8 +11,11 @@ every node is active (steady state: every node sends a message each round),
 then W warmup rounds; convergence is never reached inside the timed window.
 
 One JSON line on stdout (rank 0).  `roofline` is measured live: HIP events on
-the library's stream bracket every round kernel; its
-algorithmic bytes per node-round are DESIGN.md §4's figure.  `traffic` is
+the library's stream bracket every round kernel; `achieved` counts SURVEY.md
+§8(d)'s algorithmic bytes per node-round (B_ps = 34 + 4 [Imp3D] + 32 a + 8 a_x:
+71.1 B at C5's steady state, survey_bytes_per_node), and `design_*` the fewer
+bytes this design must move (no message is staged
+through HBM).  `traffic` is
 measured in the same run: before the bench, the workload is re-run as a child
 under three rocprofv3 --pmc passes and the round kernel's HBM bytes are read
 from the L2's request-size counters (tools/hbm_traffic.py).  `cpu_baseline` times the SRS v1 C oracle on the host cores over a
@@ -42,6 +45,27 @@ HBM_PEAK_GBPS = 8000.0  # MI355X spec (MI355X_MICROARCH.md, chip-level parameter
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def survey_bytes_per_node(topology, algorithm, g):
+    """SURVEY.md §8(d)'s algorithmic bytes per node-round in steady state (every node
+    active, a = 1): push-sum B_ps = 34 + 4 [Imp3D] + 32 a + 8 a_x, a_x the fraction of
+    messages on a random (Imp3D) or full-topology link.  Imp3D: a node with d lattice
+    neighbours picks its random link with probability 1 / (d + 1) (Program.fs:125-128);
+    along each axis a node has 2 neighbours, or 1 on the lattice's two end planes, so
+    a_x = sum_k C(3, k) (2/g)^k ((g-2)/g)^(3-k) / (7 - k) (1/7 in the interior)."""
+    if algorithm != "push-sum":
+        return None
+    imp = topology == "Imp3D"
+    if topology == "full":
+        ax = 1.0
+    elif imp:
+        from math import comb
+        pe = 2.0 / g if g > 2 else 1.0
+        ax = sum(comb(3, k) * pe ** k * (1.0 - pe) ** (3 - k) / (7 - k) for k in range(4))
+    else:
+        ax = 0.0
+    return 34.0 + (4.0 if imp else 0.0) + 32.0 + 8.0 * ax
 
 
 def preroll(sim, population, cap=2000):
@@ -263,13 +287,16 @@ def main():
         raise RuntimeError(f"only {len(got)} of {args.steps} timed rounds ran (converged inside the window)")
     elapsed = max_over_ranks(elapsed)
     kms, launches, kname = sim.kernel_stats()
-    bytes_per_node = sim.alg_bytes_per_node()
+    design_bytes = sim.alg_bytes_per_node()
+    g_edge = round(P ** (1.0 / 3.0)) if args.topology in ("3D", "Imp3D") else 0
     local_nodes = sim.local_population
     sim.close()
 
     value = P * args.steps / elapsed
     avg_ms = kms / max(1, launches)
+    bytes_per_node = survey_bytes_per_node(args.topology, args.algorithm, g_edge) or design_bytes
     achieved = bytes_per_node * local_nodes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    design_achieved = design_bytes * local_nodes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     out = {
         "metric": METRIC,
         "value": value,
@@ -301,6 +328,10 @@ def main():
             "frac": achieved / HBM_PEAK_GBPS,
             "traffic": traffic["total_bytes"] if traffic else None,
             "alg_bytes_per_node_round": bytes_per_node,
+            "alg_bytes_source": "SURVEY.md §8(d) B_ps (steady state)",
+            "design_bytes_per_node_round": design_bytes,
+            "design_achieved": design_achieved,
+            "design_frac": design_achieved / HBM_PEAK_GBPS,
             "kernel_avg_ms": avg_ms,
         },
         "cpu_baseline": None,
@@ -312,6 +343,7 @@ def main():
                       "3 passes over the same workload, last %d round kernels (tools/hbm_traffic.py)" % traffic["dispatches"],
             "read_bytes": traffic["read_bytes"], "write_bytes": traffic["write_bytes"],
             "traffic_over_algorithmic": traffic["total_bytes"] / alg,
+            "traffic_over_design_bytes": traffic["total_bytes"] / (design_bytes * local_nodes),
             "traffic_gbps": traffic["total_bytes"] / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else None,
             "fetch_size_equivalent_bytes": traffic["fetch_size_equivalent_bytes"],
         }

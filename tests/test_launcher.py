@@ -128,3 +128,17 @@ def test_python_cli_world_mismatch_refused():
                        cwd=ROOT, capture_output=True, text=True, timeout=120,
                        env=dict(os.environ, WORLD_SIZE="4", RANK="0"))
     assert r.returncode == 2 and "WORLD_SIZE" in r.stderr
+
+
+def test_bench_roofline_bytes_follow_survey():
+    """bench.py's roofline counts SURVEY.md §8(d)'s algorithmic bytes per node-round:
+    B_ps = 34 + 4 [Imp3D] + 32 a + 8 a_x in steady state -- C5 ~71, C2 66, C4 74 B."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    c5 = bench.survey_bytes_per_node("Imp3D", "push-sum", 1000)
+    assert abs(c5 - (34 + 4 + 32 + 8 / 7)) < 2e-3  # 1/7 random-link sends, end planes barely move it
+    assert bench.survey_bytes_per_node("3D", "push-sum", 100) == 66.0
+    assert bench.survey_bytes_per_node("full", "push-sum", 0) == 74.0
+    assert bench.survey_bytes_per_node("Imp3D", "gossip", 465) is None
+    # a lattice of edge 2: every node is on an end plane of all three axes (3 neighbours, 1/4)
+    assert abs(bench.survey_bytes_per_node("Imp3D", "push-sum", 2) - (70 + 8 / 4)) < 1e-12
