@@ -30,6 +30,11 @@ CASES = [  # (num_nodes, topology, algorithm, seed, rounds, checkpoint, ranks)
     (64000, "Imp3D", "push-sum", 6, 200, 50, 3),
     (125000, "Imp3D", "gossip", 7, 300, 101, 4),
     (27000, "Imp3D", "gossip", 3, 2000, 400, 2),
+    # slabs of one or two planes (400 / 800 nodes): a slab's ids span one or two 1024-id list
+    # tiles, so an exchange region may hold no tile at all
+    (8000, "Imp3D", "push-sum", 4, 300, 100, 16),
+    (8000, "Imp3D", "gossip", 5, 600, 200, 16),
+    (27000, "Imp3D", "push-sum", 12, 300, 100, 5),
     (216000, "3D", "push-sum", 9, 200, 75, 2),
     (27000, "3D", "gossip", 4, 2000, 500, 3),
     (5000, "line", "gossip", 6, 8000, 2000, 2),
