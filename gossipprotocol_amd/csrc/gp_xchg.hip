@@ -325,6 +325,15 @@ __global__ __launch_bounds__(256) void k_list_key(ListKeyArgs a) {
 // at once, ONE reservation per destination (a reservation per tile queued ~60 k
 // returning atomics on each of a C5 slab's 14 counters per round: 0.73 ms per region),
 // the header words and the messages in list order.  Two barriers per block.
+#ifndef GP_LP_STAMPS
+#define GP_LP_STAMPS 0  // experiments, diagnostics: per-phase cycle sums of k_list_pack (gp_debug_lp_stamps)
+#endif
+#if GP_LP_STAMPS
+__device__ unsigned long long gp_lp_stamp_acc[8];
+#define LP_STAMP(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#else
+#define LP_STAMP(v)
+#endif
 constexpr int LIST_LW = XTILE / 64 + XMAXW;  // LDS words of one tile's segments (<= 16 full + 1 partial each)
 #ifndef GP_LP_TILES
 #define GP_LP_TILES 8  // experiments: tiles per block (16: 0.52 -> 0.59 ms per C5 slab at W = 8, profiles/r05/rejected/pack_shapes.txt)
@@ -341,6 +350,7 @@ __global__ __launch_bounds__(LP_THREADS) void k_list_pack(ListPackArgs a) {
     __shared__ uint32_t off[XMAXW];                 // the block's reserved run in each destination's chunk
     __shared__ double2* ovals[XMAXW];
     __shared__ uint32_t ocap[XMAXW];
+    LP_STAMP(t0);
     const uint32_t tb = a.t0 + blockIdx.x * LP_TILES;
     if (tb >= a.t1) return;
     const int ntl = (int)min((uint32_t)LP_TILES, a.t1 - tb);
@@ -357,6 +367,7 @@ __global__ __launch_bounds__(LP_THREADS) void k_list_pack(ListPackArgs a) {
         if ((int)tt < ntl) lw[tt][d] = a.lwt[(size_t)(tb + tt) * (W + 1) + d];
     }
     __syncthreads();
+    LP_STAMP(t1);
     // per tile of this wave and slot: used ? 1 << 31 | d << 11 | rho : 0 (rho < 1024)
     uint32_t st[LP_WT][LP_SLOTS];
 #pragma unroll
@@ -410,7 +421,9 @@ __global__ __launch_bounds__(LP_THREADS) void k_list_pack(ListPackArgs a) {
         const uint32_t a0 = __shfl(incl, (int)(e0 > 0 ? e0 - 1 : 0), 64);
         if (l < (uint32_t)W) tn[tt][l] = e1 > e0 ? a1 - (e0 > 0 ? a0 : 0u) : 0u;
     }
+    LP_STAMP(t2);
     __syncthreads();
+    LP_STAMP(t3);
     if (threadIdx.x < (uint32_t)W) {  // the block's run per destination: one reservation
         const uint32_t d = threadIdx.x;
         uint32_t r = 0;
@@ -422,6 +435,7 @@ __global__ __launch_bounds__(LP_THREADS) void k_list_pack(ListPackArgs a) {
         off[d] = d != me && r ? atomicAdd(a.peer[d].cnt, r) : 0u;
     }
     __syncthreads();
+    LP_STAMP(t4);
 #pragma unroll
     for (int u = 0; u < LP_WT; ++u) {
         const int tt = (int)wv * LP_WT + u;
@@ -439,6 +453,12 @@ __global__ __launch_bounds__(LP_THREADS) void k_list_pack(ListPackArgs a) {
                 a.peer[seg].hdr[a.gw[(size_t)(tb + tt) * W + seg] + (l - lw[tt][seg])] = h;
             }
         }
+#if GP_LP_STAMPS
+        if (u == 0) {
+            LP_STAMP(t5);
+            if (threadIdx.x == 0) atomicAdd(&gp_lp_stamp_acc[4], (unsigned long long)(t5 - t4));
+        }
+#endif
         // the used entries' (s, w): buffer loads over the tile's ids, past the end for the
         // others (no memory touched, no load under a branch), four slots in flight.  (A compacted
         // outbox of the random-edge senders' (s, w), written by the round kernel, cut the pack's
@@ -473,6 +493,17 @@ __global__ __launch_bounds__(LP_THREADS) void k_list_pack(ListPackArgs a) {
             }
         }
     }
+#if GP_LP_STAMPS
+    LP_STAMP(t6);
+    if (threadIdx.x == 0) {
+        atomicAdd(&gp_lp_stamp_acc[0], (unsigned long long)(t1 - t0));  // LDS init, tile layouts
+        atomicAdd(&gp_lp_stamp_acc[1], (unsigned long long)(t2 - t1));  // wave 0's tile: loads, bitmap, scans
+        atomicAdd(&gp_lp_stamp_acc[2], (unsigned long long)(t3 - t2));  // waiting for the block's other tiles
+        atomicAdd(&gp_lp_stamp_acc[3], (unsigned long long)(t4 - t3));  // reservations
+        atomicAdd(&gp_lp_stamp_acc[5], (unsigned long long)(t6 - t4));  // headers + payloads (wave 0)
+        atomicAdd(&gp_lp_stamp_acc[6], 1ull);
+    }
+#endif
 }
 
 __global__ __launch_bounds__(256) void k_gather_keys(const uint32_t* __restrict__ key, const uint32_t* __restrict__ src,
@@ -677,3 +708,22 @@ hipError_t launch_expect(const ExpectArgs& a, int grid, hipStream_t st) {
 }
 
 }  // namespace gp
+
+#if GP_LP_STAMPS
+// Experiments build, diagnostics: mean cycles (s_memtime) per k_list_pack block of its phases
+// since the last reset: LDS init, wave 0's tile (loads, bitmap, scans), the wait for the
+// block's other tiles, the reservations, wave 0's header words, wave 0's headers + payloads;
+// out[6] = blocks counted.
+extern "C" int gp_debug_lp_stamps(double* out, int reset) {
+    unsigned long long h[8] = {0};
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(gp::gp_lp_stamp_acc), sizeof(h)) != hipSuccess) return -3;
+    const double n = h[6] ? (double)h[6] : 1.0;
+    for (int q = 0; q < 6; ++q) out[q] = (double)h[q] / n;
+    out[6] = (double)h[6];
+    if (reset) {
+        unsigned long long z[8] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(gp::gp_lp_stamp_acc), z, sizeof(z)) != hipSuccess) return -3;
+    }
+    return 0;
+}
+#endif
