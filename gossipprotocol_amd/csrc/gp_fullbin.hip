@@ -585,6 +585,15 @@ constexpr int FBF_THREADS = GP_FBF_THREADS;
 // (reusing the fold's arrays), one reservation per (tile, bin), coalesced runs.
 // The next round then starts at B: no send pass re-reads the state (18 B/node).
 constexpr uint32_t FBF_MAXB1 = 1024;  // coarse bins the fused send can bin into (LDS reservation slots)
+#ifndef GP_FB_STAMPS
+#define GP_FB_STAMPS 0  // experiments, diagnostics: per-phase cycle sums of the fused fold (gp_debug_fb_stamps)
+#endif
+#if GP_FB_STAMPS
+__device__ unsigned long long gp_fb_stamp_acc[8];
+#define FB_STAMP(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#else
+#define FB_STAMP(v)
+#endif
 #ifndef GP_FB_PF
 #define GP_FB_PF 1  // fused fold: the next tile's messages loaded during this tile's send phase
 #endif
@@ -627,12 +636,16 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
             pw[k] = m.y;
         }
     };
+#if GP_FB_STAMPS
+    uint64_t ph[6] = {0, 0, 0, 0, 0, 0};
+#endif
     uint32_t n_pf = 0;
     if (GP_FB_PF && SEND && blockIdx.x < a.nb2) {
         n_pf = min(ld_agent(&a.cnt2[blockIdx.x]), (uint32_t)a.cap2);
         load_msgs(blockIdx.x, n_pf);
     }
     for (uint32_t f = blockIdx.x; f < a.nb2; f += gridDim.x) {
+        FB_STAMP(t0);
         const bool pf = GP_FB_PF && SEND;
         const uint32_t n = pf ? n_pf : min(ld_agent(&a.cnt2[f]), (uint32_t)a.cap2);
         // the next tile's message count, early (a scalar load; its messages are loaded later)
@@ -676,6 +689,7 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
             rk[k] = q < n ? atomicAdd(&cnt[vr[k]], 1u) : 0u;
         }
         lds_barrier();
+        FB_STAMP(t1);
         lds_excl_scan<FBF_THREADS, true>(cnt, TILE, tmp);
         if (threadIdx.x == 0) cnt[TILE] = n;
 #pragma unroll
@@ -688,6 +702,7 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
             }
         }
         lds_barrier();
+        FB_STAMP(t2);
 #pragma unroll
         for (int k = 0; k < NPT; ++k) {
             const uint32_t v = k * FBF_THREADS + threadIdx.x;
@@ -742,6 +757,10 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
         lds_barrier();
         for (uint32_t v = threadIdx.x; v < TILE; v += FBF_THREADS) cnt[v] = 0u;
         lds_barrier();
+        FB_STAMP(t3);
+#if GP_FB_STAMPS
+        uint64_t t4 = t3;
+#endif
         if (SEND) {
             // round r+1: coarse bin of every active node's target (drawn above), LDS rank per bin
             uint32_t node[NPT], key[NPT], rank[NPT];
@@ -784,6 +803,9 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
             }
             if (q0 < a.nb1) sbase[q0] = res;
             lds_barrier();
+#if GP_FB_STAMPS
+            t4 = __builtin_amdgcn_s_memtime();
+#endif
             // write-out in bin order: consecutive threads, consecutive slots of one run
             fb_prio<2>();
 #pragma unroll
@@ -805,7 +827,20 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
             for (uint32_t v = threadIdx.x; v < a.nb1; v += FBF_THREADS) cnt[v] = 0u;
             lds_barrier();
         }
+#if GP_FB_STAMPS
+        FB_STAMP(t5);
+        ph[0] += t1 - t0;  // message count + state loads issued, Philox, LDS receiver counts
+        ph[1] += t2 - t1;  // scan, messages into LDS in receiver order
+        ph[2] += t3 - t2;  // per receiver: sort, fold, ratio test, state out
+        ph[3] += t4 - t3;  // send: LDS bin counts, scan, reservations, next tile's loads issued, LDS scatter
+        ph[4] += t5 - t4;  // send: write-out
+        ph[5] += 1;
+#endif
     }
+#if GP_FB_STAMPS
+    if (threadIdx.x == 0)
+        for (int q = 0; q < 6; ++q) atomicAdd(&gp_fb_stamp_acc[q], (unsigned long long)ph[q]);
+#endif
     uint32_t x = alerts, y = newly;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -829,6 +864,24 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
 }
 
 // ---------------------------------------------------------------- host side
+#if GP_FB_STAMPS
+}  // namespace gp
+// Experiments build, diagnostics: mean cycles (s_memtime) per tile of the fused fold's phases
+// since the last reset (see k_fb_fold); out[5] = tiles counted.
+extern "C" int gp_debug_fb_stamps(double* out, int reset) {
+    unsigned long long h[8] = {0};
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(gp::gp_fb_stamp_acc), sizeof(h)) != hipSuccess) return -3;
+    const double n = h[5] ? (double)h[5] : 1.0;
+    for (int q = 0; q < 5; ++q) out[q] = (double)h[q] / n;
+    out[5] = (double)h[5];
+    if (reset) {
+        unsigned long long z[8] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(gp::gp_fb_stamp_acc), z, sizeof(z)) != hipSuccess) return -3;
+    }
+    return 0;
+}
+namespace gp {
+#endif
 // Bins for the nrecv receivers of a rank (one rank: nrecv = P).
 FullBinPlan full_bin_plan(uint32_t P, bool fused) {
     FullBinPlan p{};
