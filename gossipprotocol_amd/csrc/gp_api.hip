@@ -111,6 +111,10 @@ struct Slab {
     uint32_t* tgt = nullptr;           // local target of every receive-bitmap bit
     uint32_t nbits_out = 0, nbits_in = 0;  // bitmap sizes (multiples of BITS_ALIGN)
     std::vector<uint32_t> bo, bn, ro, rn;  // [peer]: chunk bit offset / bits, send and receive side
+    // push-sum halo planes (3D / Imp3D, W > 1): the senders' (s, w) toward each neighbour, compacted
+    // ([0]: lower neighbour, [1]: upper; k_halo_pack / k_halo_expand, gp_xchg.hpp)
+    double2* hsend[2] = {nullptr, nullptr};
+    double2* hrecv[2] = {nullptr, nullptr};
 };
 
 constexpr uint32_t BITS_ALIGN = 1024;  // bitmap chunks start on 128-byte boundaries
@@ -159,6 +163,7 @@ struct gp_sim {
     // exchange buffers per rank pair: xhalves regions (2: full-topology push-sum, whose exchange runs
     // in two halves of each rank's senders on xstream, overlapped with the send / coarse passes)
     int xhalves = 1;
+    size_t halo_slots = 0;  // push-sum halo planes travel compacted (setup_halo): slots per buffer, else 0
     // Imp3D push-sum lists: header words of chunk (h, a -> b) at [(a * xhalves + h) * world + b],
     // every slab's (each rank computes the whole table from the global random edges)
     std::vector<uint32_t> list_nw;
@@ -373,6 +378,55 @@ int alloc_slab(gp_sim* s, Slab& sl, int r) {
         S.rbits_words = rbits_words_for(S.lo, S.nloc);
         if ((rc = dev_alloc_t(s, &S.rbits[0], S.rbits_words)) || (rc = dev_alloc_t(s, &S.rbits[1], S.rbits_words)))
             return rc;
+    }
+    return GP_OK;
+}
+
+// Push-sum on a 3D / Imp3D lattice over several ranks: the halo planes' (s, w) travel compacted
+// (only the senders toward the neighbour, HaloArgs in gp_xchg.hpp): C5 at W = 8, 16 MB -> 3.9 MB
+// per direction and round.  (GP_HALO_FULL=1, experiments: the whole plane, as before round 5.)
+int setup_halo(gp_sim* s) {
+    s->halo_slots = 0;
+    const bool lattice = s->cfg.topology == GP_3D || s->cfg.topology == GP_IMP3D;
+    if (!lattice || s->cfg.algorithm != GP_PUSHSUM || s->world < 2 || s->halo < HALO_CHUNK) return GP_OK;
+#ifdef GP_EXPERIMENTS
+    if (const char* e = std::getenv("GP_HALO_FULL"))
+        if (e[0] == '1') return GP_OK;
+#endif
+    s->halo_slots = halo_buf_slots(s->halo);
+    int rc;
+    for (Slab& sl : s->slab) {
+        for (int k = 0; k < 2; ++k) {
+            const bool has = k == 0 ? sl.rank > 0 : sl.rank < s->world - 1;
+            if (!has) continue;
+            if ((rc = dev_alloc_t(s, &sl.hsend[k], s->halo_slots)) || (rc = dev_alloc_t(s, &sl.hrecv[k], s->halo_slots)))
+                return rc;
+        }
+    }
+    return GP_OK;
+}
+
+// The halo planes' compacted (s, w) of buffers b: pack (the slab's first / last plane, before the
+// transfer) or expand (into the halo planes, after it).  Lower side: the first plane's senders
+// toward x - 1 (direction 0) go down; the lower halo takes the neighbour's senders toward x + 1
+// (direction 1).  The upper side the other way round.
+int halo_pack_expand(gp_sim* s, int b, bool pack) {
+    const uint32_t H = s->halo;
+    for (Slab& sl : s->slab) {
+        DevState& S = sl.S;
+        for (int k = 0; k < 2; ++k) {
+            if (!sl.hsend[k]) continue;
+            // plane start: pack -- lo (k = 0) / hi - H; expand -- lo - H (k = 0) / hi
+            const uint32_t at = pack ? (k == 0 ? S.lo : sl.hi - H) : (k == 0 ? S.lo - H : sl.hi);
+            HaloArgs h{};
+            h.nb = S.nb[b] + (at - S.base);
+            h.sw = S.sw[b] + (at - S.base);
+            h.buf = pack ? sl.hsend[k] : sl.hrecv[k];
+            h.n = H;
+            h.dir = pack ? (k == 0 ? 0u : 1u) : (k == 0 ? 1u : 0u);
+            h.overflow = sl.overflow ? sl.overflow : &S.ctl->overflow;
+            HIP_TRY(pack ? launch_halo_pack(h, s->stream) : launch_halo_expand(h, s->stream));
+        }
     }
     return GP_OK;
 }
@@ -1110,6 +1164,9 @@ int exchange(gp_sim* s, uint32_t rn) {
     const int NH = imp ? s->xhalves : 1;
     hipStream_t xs = NH > 1 && s->xstream ? s->xstream : s->stream;
     const size_t H = s->halo;
+    const size_t HS = s->halo_slots;  // push-sum: the halo planes' (s, w) compacted (setup_halo)
+    int rc;
+    if (push && HS && (rc = halo_pack_expand(s, b, true))) return rc;
     if (s->mode == MODE_VIRTUAL) {  // halo planes by device copies (round kernel -> next round kernel)
         for (int r = 0; r + 1 < W; ++r) {
             DevState& A = s->slab[r].S;  // lower slab
@@ -1120,7 +1177,12 @@ int exchange(gp_sim* s, uint32_t rn) {
                                    hipMemcpyDeviceToDevice, s->stream));
             HIP_TRY(hipMemcpyAsync(A.nb[b] + (edge - A.base), B.nb[b] + (edge - B.base), H, hipMemcpyDeviceToDevice,
                                    s->stream));
-            if (push) {
+            if (push && HS) {
+                HIP_TRY(hipMemcpyAsync(s->slab[r + 1].hrecv[0], s->slab[r].hsend[1], HS * 16, hipMemcpyDeviceToDevice,
+                                       s->stream));
+                HIP_TRY(hipMemcpyAsync(s->slab[r].hrecv[1], s->slab[r + 1].hsend[0], HS * 16, hipMemcpyDeviceToDevice,
+                                       s->stream));
+            } else if (push) {
                 HIP_TRY(hipMemcpyAsync(B.sw[b] + (edge - H - B.base), A.sw[b] + (edge - H - A.base), H * 16,
                                        hipMemcpyDeviceToDevice, s->stream));
                 HIP_TRY(hipMemcpyAsync(A.sw[b] + (edge - A.base), B.sw[b] + (edge - B.base), H * 16,
@@ -1215,7 +1277,7 @@ int exchange(gp_sim* s, uint32_t rn) {
                                                    hipMemcpyDeviceToDevice, xs));
                     }
             } else if (imp) {
-                int rc = transfer_xbufs(s, h, xs);
+                rc = transfer_xbufs(s, h, xs);
                 if (rc) return rc;
             }
         } else {
@@ -1226,7 +1288,10 @@ int exchange(gp_sim* s, uint32_t rn) {
             if (h == 0 && r > 0) {  // my first H ids <-> lower neighbour's last H ids
                 NCCL_TRY(ncclSend(S.nb[b] + (S.lo - S.base), H, ncclUint8, r - 1, s->comm, xs));
                 NCCL_TRY(ncclRecv(S.nb[b] + (S.lo - H - S.base), H, ncclUint8, r - 1, s->comm, xs));
-                if (push) {
+                if (push && HS) {
+                    NCCL_TRY(ncclSend(sl.hsend[0], HS * 16, ncclUint8, r - 1, s->comm, xs));
+                    NCCL_TRY(ncclRecv(sl.hrecv[0], HS * 16, ncclUint8, r - 1, s->comm, xs));
+                } else if (push) {
                     NCCL_TRY(ncclSend(S.sw[b] + (S.lo - S.base), H * 16, ncclUint8, r - 1, s->comm, xs));
                     NCCL_TRY(ncclRecv(S.sw[b] + (S.lo - H - S.base), H * 16, ncclUint8, r - 1, s->comm, xs));
                 }
@@ -1234,7 +1299,10 @@ int exchange(gp_sim* s, uint32_t rn) {
             if (h == 0 && r < W - 1) {  // my last H ids <-> upper neighbour's first H ids
                 NCCL_TRY(ncclSend(S.nb[b] + (sl.hi - H - S.base), H, ncclUint8, r + 1, s->comm, xs));
                 NCCL_TRY(ncclRecv(S.nb[b] + (sl.hi - S.base), H, ncclUint8, r + 1, s->comm, xs));
-                if (push) {
+                if (push && HS) {
+                    NCCL_TRY(ncclSend(sl.hsend[1], HS * 16, ncclUint8, r + 1, s->comm, xs));
+                    NCCL_TRY(ncclRecv(sl.hrecv[1], HS * 16, ncclUint8, r + 1, s->comm, xs));
+                } else if (push) {
                     NCCL_TRY(ncclSend(S.sw[b] + (sl.hi - H - S.base), H * 16, ncclUint8, r + 1, s->comm, xs));
                     NCCL_TRY(ncclRecv(S.sw[b] + (sl.hi - S.base), H * 16, ncclUint8, r + 1, s->comm, xs));
                 }
@@ -1303,6 +1371,7 @@ int exchange(gp_sim* s, uint32_t rn) {
     } else if (xs != s->stream) {
         HIP_TRY(hipStreamWaitEvent(s->stream, s->ev_xfer[NH - 1], 0));
     }
+    if (push && HS && (rc = halo_pack_expand(s, b, false))) return rc;
     return GP_OK;
 }
 
@@ -1526,6 +1595,7 @@ int build_sim(gp_sim* s) {
     if (s->cfg.topology == GP_IMP3D && (rc = build_imp3d(s))) return rc;
     if ((s->cfg.topology == GP_IMP3D || s->cfg.topology == GP_FULL) && s->world > 1 && (rc = setup_exchange(s)))
         return rc;
+    if ((rc = setup_halo(s))) return rc;
     if (hipHostMalloc((void**)&s->host_ctl, sizeof(Ctl), hipHostMallocDefault) != hipSuccess) {
         set_err("hipHostMalloc failed");
         return GP_ENOMEM;

@@ -506,6 +506,42 @@ __global__ __launch_bounds__(LP_THREADS) void k_list_pack(ListPackArgs a) {
 #endif
 }
 
+// A halo plane's senders toward the neighbour: their (s, w) compacted per 1024-node chunk, in
+// id order (PACK), or put back at their ids in the receiver's halo plane (!PACK) -- both sides
+// rank the same direction bytes the same way, so no counts travel.
+template <bool PACK>
+__global__ __launch_bounds__(256) void k_halo(HaloArgs a) {
+    __shared__ uint32_t wc[HALO_CHUNK / 64];  // senders per 64-node group, in id order
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t c0 = blockIdx.x * HALO_CHUNK;
+    bool m[HALO_CHUNK / 256];
+    uint32_t below[HALO_CHUNK / 256];
+#pragma unroll
+    for (int k = 0; k < (int)(HALO_CHUNK / 256); ++k) {
+        const uint32_t i = c0 + k * 256u + threadIdx.x;
+        m[k] = i < a.n && (a.nb[i] & DIR_MASK) == a.dir;
+        const unsigned long long bal = __ballot(m[k]);
+        below[k] = lane_below(bal);
+        if (lane == 0) wc[k * 4 + wv] = (uint32_t)__popcll(bal);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < (int)(HALO_CHUNK / 256); ++k) {
+        if (!m[k]) continue;
+        uint32_t rank = below[k];
+        for (uint32_t q = 0; q < (uint32_t)k * 4u + wv; ++q) rank += wc[q];
+        const uint32_t i = c0 + k * 256u + threadIdx.x;
+        double2* slot = a.buf + (size_t)blockIdx.x * HALO_CAP + rank;
+        if (rank >= HALO_CAP) {
+            if (PACK) atomicOr(a.overflow, 1u);
+        } else if (PACK) {
+            *slot = a.sw[i];
+        } else {
+            a.sw[i] = *slot;
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void k_gather_keys(const uint32_t* __restrict__ key, const uint32_t* __restrict__ src,
                                                      uint32_t n, uint32_t* __restrict__ out) {
     for (uint32_t e = blockIdx.x * 256 + threadIdx.x; e < n; e += gridDim.x * 256) out[e] = key[src[e]];
@@ -670,6 +706,14 @@ hipError_t launch_list_key(const ListKeyArgs& a, hipStream_t st) {
 hipError_t launch_list_pack(const ListPackArgs& a, hipStream_t st) {
     if (a.t1 > a.t0)
         hipLaunchKernelGGL(k_list_pack, dim3((a.t1 - a.t0 + LP_TILES - 1) / LP_TILES), dim3(LP_THREADS), 0, st, a);
+    return hipGetLastError();
+}
+hipError_t launch_halo_pack(const HaloArgs& a, hipStream_t st) {
+    if (a.n) hipLaunchKernelGGL(k_halo<true>, dim3((a.n + HALO_CHUNK - 1) / HALO_CHUNK), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+hipError_t launch_halo_expand(const HaloArgs& a, hipStream_t st) {
+    if (a.n) hipLaunchKernelGGL(k_halo<false>, dim3((a.n + HALO_CHUNK - 1) / HALO_CHUNK), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 hipError_t launch_gather_keys(const uint32_t* key, const uint32_t* src, uint32_t n, uint32_t* out, int grid,

@@ -164,6 +164,24 @@ struct BitsEndsArgs {         // this rank's encodings
     uint32_t ro[XMAXW];       // bit offset of source a's chunk in the receive bitmap
 };
 
+// Push-sum halo planes over several ranks (3D / Imp3D): a neighbour's round kernel reads the
+// (s, w) of a halo node only when that node sends to it (its direction byte, which travels in
+// full), so only those (s, w) travel -- ~1/7 of the plane, compacted per 1024-node chunk into
+// HALO_CAP slots (mean 146 at 1/7, 171 at 1/6; 256 is > 7 sigma; a fuller chunk sets the
+// overflow flag).  k_halo_pack on the sender, k_halo_expand into the receiver's halo plane.
+constexpr uint32_t HALO_CHUNK = 1024, HALO_CAP = 256;
+struct HaloArgs {
+    const uint8_t* nb;      // direction bytes of the plane's nodes
+    double2* sw;            // the plane's (s, w): read by the pack, written by the expand
+    double2* buf;           // [chunk * HALO_CAP + rank]: the senders' (s, w), in id order per chunk
+    uint32_t n;             // nodes in the plane
+    uint32_t dir;           // the direction whose senders' (s, w) travel
+    unsigned int* overflow;
+};
+inline size_t halo_buf_slots(uint32_t n) { return (size_t)((n + HALO_CHUNK - 1) / HALO_CHUNK) * HALO_CAP; }
+hipError_t launch_halo_pack(const HaloArgs& a, hipStream_t st);
+hipError_t launch_halo_expand(const HaloArgs& a, hipStream_t st);
+
 hipError_t launch_src_flag(const uint32_t* src, uint32_t n, const uint32_t* bounds, int W, int a, uint32_t* flag,
                            int grid, hipStream_t st);
 hipError_t launch_bits_pos(const BitsSetupArgs& a, int grid, hipStream_t st);

@@ -70,10 +70,11 @@ def per_slab_names(groups, short):
     return {short(name) for grp in groups for name, _ in grp}
 
 
-def pair_bytes(n, topo, alg, W, halves=1, lists=True):
+def pair_bytes(n, topo, alg, W, halves=1, lists=True, halo_compact=False):
     """Bytes rank a sends rank b per round (fixed-capacity buffers incl. their 16-B count
     headers; full push-sum: `halves` regions, one per half of a's senders) and the halo
-    bytes per neighbouring pair and direction."""
+    bytes per neighbouring pair and direction (push-sum since round 5: the plane's direction
+    bytes + HALO_CAP = 256 (s, w) slots per 1024-node chunk, gp_xchg.hpp)."""
     from tests.multirank_emu import full_capacity, resolve, slab_bounds
     from tests.test_multigpu_plan import cap_of, imp3d_pair_stats
     P, _, g = resolve(n, topo)
@@ -95,6 +96,8 @@ def pair_bytes(n, topo, alg, W, halves=1, lists=True):
     else:
         bounds, H = slab_bounds(P, g, topo, W)
         halo = H * (1 + (16 if push else 0))
+        if push and halo_compact:
+            halo = H + (H + 1023) // 1024 * 256 * 16
         if topo == "Imp3D":
             _, mu, _ = imp3d_pair_stats(P, g, W)
             for a in range(W):
@@ -174,7 +177,9 @@ def model(tdir, n, topo, alg, W, rounds, out=None):
     legacy = topo != "full" and any("k_unpack" in k for k in per_slab_names(groups, short))
     if legacy:
         first_k, second_k = "k_pack", "k_unpack"
-    P, bounds, B, halo = pair_bytes(n, topo, alg, W, halves, lists=not legacy)
+    # compacted halo planes (round 5): k_halo_pack in the trace
+    hc = any("k_halo" in k for k in per_slab_names(groups, short))
+    P, bounds, B, halo = pair_bytes(n, topo, alg, W, halves, lists=not legacy, halo_compact=hc)
     kern = {k: [statistics.mean(x[s] for x in v) for s in range(W)] for k, v in per_slab.items()}
     comp = [statistics.mean(v) for v in rank_ms]
     t_comp = max(comp)
