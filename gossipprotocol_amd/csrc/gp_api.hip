@@ -20,6 +20,7 @@
 // GP_FLAG_VIRTUAL_RANKS), which run the same kernels and exchange plan with
 // device copies -- the single-GPU test bed of the multi-GPU path.
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cmath>
 #include <cerrno>
@@ -97,7 +98,8 @@ struct Slab {
     unsigned int* overflow = nullptr;  // device flag
     // Imp3D push-sum over several ranks: sender-ordered lists (gp_xchg.hpp)
     bool lists = false;
-    uint32_t nt = 0, tsplit = 0;       // the slab's tiles; first tile of region 1
+    uint32_t nt = 0;                   // the slab's tiles
+    uint32_t tb[XMAXH + 1] = {};       // region h: tiles [tb[h], tb[h + 1])
     uint32_t* gw = nullptr;            // [tile * W + d]: first header word of the tile's segment
     uint16_t* xdr = nullptr;           // [id - lo]: d << 10 | rank in the tile's list for d (static)
     uint8_t* lwt = nullptr;            // [tile * (W + 1) + d]: the tile's LDS word layout in k_list_pack
@@ -168,7 +170,7 @@ struct gp_sim {
     // every slab's (each rank computes the whole table from the global random edges)
     std::vector<uint32_t> list_nw;
     hipStream_t xstream = nullptr;
-    hipEvent_t ev_send[2] = {nullptr, nullptr}, ev_xfer[2] = {nullptr, nullptr};
+    hipEvent_t ev_send[XMAXH] = {}, ev_xfer[XMAXH] = {};
     BlockPlan bplan{};  // KERNEL_BLOCK
 };
 
@@ -431,13 +433,20 @@ int halo_pack_expand(gp_sim* s, int b, bool pack) {
     return GP_OK;
 }
 
+constexpr int XREGIONS = 4;  // Imp3D push-sum exchange regions (see exchange_regions)
+
 // Exchange regions of a slab's senders: push-sum runs two (one's transfer overlaps the
 // other's packing), gossip one.  Imp3D push-sum cuts them at a tile boundary (the lists'
 // tiles); the full topology at the slab's middle id.
 int exchange_regions(const gp_sim* s) {
-    int NH = s->cfg.algorithm == GP_PUSHSUM ? 2 : 1;
+    const bool push = s->cfg.algorithm == GP_PUSHSUM;
+    // Imp3D push-sum lists: XREGIONS regions of the slab's tiles (the last one's transfer is what
+    // the round cannot hide); the full topology's two halves
+    int NH = push ? (s->cfg.topology == GP_IMP3D ? XREGIONS : 2) : 1;
 #ifdef GP_EXPERIMENTS
     if (const char* e = std::getenv("GP_XHALVES")) NH = std::max(1, std::min(2, std::atoi(e)));
+    if (const char* e = std::getenv("GP_XREGIONS"))
+        if (push && s->cfg.topology == GP_IMP3D) NH = std::max(1, std::min(XMAXH, std::atoi(e)));
 #endif
     return NH;
 }
@@ -450,9 +459,14 @@ uint32_t slab_tiles(uint32_t lo, uint32_t nloc) {
 void xregion(const Slab& sl, int NH, int h, uint32_t& s_lo, uint32_t& s_hi) {
     const DevState& S = sl.S;
     uint32_t split = S.nloc / 2;
-    if (sl.lists) {  // tiles [0, tsplit) | [tsplit, nt)
-        const int64_t b = (int64_t)(S.lo / XTILE + sl.tsplit) * XTILE - S.lo;
-        split = (uint32_t)std::min<int64_t>(S.nloc, std::max<int64_t>(0, b));
+    if (sl.lists) {  // tiles [tb[h], tb[h + 1])
+        auto at = [&](uint32_t t) {
+            const int64_t b = (int64_t)(S.lo / XTILE + t) * XTILE - S.lo;
+            return (uint32_t)std::min<int64_t>(S.nloc, std::max<int64_t>(0, b));
+        };
+        s_lo = at(sl.tb[h]);
+        s_hi = h + 1 == NH ? S.nloc : at(sl.tb[h + 1]);
+        return;
     }
     s_lo = NH == 1 || h == 0 ? 0u : split;
     s_hi = NH == 1 || h == 1 ? S.nloc : split;
@@ -485,12 +499,13 @@ int build_lists(gp_sim* s, const uint32_t* rnd_all, uint32_t* kk, const uint32_t
     s->list_nw.assign((size_t)W * NH * W, 0);
     std::vector<std::vector<uint32_t>> gw_all(W);
     std::vector<std::vector<uint8_t>> lwt_all(W);
-    std::vector<uint32_t> tsplit(W);
+    std::vector<std::array<uint32_t, XMAXH + 1>> tb(W);  // per slab: region tile boundaries
     Scratch tmp_mem;
     for (int a = 0; a < W; ++a) {
         const uint32_t lo = s->bounds[a], nloc = s->bounds[a + 1] - lo;
         const uint32_t nt = slab_tiles(lo, nloc);
-        tsplit[a] = NH == 2 ? nt / 2 : nt;
+        for (int h = 0; h <= NH; ++h) tb[a][h] = (uint32_t)((uint64_t)nt * h / NH);
+        for (int h = NH + 1; h <= XMAXH; ++h) tb[a][h] = nt;
         uint32_t* cnt = nullptr;
         HIP_TRY(tmp_mem.alloc(&cnt, (size_t)nt * W + 1));
         ListCountArgs ca{};
@@ -518,9 +533,9 @@ int build_lists(gp_sim* s, const uint32_t* rnd_all, uint32_t* kk, const uint32_t
             lwt[(size_t)t * (W + 1) + W] = (uint8_t)w;  // <= 16 + W words
         }
         for (int d = 0; d < W; ++d) {
-            uint64_t run[2] = {0, 0};
-            for (uint32_t t = 0; t < nt; ++t) {
-                const int h = t < tsplit[a] ? 0 : 1;
+            uint64_t run[XMAXH] = {};
+            for (uint32_t t = 0, h = 0; t < nt; ++t) {
+                while ((int)h + 1 < NH && t >= tb[a][h + 1]) ++h;
                 gw[(size_t)t * W + d] = (uint32_t)run[h];
                 run[h] += (hc[(size_t)t * W + d] + 63u) / 64u;
             }
@@ -546,7 +561,8 @@ int build_lists(gp_sim* s, const uint32_t* rnd_all, uint32_t* kk, const uint32_t
         ka.gw = gw;
         ka.lo = lo;
         ka.nloc = nloc;
-        ka.tsplit = tsplit[a];
+        for (int h = 0; h <= XMAXH; ++h) ka.tb[h] = tb[a][h];
+        ka.NH = NH;
         ka.W = W;
         ka.a = a;
         for (int w = 0; w <= W; ++w) ka.bounds[w] = s->bounds[w];
@@ -569,7 +585,7 @@ int build_lists(gp_sim* s, const uint32_t* rnd_all, uint32_t* kk, const uint32_t
         const int r = sl.rank;
         sl.lists = true;
         sl.nt = slab_tiles(S.lo, S.nloc);
-        sl.tsplit = tsplit[r];
+        for (int h = 0; h <= XMAXH; ++h) sl.tb[h] = tb[r][h];
         if ((rc = dev_alloc_t(s, &sl.gw, gw_all[r].size() + 1)) || (rc = dev_alloc_t(s, &sl.lwt, lwt_all[r].size() + 16)))
             return rc;
         HIP_TRY(hipMemcpyAsync(sl.gw, gw_all[r].data(), sizeof(uint32_t) * gw_all[r].size(), hipMemcpyHostToDevice,
@@ -1207,8 +1223,8 @@ int exchange(gp_sim* s, uint32_t rn) {
                     la.lo = S.lo;
                     la.nloc = S.nloc;
                     la.base = S.base;
-                    la.t0 = h == 0 ? 0u : sl.tsplit;
-                    la.t1 = NH == 1 || h == 1 ? sl.nt : sl.tsplit;
+                    la.t0 = sl.tb[h];
+                    la.t1 = h + 1 == NH ? sl.nt : sl.tb[h + 1];
                     la.W = W;
                     la.me = sl.rank;
                     for (int d = 0; d < W; ++d) {
@@ -2140,7 +2156,7 @@ void gp_destroy(gp_sim* s) {
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     if (s->xstream) (void)hipStreamSynchronize(s->xstream);
     for (auto& e : s->ev) (void)hipEventDestroy(e);
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < XMAXH; ++h) {
         if (s->ev_send[h]) (void)hipEventDestroy(s->ev_send[h]);
         if (s->ev_xfer[h]) (void)hipEventDestroy(s->ev_xfer[h]);
     }

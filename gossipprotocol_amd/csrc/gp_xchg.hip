@@ -305,7 +305,8 @@ __global__ __launch_bounds__(256) void k_list_key(ListKeyArgs a) {
         }
     }
     tile_list_rank(dst, rho, R, a.W);
-    const int h = t < a.tsplit ? 0 : 1;
+    int h = 0;
+    while (h + 1 < a.NH && t >= a.tb[h + 1]) ++h;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const uint32_t j = sp.T + k * 256u + threadIdx.x;

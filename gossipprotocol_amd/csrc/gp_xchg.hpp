@@ -79,7 +79,7 @@ struct ExpectArgs {
 // ---- Imp3D push-sum: sender-ordered lists (round 5).  For each rank pair a -> b
 // the static list L_ab = a's senders whose random edge lands on b, in id order,
 // cut into the slab's 1024-id tiles (XTILE, the push-sum tile kernel's TILE) and
-// two regions (tiles [0, tsplit) and [tsplit, nt)); every (tile, b) segment starts
+// NH <= XMAXH regions of consecutive tiles (tb[h] <= tile < tb[h + 1]); every (tile, b) segment starts
 // on a 64-entry boundary of the region's list (gw: its first header word).  Per
 // round the sender writes, per region and destination, one header word per 64
 // list entries -- the bitmap of the entries whose sender used its random edge and
@@ -87,6 +87,7 @@ struct ExpectArgs {
 // used entries' (s, w) compacted in list order.  The receiver finds a used remote
 // in-edge's message at base + popcount(mask below its bit): no scatter, no slots.
 constexpr uint32_t XTILE = 1024;
+constexpr int XMAXH = 4;           // exchange regions of a slab (push-sum), at most
 constexpr uint32_t XNONE = 0xFFu;  // "no list entry" (local target or no sender)
 
 struct ListPeer {              // send side: region h, destination d
@@ -121,10 +122,11 @@ struct ListCountArgs {         // setup, slab a: list entries per (tile, destina
 struct ListKeyArgs {           // setup, slab a: every sender's list key at its destination
     const uint32_t* rnd;       // global random edges
     const uint32_t* gw;        // slab a's [tile * W + d]
-    uint32_t lo, nloc, tsplit;
-    int W, a;
+    uint32_t lo, nloc;
+    uint32_t tb[XMAXH + 1];    // region h: tiles [tb[h], tb[h + 1]) of the slab (relative to lo / XTILE)
+    int NH, W, a;
     uint32_t bounds[XMAXW + 1];
-    uint32_t hw[2][XMAXW];     // [h][b]: first header word of chunk (h, a) in b's header region
+    uint32_t hw[XMAXH][XMAXW]; // [h][b]: first header word of chunk (h, a) in b's header region
     uint32_t* key;             // [global id]: 64 * header word + bit at the destination (local targets untouched)
     uint16_t* xdr;             // optional, [id - lo]: d << 10 | rank in the tile's list for d, or XDR_NONE
 };

@@ -139,12 +139,13 @@ XTILE = 1024  # the lists' tiles: 1024 ids on global multiples (the push-sum til
 class ListPlan:
     """Imp3D push-sum over several ranks: the sender-ordered lists (gp_xchg.hpp,
     gp_api.hip build_lists / setup_exchange).  List L_ab = slab a's senders whose
-    random edge lands on slab b, in id order, cut into the slab's tiles and two
-    regions (tiles [0, nt // 2) and the rest); every (tile, b) segment starts on a
-    64-entry boundary.  Computed from the global random edges, like every rank of
-    the library does for every slab."""
+    random edge lands on slab b, in id order, cut into the slab's tiles and NH
+    regions of consecutive tiles (region h: tiles [nt h / NH, nt (h + 1) / NH),
+    gp_api.hip XREGIONS = 4); every (tile, b) segment starts on a 64-entry
+    boundary.  Computed from the global random edges, like every rank of the
+    library does for every slab."""
 
-    def __init__(self, P, g, W, bounds, rnd_all, geo, NH=2):
+    def __init__(self, P, g, W, bounds, rnd_all, geo, NH=4):
         self.W, self.NH, self.bounds = W, NH, bounds
         owner = np.searchsorted(np.array(bounds[1:-1]), rnd_all, side="right")
         ids = np.arange(P)
@@ -158,8 +159,9 @@ class ListPlan:
             lo, hi = bounds[a], bounds[a + 1]
             t_of = ids[lo:hi] // XTILE - lo // XTILE            # tile of each sender (relative)
             nt = (hi + XTILE - 1) // XTILE - lo // XTILE
-            tsplit = nt // 2 if NH == 2 else nt
-            h_of = (t_of >= tsplit).astype(np.int64)
+            tb = np.array([nt * h // NH for h in range(NH + 1)])
+            region_of_tile = np.searchsorted(tb[1:NH], np.arange(nt), side="right")
+            h_of = region_of_tile[t_of]
             self.region[lo:hi] = h_of
             np.add.at(mu, (h_of, a, owner[lo:hi]), inv_deg[lo:hi])
             for b in range(W):
@@ -170,7 +172,7 @@ class ListPlan:
                 words = (cnt + 63) // 64
                 gw = np.zeros(nt, dtype=np.int64)
                 for h in range(NH):
-                    in_h = (np.arange(nt) >= tsplit) == bool(h)
+                    in_h = region_of_tile == h
                     gw[in_h] = np.cumsum(words[in_h]) - words[in_h]
                     self.nw[a, h, b] = int(words[in_h].sum())
                 first = np.cumsum(cnt) - cnt  # list position of each tile's first entry

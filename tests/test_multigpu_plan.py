@@ -171,21 +171,26 @@ def test_realised_imp3d_counts_stay_below_capacity_world8():
     src_rank = np.searchsorted(np.array(bounds[1:-1]), ids, side="right")
     dst_rank = np.searchsorted(np.array(bounds[1:-1]), rnd, side="right")
     inv_deg = 1.0 / geo.degree(ids)
-    # push-sum exchange region of every sender (setup_exchange / build_lists): its tile's half of
-    # the slab's 1024-id tiles (tiles on global multiples of 1024)
+    # push-sum exchange region of every sender (setup_exchange / build_lists): its tile's quarter
+    # of the slab's 1024-id tiles (tiles on global multiples of 1024; region h: tiles
+    # [nt h / NH, nt (h + 1) / NH), NH = 4)
+    NH = 4
     b_arr = np.array(bounds)
     lo_t = b_arr[src_rank] // 1024
     nt = (b_arr[src_rank + 1] + 1023) // 1024 - lo_t
-    half = ((ids // 1024 - lo_t) >= nt // 2).astype(np.int64)
-    mu = np.zeros((2, W, W))
+    t_rel = ids // 1024 - lo_t
+    half = np.zeros(P, dtype=np.int64)
+    for h in range(1, NH):
+        half += (t_rel >= nt * h // NH).astype(np.int64)
+    mu = np.zeros((NH, W, W))
     np.add.at(mu, (half, src_rank, dst_rank), inv_deg)
     cap = np.vectorize(lambda m: min(cap_of(m), 10**9))(mu)
     worst = 0.0
-    off = np.broadcast_to(~np.eye(W, dtype=bool), (2, W, W))
+    off = np.broadcast_to(~np.eye(W, dtype=bool), (NH, W, W))
     for r in range(40):
         d = geo.draw_dir(ids, S_PUSHSUM, r)
         sent = d == DIR_RANDOM
-        cnt = np.zeros((2, W, W), dtype=np.int64)
+        cnt = np.zeros((NH, W, W), dtype=np.int64)
         np.add.at(cnt, (half[sent], src_rank[sent], dst_rank[sent]), 1)
         assert np.all(cnt[off] <= cap[off])
         worst = max(worst, float(np.max((cnt[off] - mu[off]) / np.sqrt(mu[off]))))

@@ -170,6 +170,10 @@ def model(tdir, n, topo, alg, W, rounds, out=None):
     # (full, gp_api.hip launch_round_full_multi) or the pack / unpack (Imp3D, exchange):
     # those kernels appear twice per slab
     halves = 2 if alg == "push-sum" and topo in ("full", "Imp3D") else 1
+    if alg == "push-sum" and topo == "Imp3D":  # round 5: XREGIONS list regions (k_list_pack per region and slab)
+        npk = [sum(1 for name, _ in grp if short(name) == "k_list_pack") for grp in groups]
+        if npk and npk[-1] and npk[-1] % W == 0:
+            halves = npk[-1] // W
     # (Imp3D push-sum since round 5: k_list_pack per region, no unpack -- the round kernel reads the
     # received lists in place)
     first_k, second_k = ("k_fbm_send", "k_fbm_coarse") if topo == "full" else ("k_list_pack", None)
@@ -184,7 +188,7 @@ def model(tdir, n, topo, alg, W, rounds, out=None):
     comp = [statistics.mean(v) for v in rank_ms]
     t_comp = max(comp)
     piped = None
-    if halves == 2:
+    if halves >= 2:
         # per rank: send half 0, half 1; coarse half 0, half 1 (dispatch order), the rest
         hk = {}
         for grp in groups:
@@ -193,14 +197,14 @@ def model(tdir, n, topo, alg, W, rounds, out=None):
                 by.setdefault(short(name), []).append(ms)
             for nm in (first_k, second_k):
                 v = by.get(nm, [])
-                if nm and len(v) == 2 * W:
+                if nm and len(v) == halves * W:
                     hk.setdefault(nm, []).append(v)
         if len(hk.get(first_k, [])) and (second_k is None or len(hk.get(second_k, []))):
-            s_h = [[statistics.mean(x[h * W + k] for x in hk[first_k]) for k in range(W)] for h in range(2)]
-            c_h = ([[statistics.mean(x[h * W + k] for x in hk[second_k]) for k in range(W)] for h in range(2)]
-                   if second_k else [[0.0] * W, [0.0] * W])
+            s_h = [[statistics.mean(x[h * W + k] for x in hk[first_k]) for k in range(W)] for h in range(halves)]
+            c_h = ([[statistics.mean(x[h * W + k] for x in hk[second_k]) for k in range(W)] for h in range(halves)]
+                   if second_k else [[0.0] * W for _ in range(halves)])
             piped = {"send_half_ms": [max(v) for v in s_h], "coarse_half_ms": [max(v) for v in c_h],
-                     "rest_ms": max(comp[k] - s_h[0][k] - s_h[1][k] - c_h[0][k] - c_h[1][k] for k in range(W))}
+                     "rest_ms": max(comp[k] - sum(s_h[h][k] + c_h[h][k] for h in range(halves)) for k in range(W))}
     res = {"workload": f"{alg} {topo} n={n} P={P}", "W": W, "rounds_measured": len(groups),
            "per_slab_kernel_ms": {k: [round(x, 4) for x in v] for k, v in kern.items()},
            "global_kernel_ms": {k: round(statistics.mean(v), 4) for k, v in glob_k.items()},
@@ -222,12 +226,18 @@ def model(tdir, n, topo, alg, W, rounds, out=None):
         serial = t_comp + t_x + ALLREDUCE_LAT_MS
         overlap = max(t_comp, t_x) + ALLREDUCE_LAT_MS
         if piped:  # as scheduled: x_h after send_h / pack_h, coarse_h / unpack_h after x_h (one exchange stream)
-            xh = t_x / 2
-            s0, s1 = piped["send_half_ms"]
-            c0, c1 = piped["coarse_half_ms"]
-            x0_end = s0 + xh
-            x1_end = max(x0_end, s0 + s1) + xh
-            c_end = max(max(s0 + s1, x0_end) + c0, x1_end) + c1
+            sh, ch = piped["send_half_ms"], piped["coarse_half_ms"]
+            nh = len(sh)
+            xh = t_x / nh
+            t_send = x_end = 0.0
+            for h in range(nh):  # packs back to back on the compute stream, transfers in order on the exchange stream
+                t_send += sh[h]
+                x_end = max(x_end, t_send) + xh
+            if nh == 2:  # full topology: the coarse pass of half 0 overlaps half 1's transfer
+                x0_end = sh[0] + xh
+                c_end = max(max(sh[0] + sh[1], x0_end) + ch[0], x_end) + ch[1]
+            else:
+                c_end = x_end + sum(ch)
             overlap = c_end + piped["rest_ms"] + ALLREDUCE_LAT_MS
         res["model"].append({"link_gbps": bw, "exchange_ms": round(t_x, 4), "round_ms_serial": round(serial, 4),
                              "round_ms_as_scheduled": round(overlap, 4) if piped else round(serial, 4),
