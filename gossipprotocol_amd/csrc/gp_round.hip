@@ -357,7 +357,7 @@ __device__ __forceinline__ void st_stream(uint32_t* p, uint32_t v) {
 // Per tile:
 //   1. in-edge pass (Imp3D): did each in-edge's sender use its random edge
 //      this round?  Every node active: the sender's own Philox draw, redrawn --
-//      the senders were loaded during the previous tile, and the FU redraws of a
+//      the senders are streamed in at the tile's start, and the FU redraws of a
 //      thread run as one straight-line batch so the chains interleave; during
 //      activation: the ballot-packed bitmap.  Used edges' (s, w) are gathered by
 //      LDS-DMA into slot q (edge order);
@@ -384,8 +384,8 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
     const uint32_t cap = min((uint32_t)SLOTS, a.stage_cap);
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
 
-    // loaded one tile ahead: the next tile's in-edge range (two uniform loads)
-    // and its senders (FU words per thread, staged tiles only)
+    // loaded one tile ahead: the next tile's in-edge range (two uniform loads); the
+    // staged tile's senders, FU words per thread (loaded at the tile's start)
     uint32_t pf_tile = 0xFFFFFFFFu, pf_lo = 0, pf_hi = 0;
     uint32_t raw[FU];
 #pragma unroll
