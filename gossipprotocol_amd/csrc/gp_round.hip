@@ -123,7 +123,14 @@ struct TileLds {
 // in-edges (6 sigma above the mean TILE: ~1e-9 of tiles) takes the unstaged path,
 // so the node fold reads LDS only (no global fallback inside its loop, whose
 // join would cost a vmcnt(0) wait per message).
-constexpr int SLOTS = TILE + TILE / 8 + TILE / 16;  // 1216 at TILE = 1024: the LDS of 5 blocks per CU
+#ifndef GP_SND_PF
+// Imp3D push-sum: the next tile's in-edge senders LDS-DMA'd during this tile's node phase, so a
+// tile's in-edge pass starts from LDS (C5, same box, alternated: 12.92-13.07 -> 12.78-12.86 ms,
+// profiles/r05/sndpf/; 0 builds the round-4 form)
+#define GP_SND_PF 1
+#endif
+// 1216 at TILE = 1024: the LDS of 5 blocks per CU (GP_SND_PF: 1152, room for the senders' buffer)
+constexpr int SLOTS = GP_SND_PF ? TILE + TILE / 8 : TILE + TILE / 8 + TILE / 16;
 constexpr int SLOT_FU = (SLOTS + TPB - 1) / TPB;  // in-edges per thread in the in-edge pass
 
 struct TileLdsP {
@@ -131,6 +138,7 @@ struct TileLdsP {
     uint32_t xm[W_PLANE + DMA_SLACK];
     uint32_t xp[W_PLANE + DMA_SLACK];
     uint32_t ind[TILE / 8 + DMA_SLACK];  // in-degrees of the tile's nodes, a nibble each (DevState::ind4)
+    uint32_t snd[GP_SND_PF ? SLOTS + DMA_SLACK : 1];  // GP_SND_PF: the next tile's in-edge senders
     unsigned long long bits[SLOT_FU * (TPB / 64) + 1];  // bit q: in-edge q (tile order) was used by its sender; then 0
     double2 msg[SLOTS];               // edge q's message at slot q
     uint32_t out[TILE / 4];
@@ -387,6 +395,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
     // loaded one tile ahead: the next tile's in-edge range (two uniform loads); the
     // staged tile's senders, FU words per thread (loaded at the tile's start)
     uint32_t pf_tile = 0xFFFFFFFFu, pf_lo = 0, pf_hi = 0;
+    uint32_t snd_tile = 0xFFFFFFFFu, snd_off = 0;  // GP_SND_PF: L.snd holds tile snd_tile's senders from word snd_off
     uint32_t raw[FU];
 #pragma unroll
     for (int m = 0; m < FU; ++m) raw[m] = 0u;
@@ -462,10 +471,18 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                 if (GP_SETPRIO >= 4) __builtin_amdgcn_s_setprio(GP_PRIO);
                 // in-edge q = m * TPB + wave * 64 + lane is bit `lane` of bitmap word
                 // m * 4 + wave; its message (if used) lands in slot q
+                if (GP_SND_PF && snd_tile == ti) {  // (block-uniform) prefetched during the last tile
 #pragma unroll
-                for (int m = 0; m < FU; ++m) {
-                    const uint32_t q = threadIdx.x + m * TPB;
-                    raw[m] = q < cnt ? __builtin_nontemporal_load(srcp + e_lo + q) : 0u;
+                    for (int m = 0; m < FU; ++m) {
+                        const uint32_t q = threadIdx.x + m * TPB;
+                        raw[m] = q < cnt ? L.snd[snd_off + q] : 0u;
+                    }
+                } else {
+#pragma unroll
+                    for (int m = 0; m < FU; ++m) {
+                        const uint32_t q = threadIdx.x + m * TPB;
+                        raw[m] = q < cnt ? __builtin_nontemporal_load(srcp + e_lo + q) : 0u;
+                    }
                 }
                 uint32_t rkv[REMOTE ? FU : 1];
 #if GP_RK_EARLY
@@ -922,6 +939,16 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                         if (GP_SETPRIO >= 5) __builtin_amdgcn_s_setprio(GP_PRIO);
                         st_stream(swn + j, make_double2(acc_s, acc_w));
                         if (GP_SETPRIO >= 5) __builtin_amdgcn_s_setprio(0);
+                    }
+                }
+                // GP_SND_PF: after the first node slot (the next tile's in-edge range has arrived by
+                // then), its senders by LDS-DMA; this tile's were read in its in-edge pass, and the
+                // tile's closing barrier retires the copy before the next tile reads it
+                if (GP_SND_PF && TOPO == IMP3D && k0 == 0) {
+                    snd_tile = 0xFFFFFFFFu;
+                    if (pf_tile != 0xFFFFFFFFu && pf_hi - pf_lo <= cap) {
+                        snd_off = dma_stage_words(L.snd, srcp, pf_lo, pf_hi);
+                        snd_tile = pf_tile;
                     }
                 }
             }
