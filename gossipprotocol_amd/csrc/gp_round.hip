@@ -125,8 +125,8 @@ struct TileLds {
 // join would cost a vmcnt(0) wait per message).
 #ifndef GP_SND_PF
 // Imp3D push-sum: the next tile's in-edge senders LDS-DMA'd during this tile's node phase, so a
-// tile's in-edge pass starts from LDS (C5, same box, alternated: 12.92-13.07 -> 12.78-12.86 ms,
-// profiles/r05/sndpf/; 0 builds the round-4 form)
+// tile's in-edge pass starts from LDS (C5, same box, alternated: 12.92-13.07 -> 12.78-12.86 ms on
+// one box, 12.78-12.82 -> 12.74-12.77 on another, profiles/r05/sndpf/; 0 builds the round-4 form)
 #define GP_SND_PF 1
 #endif
 // 1216 at TILE = 1024: the LDS of 5 blocks per CU (GP_SND_PF: 1152, room for the senders' buffer)
