@@ -396,6 +396,9 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
     // staged tile's senders, FU words per thread (loaded at the tile's start)
     uint32_t pf_tile = 0xFFFFFFFFu, pf_lo = 0, pf_hi = 0;
     uint32_t snd_tile = 0xFFFFFFFFu, snd_off = 0;  // GP_SND_PF: L.snd holds tile snd_tile's senders from word snd_off
+    // (one rank only: with REMOTE slabs at W = 8 it measured 1.88-1.90 against 1.90-1.93 ms per slab without,
+    // same box -- within noise, not adopted there; profiles/r05/sndpf/w8.txt)
+    constexpr bool SNDPF = GP_SND_PF && !REMOTE;
     uint32_t raw[FU];
 #pragma unroll
     for (int m = 0; m < FU; ++m) raw[m] = 0u;
@@ -471,7 +474,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                 if (GP_SETPRIO >= 4) __builtin_amdgcn_s_setprio(GP_PRIO);
                 // in-edge q = m * TPB + wave * 64 + lane is bit `lane` of bitmap word
                 // m * 4 + wave; its message (if used) lands in slot q
-                if (GP_SND_PF && snd_tile == ti) {  // (block-uniform) prefetched during the last tile
+                if (SNDPF && snd_tile == ti) {  // (block-uniform) prefetched during the last tile
 #pragma unroll
                     for (int m = 0; m < FU; ++m) {
                         const uint32_t q = threadIdx.x + m * TPB;
@@ -944,7 +947,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                 // GP_SND_PF: after the first node slot (the next tile's in-edge range has arrived by
                 // then), its senders by LDS-DMA; this tile's were read in its in-edge pass, and the
                 // tile's closing barrier retires the copy before the next tile reads it
-                if (GP_SND_PF && TOPO == IMP3D && k0 == 0) {
+                if (SNDPF && TOPO == IMP3D && k0 == 0) {
                     snd_tile = 0xFFFFFFFFu;
                     if (pf_tile != 0xFFFFFFFFu && pf_hi - pf_lo <= cap) {
                         snd_off = dma_stage_words(L.snd, srcp, pf_lo, pf_hi);
