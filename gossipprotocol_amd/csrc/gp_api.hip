@@ -106,6 +106,8 @@ struct Slab {
     uint32_t* xcnt = nullptr;          // [h * W + d]: reservation counters of the send chunks
     std::vector<size_t> lhdr, lval;    // send buffer: byte offsets of chunk (h, d)'s header words / slots
     std::vector<size_t> rhdr, rval;    // receive buffer: byte offsets of chunk (h, p)'s header words / slots
+    size_t xr_stride = 0;              // the receive buffer of odd rounds at xrecv + xr_stride (region-by-region
+                                       // rounds: the next round's lists arrive during this one), else 0
     std::vector<uint32_t> vbase;       // [h * W + d]: index of my chunk's first slot in d's vals region
     // Imp3D gossip (column kernel) over several ranks: random-edge sends as bitmaps (gp_xchg.hpp)
     bool bits = false;
@@ -314,8 +316,8 @@ int alloc_slab(gp_sim* s, Slab& sl, int r) {
     S.rk = nullptr;
     S.rtg = nullptr;
     S.sbits = nullptr;
-    S.xhdr = nullptr;
-    S.xvals = nullptr;
+    S.xhdr[0] = S.xhdr[1] = nullptr;
+    S.xvals[0] = S.xvals[1] = nullptr;
     S.xnv = 0;
     int rc;
     const size_t next = (size_t)(S.ext_hi - S.base) + 1024;  // node arrays (+ word-I/O padding)
@@ -451,6 +453,29 @@ int exchange_regions(const gp_sim* s) {
     return NH;
 }
 
+// Round kernel launches per round (DevState::rregions).  Imp3D push-sum across ranks runs the
+// round kernel region by region (launch_round_regions): region h's lists are packed and travel
+// while the later regions compute.  C5 modelled from virtual ranks, same box, against one launch
+// per round with the lists packed and sent after it (profiles/r05/rregions/): W = 2 12.92 ->
+// 10.50 ms at 128 GB/s per link and direction, 17.97 -> 12.48 at 64; W = 4 5.46 -> 5.48 and
+// 6.76 -> 5.81; W = 8 2.75 -> 2.74 and 2.96 -> 2.83 (the round kernel itself +2-5 %: four launch
+// tails).  1: one launch per round.
+uint32_t round_regions(const gp_sim* s, int kernel, uint32_t walk) {
+    if (s->world < 2 || s->cfg.topology != GP_IMP3D || s->cfg.algorithm != GP_PUSHSUM || kernel != KERNEL_TILE ||
+        walk != 3)
+        return 1;
+    int on = 1;
+#ifdef GP_EXPERIMENTS
+    if (const char* e = std::getenv("GP_RREGIONS")) on = std::atoi(e);
+#endif
+    const int NH = exchange_regions(s);
+    if (!on || NH < 2 || NH > RREG_MAX) return 1;
+    uint32_t rb[RREG_MAX + 1];
+    for (int w = 0; w < s->world; ++w)
+        if (!region_tiles(s->bounds[w], s->bounds[w + 1] - s->bounds[w], (uint64_t)s->g * s->g, NH, rb)) return 1;
+    return (uint32_t)NH;
+}
+
 uint32_t slab_tiles(uint32_t lo, uint32_t nloc) {
     return (uint32_t)(((uint64_t)lo + nloc + XTILE - 1) / XTILE - lo / XTILE);
 }
@@ -504,7 +529,10 @@ int build_lists(gp_sim* s, const uint32_t* rnd_all, uint32_t* kk, const uint32_t
     for (int a = 0; a < W; ++a) {
         const uint32_t lo = s->bounds[a], nloc = s->bounds[a + 1] - lo;
         const uint32_t nt = slab_tiles(lo, nloc);
-        for (int h = 0; h <= NH; ++h) tb[a][h] = (uint32_t)((uint64_t)nt * h / NH);
+        // regions of whole planes (region_tiles: the round kernel's regions when it runs region by
+        // region), else of equal tile counts
+        if (!region_tiles(lo, nloc, (uint64_t)s->g * s->g, NH, tb[a].data()))
+            for (int h = 0; h <= NH; ++h) tb[a][h] = (uint32_t)((uint64_t)nt * h / NH);
         for (int h = NH + 1; h <= XMAXH; ++h) tb[a][h] = nt;
         uint32_t* cnt = nullptr;
         HIP_TRY(tmp_mem.alloc(&cnt, (size_t)nt * W + 1));
@@ -953,13 +981,17 @@ int setup_exchange(gp_sim* s) {
                 for (int b = 0; b < W; ++b)
                     if (b != a) sl.rval[(size_t)h * W + b] = hdr_in + (size_t)vo(a, h, b) * 16;
             const size_t ro = hdr_in + (size_t)nv_in * 16;
-            if ((rc = dev_alloc_t(s, &sl.xsend, so)) || (rc = dev_alloc_t(s, &sl.xrecv, ro)) ||
+            sl.xr_stride = sl.S.rregions > 1 ? (ro + 255) & ~(size_t)255 : 0;  // one buffer per round parity
+            const size_t rt = sl.xr_stride ? 2 * sl.xr_stride : ro;
+            if ((rc = dev_alloc_t(s, &sl.xsend, so)) || (rc = dev_alloc_t(s, &sl.xrecv, rt)) ||
                 (rc = dev_alloc_t(s, &sl.xcnt, R)))
                 return rc;
             HIP_TRY(hipMemsetAsync(sl.xsend, 0, so ? so : 16, s->stream));
-            HIP_TRY(hipMemsetAsync(sl.xrecv, 0, ro ? ro : 16, s->stream));
-            sl.S.xhdr = reinterpret_cast<const XHdr*>(sl.xrecv);
-            sl.S.xvals = reinterpret_cast<const double2*>(sl.xrecv + hdr_in);
+            HIP_TRY(hipMemsetAsync(sl.xrecv, 0, rt ? rt : 16, s->stream));
+            for (int k = 0; k < 2; ++k) {
+                sl.S.xhdr[k] = reinterpret_cast<const XHdr*>(sl.xrecv + k * sl.xr_stride);
+                sl.S.xvals[k] = reinterpret_cast<const double2*>(sl.xrecv + k * sl.xr_stride + hdr_in);
+            }
             sl.S.xnv = (uint32_t)std::max<uint64_t>(1, nv_in);
             sl.overflow = &sl.S.ctl->overflow;
         }
@@ -993,7 +1025,12 @@ int setup_exchange(gp_sim* s) {
         sl.overflow = &sl.S.ctl->overflow;
     }
     if (NH > 1) {  // the second stream and the events that order it with the compute stream
-        HIP_TRY(hipStreamCreateWithFlags(&s->xstream, hipStreamNonBlocking));
+        // the greatest priority: when a pack completes, the transfer it releases (RCCL's kernel) and
+        // the next persistent round kernel launch become ready together -- the transfer is dispatched
+        // first, and the round kernel's blocks fill the slots left
+        int least = 0, greatest = 0;
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        HIP_TRY(hipStreamCreateWithPriority(&s->xstream, hipStreamNonBlocking, greatest));
         for (int h = 0; h < NH; ++h) {
             HIP_TRY(hipEventCreateWithFlags(&s->ev_send[h], hipEventDisableTiming));
             HIP_TRY(hipEventCreateWithFlags(&s->ev_xfer[h], hipEventDisableTiming));
@@ -1170,19 +1207,35 @@ int launch_round_full_multi(gp_sim* s, uint32_t r, hipEvent_t e0, hipEvent_t e1)
 // (with the halo planes) overlaps region 1's packing.  Gossip packs {slot} or {count}
 // entries and unpacks them (k_pack / k_unpack).  Events order the streams, so every
 // rank issues its RCCL groups in one order (region 0, region 1), before the finalize
-// all-reduce on the compute stream.
-int exchange(gp_sim* s, uint32_t rn) {
-    const int W = s->world;
-    if (W == 1 || s->cfg.topology == GP_FULL) return GP_OK;  // full: the exchange is inside the round
-    const int b = rn & 1;
-    const bool push = s->cfg.algorithm == GP_PUSHSUM;
-    const bool imp = s->cfg.topology == GP_IMP3D;
-    const int NH = imp ? s->xhalves : 1;
-    hipStream_t xs = NH > 1 && s->xstream ? s->xstream : s->stream;
-    const size_t H = s->halo;
-    const size_t HS = s->halo_slots;  // push-sum: the halo planes' (s, w) compacted (setup_halo)
+// all-reduce on the compute stream.  exchange() = exchange_open, exchange_region for every
+// region (halo planes in region 0's group), exchange_close; launch_round_regions runs the same
+// pieces region by region behind the round kernel's launches (halo planes in the last group).
+struct XchgCtx {
+    int W, b, NH;
+    bool push, imp, lists, bits;
+    hipStream_t xs;
+    size_t H, HS;
+    XchgCtx(const gp_sim* s, uint32_t rn) {
+        W = s->world;
+        b = rn & 1;
+        push = s->cfg.algorithm == GP_PUSHSUM;
+        imp = s->cfg.topology == GP_IMP3D;
+        NH = imp ? s->xhalves : 1;
+        xs = NH > 1 && s->xstream ? s->xstream : s->stream;
+        H = s->halo;
+        HS = s->halo_slots;  // push-sum: the halo planes' (s, w) compacted (setup_halo)
+        lists = imp && push && s->slab[0].lists;
+        bits = imp && s->slab[0].bits;
+    }
+};
+
+// The halo planes of round rn: compacted (s, w) packed; in-process ranks copy them here.
+int exchange_open(gp_sim* s, uint32_t rn) {
+    const XchgCtx x(s, rn);
+    const int W = x.W, b = x.b;
+    const size_t H = x.H, HS = x.HS;
     int rc;
-    if (push && HS && (rc = halo_pack_expand(s, b, true))) return rc;
+    if (x.push && HS && (rc = halo_pack_expand(s, b, true))) return rc;
     if (s->mode == MODE_VIRTUAL) {  // halo planes by device copies (round kernel -> next round kernel)
         for (int r = 0; r + 1 < W; ++r) {
             DevState& A = s->slab[r].S;  // lower slab
@@ -1193,12 +1246,12 @@ int exchange(gp_sim* s, uint32_t rn) {
                                    hipMemcpyDeviceToDevice, s->stream));
             HIP_TRY(hipMemcpyAsync(A.nb[b] + (edge - A.base), B.nb[b] + (edge - B.base), H, hipMemcpyDeviceToDevice,
                                    s->stream));
-            if (push && HS) {
+            if (x.push && HS) {
                 HIP_TRY(hipMemcpyAsync(s->slab[r + 1].hrecv[0], s->slab[r].hsend[1], HS * 16, hipMemcpyDeviceToDevice,
                                        s->stream));
                 HIP_TRY(hipMemcpyAsync(s->slab[r].hrecv[1], s->slab[r + 1].hsend[0], HS * 16, hipMemcpyDeviceToDevice,
                                        s->stream));
-            } else if (push) {
+            } else if (x.push) {
                 HIP_TRY(hipMemcpyAsync(B.sw[b] + (edge - H - B.base), A.sw[b] + (edge - H - A.base), H * 16,
                                        hipMemcpyDeviceToDevice, s->stream));
                 HIP_TRY(hipMemcpyAsync(A.sw[b] + (edge - A.base), B.sw[b] + (edge - B.base), H * 16,
@@ -1206,154 +1259,175 @@ int exchange(gp_sim* s, uint32_t rn) {
             }
         }
     }
-    const bool lists = imp && push && s->slab[0].lists;
-    const bool bits = imp && s->slab[0].bits;
-    for (int h = 0; h < NH; ++h) {
-        if (imp && !bits) {  // (bitmaps: set by the round kernel itself)
-            for (Slab& sl : s->slab) {
-                DevState& S = sl.S;
-                if (lists) {  // header words + compacted messages of region h (k_list_pack)
-                    HIP_TRY(hipMemsetAsync(sl.xcnt + (size_t)h * W, 0, sizeof(uint32_t) * W, s->stream));
-                    ListPackArgs la{};
-                    la.nbn = S.nb[b];
-                    la.swn = S.sw[b];
-                    la.xdr = sl.xdr;
-                    la.lwt = sl.lwt;
-                    la.gw = sl.gw;
-                    la.lo = S.lo;
-                    la.nloc = S.nloc;
-                    la.base = S.base;
-                    la.t0 = sl.tb[h];
-                    la.t1 = h + 1 == NH ? sl.nt : sl.tb[h + 1];
-                    la.W = W;
-                    la.me = sl.rank;
-                    for (int d = 0; d < W; ++d) {
-                        if (d == sl.rank) continue;
-                        const size_t i = (size_t)h * W + d;
-                        la.peer[d].hdr = reinterpret_cast<XHdr*>(sl.xsend + sl.lhdr[i]);
-                        la.peer[d].vals = reinterpret_cast<double2*>(sl.xsend + sl.lval[i]);
-                        la.peer[d].cnt = sl.xcnt + i;
-                        la.peer[d].cap = sl.cap_out[i];
-                        la.peer[d].vbase = sl.vbase[i];
-                    }
-                    la.overflow = sl.overflow;
-                    HIP_TRY(launch_list_pack(la, s->stream));
-                    continue;
-                }
-                ZeroArgs z{};
-                PackArgs pa{};
-                pa.nbn = S.nb[b];
-                pa.swn = push ? S.sw[b] : nullptr;
-                pa.rnd = S.rnd;
-                pa.pos = sl.pos;
-                pa.xdst = sl.xdst;
-                pa.lo = S.lo;
-                pa.nloc = S.nloc;
-                pa.s_lo = NH == 1 || h == 0 ? 0u : S.nloc / 2;
-                pa.s_hi = NH == 1 || h == 1 ? S.nloc : S.nloc / 2;
-                pa.base = S.base;
-                pa.W = W;
-                pa.me = sl.rank;
-                pa.push = push ? 1 : 0;
-                pa.counts = col_gossip_counts(S) ? 1 : 0;
-                for (int w = 0; w <= W; ++w) pa.bounds[w] = s->bounds[w];
-                for (int p = 0; p < W; ++p) {
-                    const size_t i = (size_t)h * W + p;
-                    pa.peer[p] = xpeer(sl.xsend, sl.soff[i], sl.cap_out[i]);
-                    z.cnt[p] = pa.peer[p].cnt;
-                }
-                z.n = W;
-                pa.overflow = sl.overflow;
-                HIP_TRY(launch_zero_counts(z, s->stream));
-                HIP_TRY(launch_pack(pa, s->grid, s->stream));
-            }
-        }
-        if (xs != s->stream) {
-            HIP_TRY(hipEventRecord(s->ev_send[h], s->stream));
-            HIP_TRY(hipStreamWaitEvent(xs, s->ev_send[h], 0));
-        }
-        if (s->mode == MODE_VIRTUAL) {
-            if (bits) {
-                for (Slab& a : s->slab)
-                    for (Slab& d : s->slab)
-                        if (&a != &d && a.bn[d.rank])
-                            HIP_TRY(hipMemcpyAsync(d.rbits_in + d.ro[a.rank] / 32, a.S.sbits + a.bo[d.rank] / 32,
-                                                   (size_t)(a.bn[d.rank] + 31) / 32 * 4, hipMemcpyDeviceToDevice, xs));
-            } else if (lists) {
-                for (Slab& a : s->slab)
-                    for (Slab& d : s->slab) {
-                        if (&a == &d) continue;
-                        const size_t i = (size_t)h * W + d.rank, j = (size_t)h * W + a.rank;
-                        const size_t hb = (size_t)s->list_nw[((size_t)a.rank * NH + h) * W + d.rank] * 16;
-                        if (hb)
-                            HIP_TRY(hipMemcpyAsync(d.xrecv + d.rhdr[j], a.xsend + a.lhdr[i], hb,
-                                                   hipMemcpyDeviceToDevice, xs));
-                        if (a.cap_out[i])
-                            HIP_TRY(hipMemcpyAsync(d.xrecv + d.rval[j], a.xsend + a.lval[i], (size_t)a.cap_out[i] * 16,
-                                                   hipMemcpyDeviceToDevice, xs));
-                    }
-            } else if (imp) {
-                rc = transfer_xbufs(s, h, xs);
-                if (rc) return rc;
-            }
-        } else {
-            Slab& sl = s->slab[0];
+    return GP_OK;
+}
+
+// Region h of round rn's random-edge exchange: packed on the compute stream, then handed to the
+// exchange stream (one RCCL group per region; the halo planes travel in region hg's group).
+int exchange_region(gp_sim* s, uint32_t rn, int h, int hg) {
+    const XchgCtx x(s, rn);
+    const int W = x.W, b = x.b, NH = x.NH;
+    const bool push = x.push, imp = x.imp, lists = x.lists, bits = x.bits;
+    const hipStream_t xs = x.xs;
+    const size_t H = x.H, HS = x.HS;
+    int rc;
+    if (imp && !bits) {  // (bitmaps: set by the round kernel itself)
+        for (Slab& sl : s->slab) {
             DevState& S = sl.S;
-            const int r = sl.rank;
-            NCCL_TRY(ncclGroupStart());
-            if (h == 0 && r > 0) {  // my first H ids <-> lower neighbour's last H ids
-                NCCL_TRY(ncclSend(S.nb[b] + (S.lo - S.base), H, ncclUint8, r - 1, s->comm, xs));
-                NCCL_TRY(ncclRecv(S.nb[b] + (S.lo - H - S.base), H, ncclUint8, r - 1, s->comm, xs));
-                if (push && HS) {
-                    NCCL_TRY(ncclSend(sl.hsend[0], HS * 16, ncclUint8, r - 1, s->comm, xs));
-                    NCCL_TRY(ncclRecv(sl.hrecv[0], HS * 16, ncclUint8, r - 1, s->comm, xs));
-                } else if (push) {
-                    NCCL_TRY(ncclSend(S.sw[b] + (S.lo - S.base), H * 16, ncclUint8, r - 1, s->comm, xs));
-                    NCCL_TRY(ncclRecv(S.sw[b] + (S.lo - H - S.base), H * 16, ncclUint8, r - 1, s->comm, xs));
+            if (lists) {  // header words + compacted messages of region h (k_list_pack)
+                HIP_TRY(hipMemsetAsync(sl.xcnt + (size_t)h * W, 0, sizeof(uint32_t) * W, s->stream));
+                ListPackArgs la{};
+                la.nbn = S.nb[b];
+                la.swn = S.sw[b];
+                la.xdr = sl.xdr;
+                la.lwt = sl.lwt;
+                la.gw = sl.gw;
+                la.lo = S.lo;
+                la.nloc = S.nloc;
+                la.base = S.base;
+                la.t0 = sl.tb[h];
+                la.t1 = h + 1 == NH ? sl.nt : sl.tb[h + 1];
+                la.W = W;
+                la.me = sl.rank;
+                for (int d = 0; d < W; ++d) {
+                    if (d == sl.rank) continue;
+                    const size_t i = (size_t)h * W + d;
+                    la.peer[d].hdr = reinterpret_cast<XHdr*>(sl.xsend + sl.lhdr[i]);
+                    la.peer[d].vals = reinterpret_cast<double2*>(sl.xsend + sl.lval[i]);
+                    la.peer[d].cnt = sl.xcnt + i;
+                    la.peer[d].cap = sl.cap_out[i];
+                    la.peer[d].vbase = sl.vbase[i];
                 }
+                la.overflow = sl.overflow;
+                HIP_TRY(launch_list_pack(la, s->stream));
+                continue;
             }
-            if (h == 0 && r < W - 1) {  // my last H ids <-> upper neighbour's first H ids
-                NCCL_TRY(ncclSend(S.nb[b] + (sl.hi - H - S.base), H, ncclUint8, r + 1, s->comm, xs));
-                NCCL_TRY(ncclRecv(S.nb[b] + (sl.hi - S.base), H, ncclUint8, r + 1, s->comm, xs));
-                if (push && HS) {
-                    NCCL_TRY(ncclSend(sl.hsend[1], HS * 16, ncclUint8, r + 1, s->comm, xs));
-                    NCCL_TRY(ncclRecv(sl.hrecv[1], HS * 16, ncclUint8, r + 1, s->comm, xs));
-                } else if (push) {
-                    NCCL_TRY(ncclSend(S.sw[b] + (sl.hi - H - S.base), H * 16, ncclUint8, r + 1, s->comm, xs));
-                    NCCL_TRY(ncclRecv(S.sw[b] + (sl.hi - S.base), H * 16, ncclUint8, r + 1, s->comm, xs));
-                }
+            ZeroArgs z{};
+            PackArgs pa{};
+            pa.nbn = S.nb[b];
+            pa.swn = push ? S.sw[b] : nullptr;
+            pa.rnd = S.rnd;
+            pa.pos = sl.pos;
+            pa.xdst = sl.xdst;
+            pa.lo = S.lo;
+            pa.nloc = S.nloc;
+            pa.s_lo = NH == 1 || h == 0 ? 0u : S.nloc / 2;
+            pa.s_hi = NH == 1 || h == 1 ? S.nloc : S.nloc / 2;
+            pa.base = S.base;
+            pa.W = W;
+            pa.me = sl.rank;
+            pa.push = push ? 1 : 0;
+            pa.counts = col_gossip_counts(S) ? 1 : 0;
+            for (int w = 0; w <= W; ++w) pa.bounds[w] = s->bounds[w];
+            for (int p = 0; p < W; ++p) {
+                const size_t i = (size_t)h * W + p;
+                pa.peer[p] = xpeer(sl.xsend, sl.soff[i], sl.cap_out[i]);
+                z.cnt[p] = pa.peer[p].cnt;
             }
-            if (bits)
-                for (int p = 0; p < W; ++p) {  // the bitmap chunks, each way
-                    if (p == r) continue;
-                    const size_t ob = (size_t)(sl.bn[p] + 31) / 32 * 4, ib = (size_t)(sl.rn[p] + 31) / 32 * 4;
-                    if (ob) NCCL_TRY(ncclSend(S.sbits + sl.bo[p] / 32, ob, ncclUint8, p, s->comm, xs));
-                    if (ib) NCCL_TRY(ncclRecv(sl.rbits_in + sl.ro[p] / 32, ib, ncclUint8, p, s->comm, xs));
-                }
-            else if (lists)
-                for (int p = 0; p < W; ++p) {  // header words, then messages, each way
-                    if (p == r) continue;
-                    const size_t i = (size_t)h * W + p;
-                    const size_t ho = (size_t)s->list_nw[((size_t)r * NH + h) * W + p] * 16;
-                    const size_t hi = (size_t)s->list_nw[((size_t)p * NH + h) * W + r] * 16;
-                    if (ho) NCCL_TRY(ncclSend(sl.xsend + sl.lhdr[i], ho, ncclUint8, p, s->comm, xs));
-                    if (sl.cap_out[i])
-                        NCCL_TRY(ncclSend(sl.xsend + sl.lval[i], (size_t)sl.cap_out[i] * 16, ncclUint8, p, s->comm, xs));
-                    if (hi) NCCL_TRY(ncclRecv(sl.xrecv + sl.rhdr[i], hi, ncclUint8, p, s->comm, xs));
-                    if (sl.cap_in[i])
-                        NCCL_TRY(ncclRecv(sl.xrecv + sl.rval[i], (size_t)sl.cap_in[i] * 16, ncclUint8, p, s->comm, xs));
-                }
-            else if (imp)
-                for (int p = 0; p < W; ++p) {
-                    if (p == r) continue;
-                    const size_t i = (size_t)h * W + p;
-                    if (sl.sbytes[i]) NCCL_TRY(ncclSend(sl.xsend + sl.soff[i], sl.sbytes[i], ncclUint8, p, s->comm, xs));
-                    if (sl.rbytes[i]) NCCL_TRY(ncclRecv(sl.xrecv + sl.roff[i], sl.rbytes[i], ncclUint8, p, s->comm, xs));
-                }
-            NCCL_TRY(ncclGroupEnd());
+            z.n = W;
+            pa.overflow = sl.overflow;
+            HIP_TRY(launch_zero_counts(z, s->stream));
+            HIP_TRY(launch_pack(pa, s->grid, s->stream));
         }
-        if (xs != s->stream) HIP_TRY(hipEventRecord(s->ev_xfer[h], xs));
     }
+    if (xs != s->stream) {
+        HIP_TRY(hipEventRecord(s->ev_send[h], s->stream));
+        HIP_TRY(hipStreamWaitEvent(xs, s->ev_send[h], 0));
+    }
+    if (s->mode == MODE_VIRTUAL) {
+        if (bits) {
+            for (Slab& a : s->slab)
+                for (Slab& d : s->slab)
+                    if (&a != &d && a.bn[d.rank])
+                        HIP_TRY(hipMemcpyAsync(d.rbits_in + d.ro[a.rank] / 32, a.S.sbits + a.bo[d.rank] / 32,
+                                               (size_t)(a.bn[d.rank] + 31) / 32 * 4, hipMemcpyDeviceToDevice, xs));
+        } else if (lists) {
+            for (Slab& a : s->slab)
+                for (Slab& d : s->slab) {
+                    if (&a == &d) continue;
+                    const size_t i = (size_t)h * W + d.rank, j = (size_t)h * W + a.rank;
+                    const size_t hb = (size_t)s->list_nw[((size_t)a.rank * NH + h) * W + d.rank] * 16;
+                    if (hb)
+                        HIP_TRY(hipMemcpyAsync(d.xrecv + (size_t)b * d.xr_stride + d.rhdr[j], a.xsend + a.lhdr[i], hb,
+                                               hipMemcpyDeviceToDevice, xs));
+                    if (a.cap_out[i])
+                        HIP_TRY(hipMemcpyAsync(d.xrecv + (size_t)b * d.xr_stride + d.rval[j], a.xsend + a.lval[i],
+                                               (size_t)a.cap_out[i] * 16,
+                                               hipMemcpyDeviceToDevice, xs));
+                }
+        } else if (imp) {
+            rc = transfer_xbufs(s, h, xs);
+            if (rc) return rc;
+        }
+    } else {
+        Slab& sl = s->slab[0];
+        DevState& S = sl.S;
+        const int r = sl.rank;
+        uint8_t* xr = sl.xrecv + (size_t)b * sl.xr_stride;  // lists: this round parity's receive buffer
+        NCCL_TRY(ncclGroupStart());
+        if (h == hg && r > 0) {  // my first H ids <-> lower neighbour's last H ids
+            NCCL_TRY(ncclSend(S.nb[b] + (S.lo - S.base), H, ncclUint8, r - 1, s->comm, xs));
+            NCCL_TRY(ncclRecv(S.nb[b] + (S.lo - H - S.base), H, ncclUint8, r - 1, s->comm, xs));
+            if (push && HS) {
+                NCCL_TRY(ncclSend(sl.hsend[0], HS * 16, ncclUint8, r - 1, s->comm, xs));
+                NCCL_TRY(ncclRecv(sl.hrecv[0], HS * 16, ncclUint8, r - 1, s->comm, xs));
+            } else if (push) {
+                NCCL_TRY(ncclSend(S.sw[b] + (S.lo - S.base), H * 16, ncclUint8, r - 1, s->comm, xs));
+                NCCL_TRY(ncclRecv(S.sw[b] + (S.lo - H - S.base), H * 16, ncclUint8, r - 1, s->comm, xs));
+            }
+        }
+        if (h == hg && r < W - 1) {  // my last H ids <-> upper neighbour's first H ids
+            NCCL_TRY(ncclSend(S.nb[b] + (sl.hi - H - S.base), H, ncclUint8, r + 1, s->comm, xs));
+            NCCL_TRY(ncclRecv(S.nb[b] + (sl.hi - S.base), H, ncclUint8, r + 1, s->comm, xs));
+            if (push && HS) {
+                NCCL_TRY(ncclSend(sl.hsend[1], HS * 16, ncclUint8, r + 1, s->comm, xs));
+                NCCL_TRY(ncclRecv(sl.hrecv[1], HS * 16, ncclUint8, r + 1, s->comm, xs));
+            } else if (push) {
+                NCCL_TRY(ncclSend(S.sw[b] + (sl.hi - H - S.base), H * 16, ncclUint8, r + 1, s->comm, xs));
+                NCCL_TRY(ncclRecv(S.sw[b] + (sl.hi - S.base), H * 16, ncclUint8, r + 1, s->comm, xs));
+            }
+        }
+        if (bits)
+            for (int p = 0; p < W; ++p) {  // the bitmap chunks, each way
+                if (p == r) continue;
+                const size_t ob = (size_t)(sl.bn[p] + 31) / 32 * 4, ib = (size_t)(sl.rn[p] + 31) / 32 * 4;
+                if (ob) NCCL_TRY(ncclSend(S.sbits + sl.bo[p] / 32, ob, ncclUint8, p, s->comm, xs));
+                if (ib) NCCL_TRY(ncclRecv(sl.rbits_in + sl.ro[p] / 32, ib, ncclUint8, p, s->comm, xs));
+            }
+        else if (lists)
+            for (int p = 0; p < W; ++p) {  // header words, then messages, each way
+                if (p == r) continue;
+                const size_t i = (size_t)h * W + p;
+                const size_t ho = (size_t)s->list_nw[((size_t)r * NH + h) * W + p] * 16;
+                const size_t hi = (size_t)s->list_nw[((size_t)p * NH + h) * W + r] * 16;
+                if (ho) NCCL_TRY(ncclSend(sl.xsend + sl.lhdr[i], ho, ncclUint8, p, s->comm, xs));
+                if (sl.cap_out[i])
+                    NCCL_TRY(ncclSend(sl.xsend + sl.lval[i], (size_t)sl.cap_out[i] * 16, ncclUint8, p, s->comm, xs));
+                if (hi) NCCL_TRY(ncclRecv(xr + sl.rhdr[i], hi, ncclUint8, p, s->comm, xs));
+                if (sl.cap_in[i])
+                    NCCL_TRY(ncclRecv(xr + sl.rval[i], (size_t)sl.cap_in[i] * 16, ncclUint8, p, s->comm, xs));
+            }
+        else if (imp)
+            for (int p = 0; p < W; ++p) {
+                if (p == r) continue;
+                const size_t i = (size_t)h * W + p;
+                if (sl.sbytes[i]) NCCL_TRY(ncclSend(sl.xsend + sl.soff[i], sl.sbytes[i], ncclUint8, p, s->comm, xs));
+                if (sl.rbytes[i]) NCCL_TRY(ncclRecv(sl.xrecv + sl.roff[i], sl.rbytes[i], ncclUint8, p, s->comm, xs));
+            }
+        NCCL_TRY(ncclGroupEnd());
+    }
+    if (xs != s->stream) HIP_TRY(hipEventRecord(s->ev_xfer[h], xs));
+    return GP_OK;
+}
+
+// After the last region: received bitmaps applied / entries unpacked, halo planes expanded.
+int exchange_close(gp_sim* s, uint32_t rn) {
+    const XchgCtx x(s, rn);
+    const int W = x.W, b = x.b, NH = x.NH;
+    const bool push = x.push, imp = x.imp, lists = x.lists, bits = x.bits;
+    const hipStream_t xs = x.xs;
+    const size_t HS = x.HS;
+    int rc;
     if (bits) {
         if (xs != s->stream) HIP_TRY(hipStreamWaitEvent(s->stream, s->ev_xfer[NH - 1], 0));
         for (Slab& sl : s->slab) {
@@ -1391,6 +1465,16 @@ int exchange(gp_sim* s, uint32_t rn) {
     return GP_OK;
 }
 
+int exchange(gp_sim* s, uint32_t rn) {
+    if (s->world == 1 || s->cfg.topology == GP_FULL) return GP_OK;  // full: the exchange is inside the round
+    const XchgCtx x(s, rn);
+    int rc;
+    if ((rc = exchange_open(s, rn))) return rc;
+    for (int h = 0; h < x.NH; ++h)
+        if ((rc = exchange_region(s, rn, h, 0))) return rc;
+    return exchange_close(s, rn);
+}
+
 // Close round `round_done` (if round_next > 0) and prepare round `round_next`.
 int finalize(gp_sim* s, uint32_t round_done, uint32_t round_next) {
     if (s->mode == MODE_SINGLE) {
@@ -1411,9 +1495,33 @@ int finalize(gp_sim* s, uint32_t round_done, uint32_t round_next) {
     return GP_OK;
 }
 
+// One round of Imp3D push-sum across ranks, region by region (DevState::rregions): the round
+// kernel over region h's tiles, then region h's lists packed and handed to the exchange stream,
+// whose transfer overlaps the next regions' round kernel launches; the halo planes (first and
+// last region) travel in the last group.  The lists arrive in the other parity's receive buffer
+// (Slab::xr_stride): this round's kernels still read theirs.  e0 / e1 bracket the round kernel
+// launches and the packs between them.
+int launch_round_regions(gp_sim* s, uint32_t r, hipEvent_t e0, hipEvent_t e1) {
+    const uint32_t NR = s->slab[0].S.rregions;
+    const uint32_t rn = r + 1;
+    int rc;
+    if (e0) HIP_TRY(hipEventRecord(e0, s->stream));
+    for (uint32_t h = 0; h < NR; ++h) {
+        for (Slab& sl : s->slab) HIP_TRY(launch_round_tile_region(sl.S, r, h, s->grid, s->stream));
+        if (h + 1 == NR) {
+            if (e1) HIP_TRY(hipEventRecord(e1, s->stream));
+            if ((rc = exchange_open(s, rn))) return rc;
+        }
+        if ((rc = exchange_region(s, rn, (int)h, (int)NR - 1))) return rc;
+    }
+    if ((rc = exchange_close(s, rn))) return rc;
+    return finalize(s, r, rn);
+}
+
 // One synchronous round r: round kernel(s), exchange, finalize.
 int launch_round(gp_sim* s, uint32_t r, hipEvent_t e0, hipEvent_t e1) {
     if (s->cfg.topology == GP_FULL && s->world > 1) return launch_round_full_multi(s, r, e0, e1);
+    if (s->slab[0].S.rregions > 1) return launch_round_regions(s, r, e0, e1);
     for (size_t q = 0; q < s->slab.size(); ++q) {
         DevState& S = s->slab[q].S;
         if (q == 0 && e0) HIP_TRY(hipEventRecord(e0, s->stream));
@@ -1565,6 +1673,7 @@ int build_sim(gp_sim* s) {
     int kernel;
     uint32_t col_xsegs, walk, wx, wide;
     choose_kernel(s, nloc_max, kernel, col_xsegs, walk, wx, wide);
+    const uint32_t rreg = round_regions(s, kernel, walk);
     if (s->mode == MODE_VIRTUAL) {
         s->slab.resize(s->world);
         for (int w = 0; w < s->world; ++w) s->slab[w].rank = w;
@@ -1598,9 +1707,10 @@ int build_sim(gp_sim* s) {
         if (const char* e = std::getenv("GP_STAGE_CAP")) sl.S.tile_stage_cap = (uint32_t)std::max(0, std::atoi(e));
 #endif
         if ((rc = alloc_slab(s, sl, sl.rank))) return rc;
+        sl.S.rregions = rreg;
         if (sl.S.tile_walk == 3) {  // the tile list of the per-XCD queues
             std::vector<uint32_t> list;
-            if (!build_walk_list(sl.S, list, sl.S.woff)) {
+            if (!build_walk_list(sl.S, (int)sl.S.rregions, list, sl.S.woff)) {
                 set_err("internal: walk-3 tile list does not cover the slab");
                 return GP_EINVAL;
             }

@@ -15,6 +15,7 @@ constexpr int HIST = 4096;            // per-round alert ring (host syncs at lea
 constexpr uint32_t INJ_CHUNK = 65536; // injector live-list chunk (ids); 2048 bitmap words
 constexpr int BULK_THREADS = 256;
 constexpr int FIN_THREADS = 1024;
+constexpr int RREG_MAX = 4;           // round kernel launches per round, at most (DevState::rregions)
 
 // Device-resident control block.  Written by the single-block finalize kernel
 // between bulk rounds; bulk kernels only read it (plus atomics on the
@@ -202,9 +203,11 @@ struct DevState {
     // Imp3D push-sum across ranks (sender-ordered lists, gp_xchg.hpp): per local in-edge
     // whose sender lives on another rank, its list key (64 * header word + bit) in this
     // rank's received header region; the received headers and messages of the round
+    // ([b]: the buffer the exchange for a round of parity b fills; one buffer for both unless
+    // the round kernel runs region by region, when the next round's lists arrive during this one)
     uint32_t* rk;
-    const XHdr* xhdr;
-    const double2* xvals;
+    const XHdr* xhdr[2];
+    const double2* xvals[2];
     uint32_t xnv;  // message slots in the vals region
     int kernel;  // KERNEL_* below
     // column kernels: x segments per patch (set at create from the resident grid)
@@ -223,11 +226,15 @@ struct DevState {
     // TQ_STRIDE words apart (one 256-byte line each)
     uint32_t* tq;
     // walk 3: the slab's tiles (relative to lo / TILE) in visiting order, XCD c's
-    // items at [woff[c], woff[c + 1])
+    // items at [woff[0][c], woff[0][c + 1]); with rregions > 1 launches per round
+    // (launch_round_regions, gp_api.hip) launch h visits region h's tiles, XCD c's
+    // at [woff[h][c], woff[h][c + 1])
     uint32_t* wtiles;
-    uint32_t woff[9];
+    uint32_t rregions;
+    uint32_t woff[RREG_MAX][9];
 };
 constexpr int TQ_STRIDE = 64;
+hipError_t launch_round_tile_region(const DevState& S, uint32_t round, uint32_t h, int grid, hipStream_t st);
 
 // Arguments of the tiled round kernels (gp_round.hip): only what they read.
 struct RoundArgs {
@@ -317,7 +324,8 @@ hipError_t launch_col_seed_init(const DevState& S, hipStream_t st);
 uint32_t rbits_words_for(uint32_t lo, uint32_t nloc);
 hipError_t launch_round_tile(const DevState& S, uint32_t round, int grid, hipStream_t st);
 int ps_tile_resident_blocks(int topo, bool remote, int device);
-bool build_walk_list(const DevState& S, std::vector<uint32_t>& list, uint32_t woff[9]);
+bool build_walk_list(const DevState& S, int NR, std::vector<uint32_t>& list, uint32_t woff[][9]);
+bool region_tiles(uint32_t lo, uint32_t nloc, uint64_t g2, int NR, uint32_t* rb);
 hipError_t launch_rbits_init(const DevState& S, int grid, hipStream_t st);
 uint32_t ind4_bytes_for(uint32_t lo, uint32_t nloc);
 hipError_t launch_pack_ind4(const DevState& S, uint32_t wide_at, int grid, hipStream_t st);

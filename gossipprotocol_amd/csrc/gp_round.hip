@@ -1285,8 +1285,8 @@ RoundArgs make_round_args(const DevState& S, uint32_t round) {
     a.rtag = S.rtag;
     a.rmsg = S.rmsg;
     a.rk = S.rk;
-    a.xhdr = S.xhdr;
-    a.xvals = S.xvals;
+    a.xhdr = S.xhdr[round & 1];
+    a.xvals = S.xvals[round & 1];
     a.xnv = S.xnv;
     a.c = S.c ? S.c - S.lo : nullptr;
     a.lo = S.lo;
@@ -1304,18 +1304,35 @@ RoundArgs make_round_args(const DevState& S, uint32_t round) {
     a.wx = S.tile_wx;
     a.fuse = S.fuse_finalize;
     a.wt = S.wtiles;
-    for (int c = 0; c <= 8; ++c) a.wo[c] = S.woff[c];
+    for (int c = 0; c <= 8; ++c) a.wo[c] = S.woff[0][c];
     a.tq = S.tq + (round & 1) * 8 * TQ_STRIDE;
     a.tq_next = S.tq + ((round + 1) & 1) * 8 * TQ_STRIDE;
     return a;
 }
 
+// Region h of NR of a plane-aligned slab: planes [x0 + nx h / NR, x0 + nx (h + 1) / NR), whose
+// tiles (relative to lo / TILE) are [rb[h], rb[h + 1]) -- a tile belongs to the plane it starts
+// in (the slab's first tile to the first plane).  False if the slab is not plane-aligned.
+bool region_tiles(uint32_t lo, uint32_t nloc, uint64_t g2, int NR, uint32_t* rb) {
+    if (!g2 || nloc % g2 || lo % g2 || NR < 1) return false;
+    const uint32_t tb = lo / TILE;
+    const uint32_t tend = (uint32_t)(((uint64_t)lo + nloc + TILE - 1) / TILE);
+    const uint32_t x0 = (uint32_t)(lo / g2), nx = (uint32_t)(nloc / g2);
+    for (int h = 0; h <= NR; ++h) {
+        const uint64_t x = x0 + (uint64_t)nx * h / NR;
+        rb[h] = (x <= x0 ? tb : (uint32_t)std::min<uint64_t>((x * g2 + TILE - 1) / TILE, tend)) - tb;
+    }
+    return true;
+}
+
 // Walk 3's visiting order (host, at create): walk 2's items (TileWalk) for each
 // of the 8 XCDs, empty items dropped -- every tile of the slab exactly once.
-// list: tiles relative to lo / TILE; woff[c]..woff[c + 1]: XCD c's items.
-bool build_walk_list(const DevState& S, std::vector<uint32_t>& list, uint32_t woff[9]) {
+// list: tiles relative to lo / TILE; woff[0][c]..woff[0][c + 1]: XCD c's items.
+// NR > 1 (launch_round_regions): the planes of region h (region_tiles) dealt to the
+// 8 XCDs in the same way, XCD c's items at woff[h][c]..woff[h][c + 1].
+bool build_walk_list(const DevState& S, int NR, std::vector<uint32_t>& list, uint32_t woff[][9]) {
     const uint64_t g2 = S.G.g2;
-    if (!g2 || S.nloc % g2 || S.lo % g2) return false;
+    if (!g2 || S.nloc % g2 || S.lo % g2 || NR < 1 || NR > RREG_MAX) return false;
     const uint32_t tb = S.lo / TILE;
     const uint32_t tend = (uint32_t)(((uint64_t)S.lo + S.nloc + TILE - 1) / TILE);
     const uint32_t x0 = (uint32_t)(S.lo / g2), nx = (uint32_t)(S.nloc / g2);
@@ -1324,22 +1341,26 @@ bool build_walk_list(const DevState& S, std::vector<uint32_t>& list, uint32_t wo
         return x <= x0 ? tb : (uint32_t)std::min<uint64_t>((x * g2 + TILE - 1) / TILE, tend);
     };
     list.clear();
-    for (uint32_t c = 0; c < 8; ++c) {
-        woff[c] = (uint32_t)list.size();
-        const uint32_t xa = x0 + (uint32_t)((uint64_t)nx * c / 8);
-        const uint32_t nxa = x0 + (uint32_t)((uint64_t)nx * (c + 1) / 8) - xa;
-        uint32_t nwin = S.tile_wx ? (nxa + S.tile_wx - 1) / S.tile_wx : 1u;
-        if (nwin == 0) nwin = 1;
-        for (uint32_t v = 0; v < nwin; ++v) {
-            const uint32_t xs = (uint32_t)((uint64_t)nxa * v / nwin), xe = (uint32_t)((uint64_t)nxa * (v + 1) / nwin);
-            for (uint32_t k = 0; k < kp; ++k)
-                for (uint32_t x = xa + xs; x < xa + xe; ++x) {
-                    const uint32_t ti = first(x) + k;
-                    if (ti < first(x + 1)) list.push_back(ti - tb);
-                }
+    for (int h = 0; h < NR; ++h) {
+        const uint32_t r0 = x0 + (uint32_t)((uint64_t)nx * h / NR);
+        const uint32_t nr = x0 + (uint32_t)((uint64_t)nx * (h + 1) / NR) - r0;
+        for (uint32_t c = 0; c < 8; ++c) {
+            woff[h][c] = (uint32_t)list.size();
+            const uint32_t xa = r0 + (uint32_t)((uint64_t)nr * c / 8);
+            const uint32_t nxa = r0 + (uint32_t)((uint64_t)nr * (c + 1) / 8) - xa;
+            uint32_t nwin = S.tile_wx ? (nxa + S.tile_wx - 1) / S.tile_wx : 1u;
+            if (nwin == 0) nwin = 1;
+            for (uint32_t v = 0; v < nwin && nxa; ++v) {
+                const uint32_t xs = (uint32_t)((uint64_t)nxa * v / nwin), xe = (uint32_t)((uint64_t)nxa * (v + 1) / nwin);
+                for (uint32_t k = 0; k < kp; ++k)
+                    for (uint32_t x = xa + xs; x < xa + xe; ++x) {
+                        const uint32_t ti = first(x) + k;
+                        if (ti < first(x + 1)) list.push_back(ti - tb);
+                    }
+            }
         }
+        woff[h][8] = (uint32_t)list.size();
     }
-    woff[8] = (uint32_t)list.size();
     return list.size() == (size_t)(tend - tb);
 }
 
@@ -1356,7 +1377,23 @@ int ps_tile_resident_blocks(int topo, bool remote, int device) {
     return per_cu * cus;
 }
 
+// Launch h of round `round` when the round kernel runs region by region (DevState::rregions;
+// Imp3D push-sum across ranks): region h's tiles, its own pair of queue counters by launch parity.
+hipError_t launch_round_tile_region(const DevState& S, uint32_t round, uint32_t h, int grid, hipStream_t st) {
+    if (S.alg != PUSHSUM || S.topo != IMP3D || !S.rk || !S.ind4 || !S.wtiles || S.tile_walk != 3 ||
+        h >= S.rregions || (grid & 7))
+        return hipErrorInvalidValue;
+    RoundArgs a = make_round_args(S, round);
+    for (int c = 0; c <= 8; ++c) a.wo[c] = S.woff[h][c];
+    const uint64_t L = (uint64_t)round * S.rregions + h;
+    a.tq = S.tq + (L & 1) * 8 * TQ_STRIDE;
+    a.tq_next = S.tq + ((L + 1) & 1) * 8 * TQ_STRIDE;
+    hipLaunchKernelGGL((k_ps_tile<IMP3D, true>), dim3(grid), dim3(TPB), 0, st, a, round);
+    return hipGetLastError();
+}
+
 hipError_t launch_round_tile(const DevState& S, uint32_t round, int grid, hipStream_t st) {
+    if (S.rregions > 1) return hipErrorInvalidValue;  // launch_round_tile_region per region
     const RoundArgs a = make_round_args(S, round);
     const dim3 g(grid), b(TPB);
     // Imp3D slabs of a multi-rank run (push-sum: received lists; gossip: tagged slots)

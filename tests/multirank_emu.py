@@ -136,12 +136,28 @@ def slab_bounds(P, g, topo, W):
 XTILE = 1024  # the lists' tiles: 1024 ids on global multiples (the push-sum tile kernel's TILE)
 
 
+def region_tiles(lo, nloc, g2, NH, nt):
+    """Tile boundaries (relative to lo // XTILE) of the NH exchange regions of a slab
+    (gp_round.hip region_tiles): region h holds the planes [x0 + nx h / NH, x0 + nx (h + 1) / NH),
+    a tile belonging to the plane it starts in; a slab not made of whole planes is cut
+    into equal tile counts."""
+    if not g2 or nloc % g2 or lo % g2:
+        return [nt * h // NH for h in range(NH + 1)]
+    tb, tend = lo // XTILE, (lo + nloc + XTILE - 1) // XTILE
+    x0, nx = lo // g2, nloc // g2
+    out = []
+    for h in range(NH + 1):
+        x = x0 + nx * h // NH
+        out.append((tb if x <= x0 else min((x * g2 + XTILE - 1) // XTILE, tend)) - tb)
+    return out
+
+
 class ListPlan:
     """Imp3D push-sum over several ranks: the sender-ordered lists (gp_xchg.hpp,
     gp_api.hip build_lists / setup_exchange).  List L_ab = slab a's senders whose
     random edge lands on slab b, in id order, cut into the slab's tiles and NH
-    regions of consecutive tiles (region h: tiles [nt h / NH, nt (h + 1) / NH),
-    gp_api.hip XREGIONS = 4); every (tile, b) segment starts on a 64-entry
+    regions of consecutive tiles (region_tiles: whole planes, gp_api.hip XREGIONS = 4);
+    every (tile, b) segment starts on a 64-entry
     boundary.  Computed from the global random edges, like every rank of the
     library does for every slab."""
 
@@ -159,7 +175,7 @@ class ListPlan:
             lo, hi = bounds[a], bounds[a + 1]
             t_of = ids[lo:hi] // XTILE - lo // XTILE            # tile of each sender (relative)
             nt = (hi + XTILE - 1) // XTILE - lo // XTILE
-            tb = np.array([nt * h // NH for h in range(NH + 1)])
+            tb = np.array(region_tiles(lo, hi - lo, g * g, NH, nt))
             region_of_tile = np.searchsorted(tb[1:NH], np.arange(nt), side="right")
             h_of = region_of_tile[t_of]
             self.region[lo:hi] = h_of

@@ -152,10 +152,13 @@ def model(tdir, n, topo, alg, W, rounds, out=None):
         for name, v in by.items():
             if "rocclr_copy" in name:
                 cp += sum(v)
-            elif len(v) == W:
-                per_slab.setdefault(short(name), []).append(v)
+            elif len(v) == W or (len(v) % W == 0 and "k_ps_tile" in name):
+                # (region-by-region rounds: the round kernel once per region and slab, slab k's
+                # launches at k, W + k, ...)
+                vs = [sum(v[h * W + k] for h in range(len(v) // W)) for k in range(W)]
+                per_slab.setdefault(short(name), []).append(vs)
                 for k in range(W):
-                    tr[k] += v[k]
+                    tr[k] += vs[k]
             elif "fill" not in name:  # (memsets: counters, on every rank)
                 glob_k.setdefault(short(name), []).append(sum(v))
                 for k in range(W):
@@ -188,7 +191,29 @@ def model(tdir, n, topo, alg, W, rounds, out=None):
     comp = [statistics.mean(v) for v in rank_ms]
     t_comp = max(comp)
     piped = None
-    if halves >= 2:
+    # region-by-region rounds (gp_api.hip launch_round_regions): per rank the round kernel of
+    # region h, then region h's pack; region h's transfer after both, overlapping region h + 1
+    rk_name = next((nm for nm in per_slab_names(groups, short) if nm.startswith("k_ps_tile")), None)
+    nreg = 0
+    if rk_name and alg == "push-sum" and topo == "Imp3D":
+        nk = sum(1 for name, _ in groups[-1] if short(name) == rk_name)
+        nreg = nk // W if nk % W == 0 and nk > W else 0
+    regions = None
+    if nreg:
+        kr, pr = [], []
+        for grp in groups:
+            kv = [ms for name, ms in grp if short(name) == rk_name]
+            pv = [ms for name, ms in grp if short(name) == "k_list_pack"]
+            if len(kv) == nreg * W and len(pv) == nreg * W:
+                kr.append(kv)
+                pr.append(pv)
+        if kr:
+            K = [[statistics.mean(x[h * W + k] for x in kr) for h in range(nreg)] for k in range(W)]
+            Pk = [[statistics.mean(x[h * W + k] for x in pr) for h in range(nreg)] for k in range(W)]
+            regions = {"kernel_region_ms": [round(max(K[k][h] for k in range(W)), 4) for h in range(nreg)],
+                       "pack_region_ms": [round(max(Pk[k][h] for k in range(W)), 4) for h in range(nreg)],
+                       "K": K, "P": Pk}
+    if halves >= 2 and not regions:
         # per rank: send half 0, half 1; coarse half 0, half 1 (dispatch order), the rest
         hk = {}
         for grp in groups:
@@ -214,7 +239,9 @@ def model(tdir, n, topo, alg, W, rounds, out=None):
            "halo_bytes_per_direction": halo, "assumptions": {
                "link_gbps_per_direction": LINK_GBPS, "group_latency_ms": GROUP_LAT_MS,
                "allreduce_latency_ms": ALLREDUCE_LAT_MS, "topology": "one xGMI link per rank pair (8-GPU node)"},
-           "model": [], "pipelined_halves": piped}
+           "model": [], "pipelined_halves": piped,
+           "round_regions": ({k: v for k, v in regions.items() if k in ("kernel_region_ms", "pack_region_ms")}
+                             if regions else None)}
     for bw in LINK_GBPS:
         # the busiest link: a pair's buffer plus, between slab neighbours, the halo plane
         link = 0.0
@@ -225,7 +252,18 @@ def model(tdir, n, topo, alg, W, rounds, out=None):
         t_x = link / (bw * 1e9) * 1e3 + (GROUP_LAT_MS if link else 0.0) * halves
         serial = t_comp + t_x + ALLREDUCE_LAT_MS
         overlap = max(t_comp, t_x) + ALLREDUCE_LAT_MS
-        if piped:  # as scheduled: x_h after send_h / pack_h, coarse_h / unpack_h after x_h (one exchange stream)
+        if regions:  # as scheduled, per rank: K_0 P_0 K_1 P_1 ...; x_h after P_h, in order on the link
+            K, Pk = regions["K"], regions["P"]
+            xh = t_x / nreg
+            worst = 0.0
+            for k in range(W):
+                t = x_end = 0.0
+                for h in range(nreg):
+                    t += K[k][h] + Pk[k][h]
+                    x_end = max(x_end, t) + xh
+                worst = max(worst, max(t, x_end) + comp[k] - sum(K[k]) - sum(Pk[k]))
+            overlap = worst + ALLREDUCE_LAT_MS
+        elif piped:  # as scheduled: x_h after send_h / pack_h, coarse_h / unpack_h after x_h (one exchange stream)
             sh, ch = piped["send_half_ms"], piped["coarse_half_ms"]
             nh = len(sh)
             xh = t_x / nh
@@ -240,7 +278,7 @@ def model(tdir, n, topo, alg, W, rounds, out=None):
                 c_end = x_end + sum(ch)
             overlap = c_end + piped["rest_ms"] + ALLREDUCE_LAT_MS
         res["model"].append({"link_gbps": bw, "exchange_ms": round(t_x, 4), "round_ms_serial": round(serial, 4),
-                             "round_ms_as_scheduled": round(overlap, 4) if piped else round(serial, 4),
+                             "round_ms_as_scheduled": round(overlap, 4) if piped or regions else round(serial, 4),
                              "exchange_share_serial": round(t_x / serial, 3), "round_ms_overlapped": round(overlap, 4),
                              "node_updates_per_s_serial": P / (serial * 1e-3),
                              "node_updates_per_s_overlapped": P / (overlap * 1e-3)})
