@@ -459,12 +459,17 @@ int exchange_regions(const gp_sim* s) {
 // per round with the lists packed and sent after it (profiles/r05/rregions/): W = 2 12.92 ->
 // 10.50 ms at 128 GB/s per link and direction, 17.97 -> 12.48 at 64; W = 4 5.46 -> 5.48 and
 // 6.76 -> 5.81; W = 8 2.75 -> 2.74 and 2.96 -> 2.83 (the round kernel itself +2-5 %: four launch
-// tails).  1: one launch per round.
+// tails).  Small slabs (< RREG_MIN_NODES) move little and keep one launch per round: their rounds
+// are launch-bound, and rank processes sharing one GPU (the tests) run them several times slower
+// with four persistent launches per round.  The experiments build's GP_RREGIONS=0/1 overrides.
+constexpr uint32_t RREG_MIN_NODES = 1u << 24;
 uint32_t round_regions(const gp_sim* s, int kernel, uint32_t walk) {
     if (s->world < 2 || s->cfg.topology != GP_IMP3D || s->cfg.algorithm != GP_PUSHSUM || kernel != KERNEL_TILE ||
         walk != 3)
         return 1;
     int on = 1;
+    for (int w = 0; w < s->world; ++w)
+        if (s->bounds[w + 1] - s->bounds[w] < RREG_MIN_NODES) on = 0;
 #ifdef GP_EXPERIMENTS
     if (const char* e = std::getenv("GP_RREGIONS")) on = std::atoi(e);
 #endif
@@ -1025,12 +1030,7 @@ int setup_exchange(gp_sim* s) {
         sl.overflow = &sl.S.ctl->overflow;
     }
     if (NH > 1) {  // the second stream and the events that order it with the compute stream
-        // the greatest priority: when a pack completes, the transfer it releases (RCCL's kernel) and
-        // the next persistent round kernel launch become ready together -- the transfer is dispatched
-        // first, and the round kernel's blocks fill the slots left
-        int least = 0, greatest = 0;
-        HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
-        HIP_TRY(hipStreamCreateWithPriority(&s->xstream, hipStreamNonBlocking, greatest));
+        HIP_TRY(hipStreamCreateWithFlags(&s->xstream, hipStreamNonBlocking));
         for (int h = 0; h < NH; ++h) {
             HIP_TRY(hipEventCreateWithFlags(&s->ev_send[h], hipEventDisableTiming));
             HIP_TRY(hipEventCreateWithFlags(&s->ev_xfer[h], hipEventDisableTiming));
@@ -2232,6 +2232,11 @@ int gp_get_info(gp_sim* s, gp_info* o) {
     }
     return GP_OK;
 }
+
+#ifdef GP_EXPERIMENTS
+// Experiments build, tests: round kernel launches per round (DevState::rregions), -1 without a handle.
+int gp_debug_round_regions(gp_sim* s) { return s && !s->slab.empty() ? (int)s->slab[0].S.rregions : -1; }
+#endif
 
 int gp_sync(gp_sim* s) {
     if (!s) {

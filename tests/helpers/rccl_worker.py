@@ -36,7 +36,9 @@ def main(argv):
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from gossipprotocol_amd import Simulation
-    sim = Simulation(n, topo, alg, seed=seed, device=device, rank=rank, world=world, dist=dist)
+    # GP_EXP=1: the experiments build (A/B runs of its GP_* switches, scripts/)
+    sim = Simulation(n, topo, alg, seed=seed, device=device, rank=rank, world=world, dist=dist,
+                     experimental=os.environ.get("GP_EXP") == "1")
     alerts = sim.step(rounds)
     info = sim.info()
     if info.slab_count <= 1 << 24:

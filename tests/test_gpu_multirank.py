@@ -46,22 +46,36 @@ CASES = [  # (num_nodes, topology, algorithm, seed, rounds, checkpoint, ranks)
 ]
 
 
-@pytest.mark.parametrize("kernel", ["default", "tile", "col"])
+@pytest.mark.parametrize("kernel", ["default", "tile", "col", "regions"])
 @pytest.mark.parametrize("n,topo,alg,seed,rounds,chk,ranks", CASES, ids=lambda v: str(v))
 def test_virtual_ranks_parity(kernel, n, topo, alg, seed, rounds, chk, ranks, monkeypatch):
     """default: the product library's own kernel choice; the others force a
-    variant through the experiments build (GP_KERNEL)."""
+    variant through the experiments build (GP_KERNEL).  regions: Imp3D push-sum
+    with the round kernel run region by region (GP_RREGIONS=1; the product does
+    so for slabs of >= 2^24 nodes, gp_api.hip round_regions) -- four launches per
+    round, the lists of each region sent behind the next, the receive buffer by
+    round parity, regions holding no plane at 8 000 nodes / 16 ranks."""
     if kernel == "col" and (topo == "line" or alg == "push-sum"):
         pytest.skip("the column march runs lattice gossip only")
     if topo == "full" and kernel not in ("default", "tile"):
         pytest.skip("the full topology has one kernel set")
+    if kernel == "regions" and (topo, alg) != ("Imp3D", "push-sum"):
+        pytest.skip("region rounds: Imp3D push-sum across ranks")
     exp = kernel != "default"
-    if exp:
+    if kernel == "regions":
+        monkeypatch.setenv("GP_RREGIONS", "1")
+        monkeypatch.setenv("GP_WALK", "3")  # (the product walks the per-XCD queues from g / W >= 64)
+        monkeypatch.setenv("GP_CHECK_CLOSE", "1")
+    elif exp:
         monkeypatch.setenv("GP_KERNEL", kernel)
         monkeypatch.setenv("GP_CHECK_CLOSE", "1")  # alerts recounted from the state after every batch
     sim = Sim(n, topo, alg, seed=seed, virtual_ranks=ranks, experimental=exp)
     orc = Oracle(n, topo, alg, seed)
     assert sim.info().num_gpus == ranks
+    if kernel == "regions":
+        assert sim._L.gp_debug_round_regions(sim._h) == 4
+    elif topo == "Imp3D" and alg == "push-sum":
+        assert (sim._L.gp_debug_round_regions(sim._h) if exp else 1) == 1  # small slabs: one launch
     done = 0
     while done < rounds:
         k = min(chk, rounds - done)
