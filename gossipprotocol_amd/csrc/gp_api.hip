@@ -436,6 +436,7 @@ int halo_pack_expand(gp_sim* s, int b, bool pack) {
 }
 
 constexpr int XREGIONS = 4;  // Imp3D push-sum exchange regions (see exchange_regions)
+constexpr uint32_t RREG_MIN_NODES = 1u << 24;  // region rounds from this slab size on (round_regions)
 
 // Exchange regions of a slab's senders: push-sum runs two (one's transfer overlaps the
 // other's packing), gossip one.  Imp3D push-sum cuts them at a tile boundary (the lists'
@@ -443,8 +444,15 @@ constexpr int XREGIONS = 4;  // Imp3D push-sum exchange regions (see exchange_re
 int exchange_regions(const gp_sim* s) {
     const bool push = s->cfg.algorithm == GP_PUSHSUM;
     // Imp3D push-sum lists: XREGIONS regions of the slab's tiles (the last one's transfer is what
-    // the round cannot hide); the full topology's two halves
+    // the round cannot hide); the full topology's two halves.  Two ranks with large slabs: eight
+    // regions, where one link carries half of every rank's messages -- C5, region rounds, same box
+    // (profiles/r05/rregions/reg8.txt): W = 2 10.72 -> 10.21 ms at 128 GB/s, 12.53 -> 11.50 at
+    // 64; at W = 4 and 8 eight were slower (5.50 -> 5.69, 2.82 -> 3.00 ms at 128 GB/s)
     int NH = push ? (s->cfg.topology == GP_IMP3D ? XREGIONS : 2) : 1;
+    if (push && s->cfg.topology == GP_IMP3D && s->world == 2 && s->bounds.size() == 3 &&
+        std::min(s->bounds[1] - s->bounds[0], s->bounds[2] - s->bounds[1]) >= RREG_MIN_NODES)
+        NH = 8;
+    static_assert(XMAXH >= 8 && RREG_MAX >= 8, "eight regions for two ranks");
 #ifdef GP_EXPERIMENTS
     if (const char* e = std::getenv("GP_XHALVES")) NH = std::max(1, std::min(2, std::atoi(e)));
     if (const char* e = std::getenv("GP_XREGIONS"))
@@ -462,7 +470,6 @@ int exchange_regions(const gp_sim* s) {
 // tails).  Small slabs (< RREG_MIN_NODES) move little and keep one launch per round: their rounds
 // are launch-bound, and rank processes sharing one GPU (the tests) run them several times slower
 // with four persistent launches per round.  The experiments build's GP_RREGIONS=0/1 overrides.
-constexpr uint32_t RREG_MIN_NODES = 1u << 24;
 uint32_t round_regions(const gp_sim* s, int kernel, uint32_t walk) {
     if (s->world < 2 || s->cfg.topology != GP_IMP3D || s->cfg.algorithm != GP_PUSHSUM || kernel != KERNEL_TILE ||
         walk != 3)

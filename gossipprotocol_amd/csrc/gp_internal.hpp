@@ -15,7 +15,7 @@ constexpr int HIST = 4096;            // per-round alert ring (host syncs at lea
 constexpr uint32_t INJ_CHUNK = 65536; // injector live-list chunk (ids); 2048 bitmap words
 constexpr int BULK_THREADS = 256;
 constexpr int FIN_THREADS = 1024;
-constexpr int RREG_MAX = 4;           // round kernel launches per round, at most (DevState::rregions)
+constexpr int RREG_MAX = 8;           // round kernel launches per round, at most (DevState::rregions)
 
 // Device-resident control block.  Written by the single-block finalize kernel
 // between bulk rounds; bulk kernels only read it (plus atomics on the

@@ -87,7 +87,7 @@ struct ExpectArgs {
 // used entries' (s, w) compacted in list order.  The receiver finds a used remote
 // in-edge's message at base + popcount(mask below its bit): no scatter, no slots.
 constexpr uint32_t XTILE = 1024;
-constexpr int XMAXH = 4;           // exchange regions of a slab (push-sum), at most
+constexpr int XMAXH = 8;           // exchange regions of a slab (push-sum), at most
 constexpr uint32_t XNONE = 0xFFu;  // "no list entry" (local target or no sender)
 
 struct ListPeer {              // send side: region h, destination d

@@ -73,7 +73,7 @@ def test_virtual_ranks_parity(kernel, n, topo, alg, seed, rounds, chk, ranks, mo
     orc = Oracle(n, topo, alg, seed)
     assert sim.info().num_gpus == ranks
     if kernel == "regions":
-        assert sim._L.gp_debug_round_regions(sim._h) == 4
+        assert sim._L.gp_debug_round_regions(sim._h) > 1
     elif topo == "Imp3D" and alg == "push-sum":
         assert (sim._L.gp_debug_round_regions(sim._h) if exp else 1) == 1  # small slabs: one launch
     done = 0
