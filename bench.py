@@ -31,6 +31,7 @@ d (the one-GPU rehearsal: RCCL over sockets, recorded as such in the JSON line).
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -200,6 +201,20 @@ def akka_baseline():
     return rec
 
 
+@contextlib.contextmanager
+def stdout_to_stderr():
+    """File descriptor 1 -> 2 for the block (messages libraries write to stdout themselves)."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -242,7 +257,9 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist  # gloo: host-side barrier / max only; data path is RCCL in the library
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        with stdout_to_stderr():  # gloo announces its connections on stdout: the JSON line stays alone there
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+            dist.barrier()
 
     def barrier():
         if dist is not None:

@@ -1506,29 +1506,32 @@ int finalize(gp_sim* s, uint32_t round_done, uint32_t round_next) {
 // kernel over region h's tiles, then region h's lists packed and handed to the exchange stream,
 // whose transfer overlaps the next regions' round kernel launches; the halo planes (first and
 // last region) travel in the last group.  The lists arrive in the other parity's receive buffer
-// (Slab::xr_stride): this round's kernels still read theirs.  e0 / e1 bracket the round kernel
-// launches and the packs between them.
-int launch_round_regions(gp_sim* s, uint32_t r, hipEvent_t e0, hipEvent_t e1) {
+// (Slab::xr_stride): this round's kernels still read theirs.  ev (kernel timing, else null):
+// 2 NR events, ev[2h] / ev[2h + 1] around launch h (the round kernel time excludes the packs).
+int launch_round_regions(gp_sim* s, uint32_t r, hipEvent_t* ev) {
     const uint32_t NR = s->slab[0].S.rregions;
     const uint32_t rn = r + 1;
     int rc;
-    if (e0) HIP_TRY(hipEventRecord(e0, s->stream));
     for (uint32_t h = 0; h < NR; ++h) {
+        if (ev) HIP_TRY(hipEventRecord(ev[2 * h], s->stream));
         for (Slab& sl : s->slab) HIP_TRY(launch_round_tile_region(sl.S, r, h, s->grid, s->stream));
-        if (h + 1 == NR) {
-            if (e1) HIP_TRY(hipEventRecord(e1, s->stream));
-            if ((rc = exchange_open(s, rn))) return rc;
-        }
+        if (ev) HIP_TRY(hipEventRecord(ev[2 * h + 1], s->stream));
+        if (h + 1 == NR && (rc = exchange_open(s, rn))) return rc;
         if ((rc = exchange_region(s, rn, (int)h, (int)NR - 1))) return rc;
     }
     if ((rc = exchange_close(s, rn))) return rc;
     return finalize(s, r, rn);
 }
 
+// Round kernel launches per round the kernel timing brackets (DevState::rregions, else 1).
+uint32_t round_launches(const gp_sim* s) { return std::max<uint32_t>(1u, s->slab[0].S.rregions); }
+
 // One synchronous round r: round kernel(s), exchange, finalize.
-int launch_round(gp_sim* s, uint32_t r, hipEvent_t e0, hipEvent_t e1) {
+// ev (kernel timing, else null): 2 * round_launches(s) events.
+int launch_round(gp_sim* s, uint32_t r, hipEvent_t* ev) {
+    if (s->slab[0].S.rregions > 1) return launch_round_regions(s, r, ev);
+    const hipEvent_t e0 = ev ? ev[0] : nullptr, e1 = ev ? ev[1] : nullptr;
     if (s->cfg.topology == GP_FULL && s->world > 1) return launch_round_full_multi(s, r, e0, e1);
-    if (s->slab[0].S.rregions > 1) return launch_round_regions(s, r, e0, e1);
     for (size_t q = 0; q < s->slab.size(); ++q) {
         DevState& S = s->slab[q].S;
         if (q == 0 && e0) HIP_TRY(hipEventRecord(e0, s->stream));
@@ -1755,7 +1758,7 @@ int build_sim(gp_sim* s) {
         return GP_EHIP;
     }
     if (s->timing) {
-        s->ev.resize(2 * BATCH);
+        s->ev.resize((size_t)2 * BATCH * round_launches(s));
         for (auto& x : s->ev) HIP_TRY(hipEventCreate(&x));
     }
     return GP_OK;
@@ -2019,11 +2022,10 @@ int64_t gp_step(gp_sim* s, int64_t nrounds, int64_t* alerts_out) {
                 return GP_ESTATE;
             }
         } else {
+            const size_t nl = round_launches(s);
             for (int64_t k = 0; k < batch; ++k) {
                 const uint32_t r = (uint32_t)(s->rounds_done + k);
-                hipEvent_t e0 = s->timing ? s->ev[2 * k] : nullptr;
-                hipEvent_t e1 = s->timing ? s->ev[2 * k + 1] : nullptr;
-                int rc = launch_round(s, r, e0, e1);
+                int rc = launch_round(s, r, s->timing ? &s->ev[2 * nl * k] : nullptr);
                 if (rc) return rc;
             }
         }
@@ -2060,11 +2062,14 @@ int64_t gp_step(gp_sim* s, int64_t nrounds, int64_t* alerts_out) {
             HIP_TRY(hipEventElapsedTime(&ms, s->ev[0], s->ev[1]));
             s->kernel_ms += ms;
             s->launches += ex;
-        } else if (s->timing) {
+        } else if (s->timing) {  // per round: the sum over its round kernel launches
+            const size_t nl = round_launches(s);
             for (int64_t k = 0; k < ex; ++k) {
-                float ms = 0.f;
-                HIP_TRY(hipEventElapsedTime(&ms, s->ev[2 * k], s->ev[2 * k + 1]));
-                s->kernel_ms += ms;
+                for (size_t h = 0; h < nl; ++h) {
+                    float ms = 0.f;
+                    HIP_TRY(hipEventElapsedTime(&ms, s->ev[2 * (nl * k + h)], s->ev[2 * (nl * k + h) + 1]));
+                    s->kernel_ms += ms;
+                }
                 ++s->launches;
             }
         }

@@ -91,8 +91,8 @@ def test_bench_gpus_rehearsal_reports_world():
                         str(200**3), "--no-cpu", "--no-traffic"], capture_output=True, text=True, timeout=400,
                        cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
-    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, r.stdout
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout  # one JSON line, nothing else on stdout
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["steps"] == 10
     assert "rehearsal" in out["config"]["transport"] and out["config"]["launcher"].startswith("bench.py")

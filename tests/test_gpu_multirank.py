@@ -89,6 +89,21 @@ def test_virtual_ranks_parity(kernel, n, topo, alg, seed, rounds, chk, ranks, mo
     sim.close()
 
 
+def test_region_rounds_kernel_timing(monkeypatch):
+    """Kernel timing with the round kernel run region by region: one entry per round, the sum
+    of its region launches (events around each launch; the packs between them excluded)."""
+    monkeypatch.setenv("GP_RREGIONS", "1")
+    monkeypatch.setenv("GP_WALK", "3")
+    sim = Sim(64000, "Imp3D", "push-sum", seed=5, virtual_ranks=2, experimental=True, kernel_timing=True)
+    assert sim._L.gp_debug_round_regions(sim._h) > 1
+    sim.step(20)
+    sim.kernel_stats(reset=True)
+    assert len(sim.step(30)) == 30
+    ms, n, name = sim.kernel_stats()
+    assert n == 30 and ms > 0 and "tile" in name
+    sim.close()
+
+
 @pytest.mark.parametrize("topo", ["Imp3D", "full"])
 def test_virtual_ranks_converge_like_single(topo):
     """Whole runs to convergence: same round count and alert sequence for 1, 2, 4, 8 ranks."""
