@@ -173,6 +173,10 @@ struct gp_sim {
     std::vector<uint32_t> list_nw;
     hipStream_t xstream = nullptr;
     hipEvent_t ev_send[XMAXH] = {}, ev_xfer[XMAXH] = {};
+    // region rounds (launch_round_regions): the packs' stream -- region h's pack runs beside the
+    // round kernel's launch h + 1 -- and the events that release it
+    hipStream_t pstream = nullptr;
+    hipEvent_t ev_kern[XMAXH] = {};
     BlockPlan bplan{};  // KERNEL_BLOCK
 };
 
@@ -414,7 +418,7 @@ int setup_halo(gp_sim* s) {
 // transfer) or expand (into the halo planes, after it).  Lower side: the first plane's senders
 // toward x - 1 (direction 0) go down; the lower halo takes the neighbour's senders toward x + 1
 // (direction 1).  The upper side the other way round.
-int halo_pack_expand(gp_sim* s, int b, bool pack) {
+int halo_pack_expand(gp_sim* s, int b, bool pack, hipStream_t st) {
     const uint32_t H = s->halo;
     for (Slab& sl : s->slab) {
         DevState& S = sl.S;
@@ -429,12 +433,15 @@ int halo_pack_expand(gp_sim* s, int b, bool pack) {
             h.n = H;
             h.dir = pack ? (k == 0 ? 0u : 1u) : (k == 0 ? 1u : 0u);
             h.overflow = sl.overflow ? sl.overflow : &S.ctl->overflow;
-            HIP_TRY(pack ? launch_halo_pack(h, s->stream) : launch_halo_expand(h, s->stream));
+            HIP_TRY(pack ? launch_halo_pack(h, st) : launch_halo_expand(h, st));
         }
     }
     return GP_OK;
 }
 
+#ifndef GP_PACK_STREAM
+#define GP_PACK_STREAM 0  // region rounds: packs on their own stream (s->pstream)
+#endif
 constexpr int XREGIONS = 4;  // Imp3D push-sum exchange regions (see exchange_regions)
 constexpr uint32_t RREG_MIN_NODES = 1u << 24;  // region rounds from this slab size on (round_regions)
 
@@ -1038,6 +1045,14 @@ int setup_exchange(gp_sim* s) {
     }
     if (NH > 1) {  // the second stream and the events that order it with the compute stream
         HIP_TRY(hipStreamCreateWithFlags(&s->xstream, hipStreamNonBlocking));
+        bool pk = s->slab[0].S.rregions > 1 && GP_PACK_STREAM;
+#ifdef GP_EXPERIMENTS
+        if (const char* e = std::getenv("GP_PSTREAM")) pk = s->slab[0].S.rregions > 1 && e[0] == '1';
+#endif
+        if (pk) {
+            HIP_TRY(hipStreamCreateWithFlags(&s->pstream, hipStreamNonBlocking));
+            for (int h = 0; h < NH; ++h) HIP_TRY(hipEventCreateWithFlags(&s->ev_kern[h], hipEventDisableTiming));
+        }
         for (int h = 0; h < NH; ++h) {
             HIP_TRY(hipEventCreateWithFlags(&s->ev_send[h], hipEventDisableTiming));
             HIP_TRY(hipEventCreateWithFlags(&s->ev_xfer[h], hipEventDisableTiming));
@@ -1237,12 +1252,13 @@ struct XchgCtx {
 };
 
 // The halo planes of round rn: compacted (s, w) packed; in-process ranks copy them here.
-int exchange_open(gp_sim* s, uint32_t rn) {
+// cs: the stream of the packs (the compute stream, or s->pstream in region rounds).
+int exchange_open(gp_sim* s, uint32_t rn, hipStream_t cs) {
     const XchgCtx x(s, rn);
     const int W = x.W, b = x.b;
     const size_t H = x.H, HS = x.HS;
     int rc;
-    if (x.push && HS && (rc = halo_pack_expand(s, b, true))) return rc;
+    if (x.push && HS && (rc = halo_pack_expand(s, b, true, cs))) return rc;
     if (s->mode == MODE_VIRTUAL) {  // halo planes by device copies (round kernel -> next round kernel)
         for (int r = 0; r + 1 < W; ++r) {
             DevState& A = s->slab[r].S;  // lower slab
@@ -1250,19 +1266,19 @@ int exchange_open(gp_sim* s, uint32_t rn) {
             const uint32_t edge = B.lo;  // A's hi
             // A's last H ids -> B's lower halo; B's first H ids -> A's upper halo
             HIP_TRY(hipMemcpyAsync(B.nb[b] + (edge - H - B.base), A.nb[b] + (edge - H - A.base), H,
-                                   hipMemcpyDeviceToDevice, s->stream));
+                                   hipMemcpyDeviceToDevice, cs));
             HIP_TRY(hipMemcpyAsync(A.nb[b] + (edge - A.base), B.nb[b] + (edge - B.base), H, hipMemcpyDeviceToDevice,
-                                   s->stream));
+                                   cs));
             if (x.push && HS) {
                 HIP_TRY(hipMemcpyAsync(s->slab[r + 1].hrecv[0], s->slab[r].hsend[1], HS * 16, hipMemcpyDeviceToDevice,
-                                       s->stream));
+                                       cs));
                 HIP_TRY(hipMemcpyAsync(s->slab[r].hrecv[1], s->slab[r + 1].hsend[0], HS * 16, hipMemcpyDeviceToDevice,
-                                       s->stream));
+                                       cs));
             } else if (x.push) {
                 HIP_TRY(hipMemcpyAsync(B.sw[b] + (edge - H - B.base), A.sw[b] + (edge - H - A.base), H * 16,
-                                       hipMemcpyDeviceToDevice, s->stream));
+                                       hipMemcpyDeviceToDevice, cs));
                 HIP_TRY(hipMemcpyAsync(A.sw[b] + (edge - A.base), B.sw[b] + (edge - B.base), H * 16,
-                                       hipMemcpyDeviceToDevice, s->stream));
+                                       hipMemcpyDeviceToDevice, cs));
             }
         }
     }
@@ -1271,7 +1287,7 @@ int exchange_open(gp_sim* s, uint32_t rn) {
 
 // Region h of round rn's random-edge exchange: packed on the compute stream, then handed to the
 // exchange stream (one RCCL group per region; the halo planes travel in region hg's group).
-int exchange_region(gp_sim* s, uint32_t rn, int h, int hg) {
+int exchange_region(gp_sim* s, uint32_t rn, int h, int hg, hipStream_t cs) {
     const XchgCtx x(s, rn);
     const int W = x.W, b = x.b, NH = x.NH;
     const bool push = x.push, imp = x.imp, lists = x.lists, bits = x.bits;
@@ -1282,7 +1298,7 @@ int exchange_region(gp_sim* s, uint32_t rn, int h, int hg) {
         for (Slab& sl : s->slab) {
             DevState& S = sl.S;
             if (lists) {  // header words + compacted messages of region h (k_list_pack)
-                HIP_TRY(hipMemsetAsync(sl.xcnt + (size_t)h * W, 0, sizeof(uint32_t) * W, s->stream));
+                HIP_TRY(hipMemsetAsync(sl.xcnt + (size_t)h * W, 0, sizeof(uint32_t) * W, cs));
                 ListPackArgs la{};
                 la.nbn = S.nb[b];
                 la.swn = S.sw[b];
@@ -1306,7 +1322,7 @@ int exchange_region(gp_sim* s, uint32_t rn, int h, int hg) {
                     la.peer[d].vbase = sl.vbase[i];
                 }
                 la.overflow = sl.overflow;
-                HIP_TRY(launch_list_pack(la, s->stream));
+                HIP_TRY(launch_list_pack(la, cs));
                 continue;
             }
             ZeroArgs z{};
@@ -1333,12 +1349,12 @@ int exchange_region(gp_sim* s, uint32_t rn, int h, int hg) {
             }
             z.n = W;
             pa.overflow = sl.overflow;
-            HIP_TRY(launch_zero_counts(z, s->stream));
-            HIP_TRY(launch_pack(pa, s->grid, s->stream));
+            HIP_TRY(launch_zero_counts(z, cs));
+            HIP_TRY(launch_pack(pa, s->grid, cs));
         }
     }
     if (xs != s->stream) {
-        HIP_TRY(hipEventRecord(s->ev_send[h], s->stream));
+        HIP_TRY(hipEventRecord(s->ev_send[h], cs));
         HIP_TRY(hipStreamWaitEvent(xs, s->ev_send[h], 0));
     }
     if (s->mode == MODE_VIRTUAL) {
@@ -1468,7 +1484,7 @@ int exchange_close(gp_sim* s, uint32_t rn) {
     } else if (xs != s->stream) {
         HIP_TRY(hipStreamWaitEvent(s->stream, s->ev_xfer[NH - 1], 0));
     }
-    if (push && HS && (rc = halo_pack_expand(s, b, false))) return rc;
+    if (push && HS && (rc = halo_pack_expand(s, b, false, s->stream))) return rc;
     return GP_OK;
 }
 
@@ -1476,9 +1492,9 @@ int exchange(gp_sim* s, uint32_t rn) {
     if (s->world == 1 || s->cfg.topology == GP_FULL) return GP_OK;  // full: the exchange is inside the round
     const XchgCtx x(s, rn);
     int rc;
-    if ((rc = exchange_open(s, rn))) return rc;
+    if ((rc = exchange_open(s, rn, s->stream))) return rc;
     for (int h = 0; h < x.NH; ++h)
-        if ((rc = exchange_region(s, rn, h, 0))) return rc;
+        if ((rc = exchange_region(s, rn, h, 0, s->stream))) return rc;
     return exchange_close(s, rn);
 }
 
@@ -1516,8 +1532,14 @@ int launch_round_regions(gp_sim* s, uint32_t r, hipEvent_t* ev) {
         if (ev) HIP_TRY(hipEventRecord(ev[2 * h], s->stream));
         for (Slab& sl : s->slab) HIP_TRY(launch_round_tile_region(sl.S, r, h, s->grid, s->stream));
         if (ev) HIP_TRY(hipEventRecord(ev[2 * h + 1], s->stream));
-        if (h + 1 == NR && (rc = exchange_open(s, rn))) return rc;
-        if ((rc = exchange_region(s, rn, (int)h, (int)NR - 1))) return rc;
+        hipStream_t cs = s->stream;
+        if (s->pstream) {  // region h's pack beside launch h + 1
+            HIP_TRY(hipEventRecord(s->ev_kern[h], s->stream));
+            HIP_TRY(hipStreamWaitEvent(s->pstream, s->ev_kern[h], 0));
+            cs = s->pstream;
+        }
+        if (h + 1 == NR && (rc = exchange_open(s, rn, cs))) return rc;
+        if ((rc = exchange_region(s, rn, (int)h, (int)NR - 1, cs))) return rc;
     }
     if ((rc = exchange_close(s, rn))) return rc;
     return finalize(s, r, rn);
@@ -2282,16 +2304,19 @@ void gp_destroy(gp_sim* s) {
     (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     if (s->xstream) (void)hipStreamSynchronize(s->xstream);
+    if (s->pstream) (void)hipStreamSynchronize(s->pstream);
     for (auto& e : s->ev) (void)hipEventDestroy(e);
     for (int h = 0; h < XMAXH; ++h) {
         if (s->ev_send[h]) (void)hipEventDestroy(s->ev_send[h]);
         if (s->ev_xfer[h]) (void)hipEventDestroy(s->ev_xfer[h]);
+        if (s->ev_kern[h]) (void)hipEventDestroy(s->ev_kern[h]);
     }
     if (s->comm) (void)ncclCommDestroy(s->comm);
     free_all(s);
     if (s->host_ctl) (void)hipHostFree(s->host_ctl);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     if (s->xstream) (void)hipStreamDestroy(s->xstream);
+    if (s->pstream) (void)hipStreamDestroy(s->pstream);
     delete s;
 }
 
