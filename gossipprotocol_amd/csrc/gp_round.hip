@@ -1310,16 +1310,31 @@ RoundArgs make_round_args(const DevState& S, uint32_t round) {
     return a;
 }
 
-// Region h of NR of a plane-aligned slab: planes [x0 + nx h / NR, x0 + nx (h + 1) / NR), whose
-// tiles (relative to lo / TILE) are [rb[h], rb[h + 1]) -- a tile belongs to the plane it starts
-// in (the slab's first tile to the first plane).  False if the slab is not plane-aligned.
+#ifndef GP_RLAST
+#define GP_RLAST 0  // the last region half the size of the others (region_plane)
+#endif
+// First plane (relative to the slab's) of region h of NR over nx planes: equal regions, or with
+// GP_RLAST the last one half the size of the others (its pack and transfer are the round's
+// exposed tail) -- region h starts at nx 2h / (2 NR - 1).
+uint32_t region_plane(uint32_t nx, int NR, int h) {
+    bool half = GP_RLAST;
+#ifdef GP_EXPERIMENTS
+    if (const char* e = std::getenv("GP_RLAST")) half = e[0] == '1';
+#endif
+    if (h >= NR) return nx;
+    return half && NR > 1 ? (uint32_t)((uint64_t)nx * 2 * h / (2 * NR - 1)) : (uint32_t)((uint64_t)nx * h / NR);
+}
+
+// Region h of NR of a plane-aligned slab: planes [x0 + region_plane(h), x0 + region_plane(h + 1)),
+// whose tiles (relative to lo / TILE) are [rb[h], rb[h + 1]) -- a tile belongs to the plane it
+// starts in (the slab's first tile to the first plane).  False if the slab is not plane-aligned.
 bool region_tiles(uint32_t lo, uint32_t nloc, uint64_t g2, int NR, uint32_t* rb) {
     if (!g2 || nloc % g2 || lo % g2 || NR < 1) return false;
     const uint32_t tb = lo / TILE;
     const uint32_t tend = (uint32_t)(((uint64_t)lo + nloc + TILE - 1) / TILE);
     const uint32_t x0 = (uint32_t)(lo / g2), nx = (uint32_t)(nloc / g2);
     for (int h = 0; h <= NR; ++h) {
-        const uint64_t x = x0 + (uint64_t)nx * h / NR;
+        const uint64_t x = x0 + region_plane(nx, NR, h);
         rb[h] = (x <= x0 ? tb : (uint32_t)std::min<uint64_t>((x * g2 + TILE - 1) / TILE, tend)) - tb;
     }
     return true;
@@ -1342,8 +1357,8 @@ bool build_walk_list(const DevState& S, int NR, std::vector<uint32_t>& list, uin
     };
     list.clear();
     for (int h = 0; h < NR; ++h) {
-        const uint32_t r0 = x0 + (uint32_t)((uint64_t)nx * h / NR);
-        const uint32_t nr = x0 + (uint32_t)((uint64_t)nx * (h + 1) / NR) - r0;
+        const uint32_t r0 = x0 + region_plane(nx, NR, h);
+        const uint32_t nr = x0 + region_plane(nx, NR, h + 1) - r0;
         for (uint32_t c = 0; c < 8; ++c) {
             woff[h][c] = (uint32_t)list.size();
             const uint32_t xa = r0 + (uint32_t)((uint64_t)nr * c / 8);
