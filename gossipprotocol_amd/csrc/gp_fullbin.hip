@@ -571,6 +571,9 @@ __global__ __launch_bounds__(FBR_THREADS, GP_FBR_MINB) void k_fbm_coarse(FullBin
 // sender ids and payloads in receiver order; each receiver's (few) messages are
 // put in ascending sender order (insertion sort of (sender, LDS position)) and
 // folded from LDS -- no gather of the bin's payloads from global memory.
+#ifndef GP_FB_ILP
+#define GP_FB_ILP 2  // receivers of a thread folded in lock step (k_fb_fold), 1: one after the other
+#endif
 #ifndef GP_FBF_THREADS
 #define GP_FBF_THREADS 1024
 #endif
@@ -703,34 +706,12 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
         }
         lds_barrier();
         FB_STAMP(t2);
-#pragma unroll
-        for (int k = 0; k < NPT; ++k) {
-            const uint32_t v = k * FBF_THREADS + threadIdx.x;
-            const uint32_t j = f * TILE + v;
-            const uint32_t p0 = cnt[v], p1 = j < a.nloc ? cnt[v + 1] : p0;
-            // this receiver's messages in ascending sender id (canonical order)
-            for (uint32_t p = p0 + 1; p < p1; ++p) {
-                const uint32_t s = src[p];
-                const uint16_t xi = idx[p];
-                uint32_t q = p;
-                while (q > p0 && src[q - 1] > s) {
-                    src[q] = src[q - 1];
-                    idx[q] = idx[q - 1];
-                    --q;
-                }
-                src[q] = s;
-                idx[q] = xi;
-            }
+        // per receiver after its fold: ratio test, flags, state out (and the fused send's inputs)
+        auto close_receiver = [&](int k, uint32_t p0, uint32_t p1, double acc_s, double acc_w) {
+            const uint32_t j = f * TILE + k * FBF_THREADS + threadIdx.x;
             const uint8_t b = bk[k];
             const double2 sv = svk[k];
             const bool active = (b & B_ACTIVE) != 0;
-            double acc_s = active && P > 1 ? sv.x * 0.5 : sv.x;
-            double acc_w = active && P > 1 ? sv.y * 0.5 : sv.y;
-            for (uint32_t p = p0; p < p1; ++p) {
-                const double2 m = msg[idx[p]];  // already halved by the sender
-                acc_s = acc_s + m.x;
-                acc_w = acc_w + m.y;
-            }
             if (p1 > p0) {
                 uint32_t flags = b;
                 if (!(b & B_CONV)) {
@@ -753,6 +734,58 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
                 nfl[k] = j < a.nloc && P > 1 && (b & B_ACTIVE || p1 > p0) ? 1u : 0u;  // active next round
                 nsw[k] = make_double2(acc_s * 0.5, acc_w * 0.5);
             }
+        };
+        // this receiver's messages in ascending sender id (canonical order): insertion sort
+        auto sort_receiver = [&](uint32_t p0, uint32_t p1) {
+            for (uint32_t p = p0 + 1; p < p1; ++p) {
+                const uint32_t s = src[p];
+                const uint16_t xi = idx[p];
+                uint32_t q = p;
+                while (q > p0 && src[q - 1] > s) {
+                    src[q] = src[q - 1];
+                    idx[q] = idx[q - 1];
+                    --q;
+                }
+                src[q] = s;
+                idx[q] = xi;
+            }
+        };
+        // GP_FB_ILP receivers folded in lock step (one LDS chain each in flight, each receiver's
+        // own order kept); 1: one receiver after the other
+        constexpr int FG = GP_FB_ILP;
+        static_assert(FG >= 1 && NPT % FG == 0, "fold groups");
+#pragma unroll
+        for (int g0 = 0; g0 < NPT; g0 += FG) {
+            uint32_t fp0[FG], fp1[FG];
+            double fs[FG], fw[FG];
+            uint32_t most = 0;
+#pragma unroll
+            for (int i = 0; i < FG; ++i) {
+                const int k = g0 + i;
+                const uint32_t v = k * FBF_THREADS + threadIdx.x;
+                const uint32_t j = f * TILE + v;
+                fp0[i] = cnt[v];
+                fp1[i] = j < a.nloc ? cnt[v + 1] : fp0[i];
+                sort_receiver(fp0[i], fp1[i]);
+                most = max(most, fp1[i] - fp0[i]);
+                const bool active = (bk[k] & B_ACTIVE) != 0;
+                fs[i] = active && P > 1 ? svk[k].x * 0.5 : svk[k].x;
+                fw[i] = active && P > 1 ? svk[k].y * 0.5 : svk[k].y;
+            }
+            for (uint32_t t = 0; t < most; ++t) {
+                uint16_t xi[FG];
+#pragma unroll
+                for (int i = 0; i < FG; ++i) xi[i] = idx[min(fp0[i] + t, (uint32_t)FB_CAP2 - 1u)];
+#pragma unroll
+                for (int i = 0; i < FG; ++i)
+                    if (fp0[i] + t < fp1[i]) {
+                        const double2 m = msg[xi[i]];  // already halved by the sender
+                        fs[i] = fs[i] + m.x;
+                        fw[i] = fw[i] + m.y;
+                    }
+            }
+#pragma unroll
+            for (int i = 0; i < FG; ++i) close_receiver(g0 + i, fp0[i], fp1[i], fs[i], fw[i]);
         }
         lds_barrier();
         for (uint32_t v = threadIdx.x; v < TILE; v += FBF_THREADS) cnt[v] = 0u;
