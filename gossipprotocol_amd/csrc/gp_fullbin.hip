@@ -571,6 +571,9 @@ __global__ __launch_bounds__(FBR_THREADS, GP_FBR_MINB) void k_fbm_coarse(FullBin
 // sender ids and payloads in receiver order; each receiver's (few) messages are
 // put in ascending sender order (insertion sort of (sender, LDS position)) and
 // folded from LDS -- no gather of the bin's payloads from global memory.
+#ifndef GP_FB_SORT_ILP
+#define GP_FB_SORT_ILP 0  // k_fb_fold: the lock-step receivers' insertion sorts in lock step too
+#endif
 #ifndef GP_FB_ILP
 #define GP_FB_ILP 2  // receivers of a thread folded in lock step (k_fb_fold), 1: one after the other
 #endif
@@ -766,12 +769,56 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
                 const uint32_t j = f * TILE + v;
                 fp0[i] = cnt[v];
                 fp1[i] = j < a.nloc ? cnt[v + 1] : fp0[i];
-                sort_receiver(fp0[i], fp1[i]);
+                if (!GP_FB_SORT_ILP) sort_receiver(fp0[i], fp1[i]);
                 most = max(most, fp1[i] - fp0[i]);
                 const bool active = (bk[k] & B_ACTIVE) != 0;
                 fs[i] = active && P > 1 ? svk[k].x * 0.5 : svk[k].x;
                 fw[i] = active && P > 1 ? svk[k].y * 0.5 : svk[k].y;
             }
+#if GP_FB_SORT_ILP
+            // the FG insertion sorts in lock step too (disjoint LDS ranges): element t of each
+            // receiver sinks into its sorted prefix
+            for (uint32_t t = 1; t < most; ++t) {
+                uint32_t sv_[FG], q[FG];
+                uint16_t xv[FG];
+                bool go[FG];
+#pragma unroll
+                for (int i = 0; i < FG; ++i) {
+                    q[i] = fp0[i] + t;
+                    go[i] = q[i] < fp1[i];
+                    const uint32_t qc = min(q[i], (uint32_t)FB_CAP2 - 1u);
+                    sv_[i] = src[qc];
+                    xv[i] = idx[qc];
+                }
+                bool moved[FG];
+#pragma unroll
+                for (int i = 0; i < FG; ++i) moved[i] = false;
+                for (;;) {
+                    bool any = false;
+#pragma unroll
+                    for (int i = 0; i < FG; ++i)
+                        if (go[i]) {
+                            const uint32_t prev = q[i] > fp0[i] ? src[q[i] - 1] : 0u;
+                            if (q[i] > fp0[i] && prev > sv_[i]) {
+                                src[q[i]] = prev;
+                                idx[q[i]] = idx[q[i] - 1];
+                                --q[i];
+                                moved[i] = true;
+                                any = true;
+                            } else {
+                                go[i] = false;
+                            }
+                        }
+                    if (!any) break;
+                }
+#pragma unroll
+                for (int i = 0; i < FG; ++i)
+                    if (moved[i]) {
+                        src[q[i]] = sv_[i];
+                        idx[q[i]] = xv[i];
+                    }
+            }
+#endif
             for (uint32_t t = 0; t < most; ++t) {
                 uint16_t xi[FG];
 #pragma unroll
