@@ -36,7 +36,9 @@ def main(argv=None):
     # torch.distributed.run (WORLD_SIZE / RANK in the environment) -- never launch again
     external = "WORLD_SIZE" in os.environ and not os.environ.get("GOSSIP_LAUNCHED")
     if external and int(os.environ["WORLD_SIZE"]) != a.gpus:
-        print(f"--gpus {a.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}: refusing to run another GPU count",
+        seen = ", ".join(f"{k}={os.environ[k]}" for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK") if k in os.environ)
+        print(f"external launcher detected ({seen}) but --gpus {a.gpus}: pass --gpus "
+              f"{os.environ['WORLD_SIZE']} (or GOSSIP_GPUS) to run as its rank; refusing to run another GPU count",
               file=sys.stderr)
         return 2
     if a.gpus > 1 and not os.environ.get("GOSSIP_LAUNCHED") and not external:
@@ -54,19 +56,23 @@ def main(argv=None):
         # gloo group on its MASTER_ADDR / MASTER_PORT (host side only)
         import torch.distributed as dist
         dist.init_process_group("gloo", rank=rank, world_size=a.gpus)
-    try:
-        sim = Simulation(a.num_nodes, a.topology, a.algorithm, seed=a.seed, max_rounds=a.max_rounds,
-                         device=device, rank=rank, world=a.gpus, dist=dist,
-                         rendezvous=os.environ.get("GOSSIP_RDV"))
-    except L.GossipError as e:
-        print(f"[rank {rank}/{a.gpus}] {e}", file=sys.stderr)
-        return 2 if e.code == -1 else 1
-    if rank == 0:
-        print("Gossip Starts" if a.algorithm == "gossip" else "Push Sum Starts", flush=True)
-    res = sim.run()
-    sim.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    try:  # the gloo group is torn down on every exit path
+        try:
+            sim = Simulation(a.num_nodes, a.topology, a.algorithm, seed=a.seed, max_rounds=a.max_rounds,
+                             device=device, rank=rank, world=a.gpus, dist=dist,
+                             rendezvous=os.environ.get("GOSSIP_RDV"))
+        except L.GossipError as e:
+            print(f"[rank {rank}/{a.gpus}] {e}", file=sys.stderr)
+            return 2 if e.code == -1 else 1
+        if rank == 0:
+            print("Gossip Starts" if a.algorithm == "gossip" else "Push Sum Starts", flush=True)
+        try:
+            res = sim.run()
+        finally:
+            sim.close()
+    finally:
+        if dist is not None:
+            dist.destroy_process_group()
     if res.status == L.GP_STATUS_CONVERGED:
         if rank == 0:
             print("Convergence Time: %f ms" % res.elapsed_ms, flush=True)

@@ -42,6 +42,20 @@
 #include "gp_internal.hpp"
 #include "gp_full.hpp"
 #include "gp_fullbin.hpp"
+
+namespace {
+// The experiments build (-DGP_EXPERIMENTS, libgossip_hip_exp.so) reads the GP_* environment
+// overrides the kernel-variant tests use; the product library reads none (nullptr: every
+// override below folds away, its name included -- tests/test_abi.py checks the strings).
+inline const char* exp_env(const char* name) {
+#ifdef GP_EXPERIMENTS
+    return std::getenv(name);
+#else
+    (void)name;
+    return nullptr;
+#endif
+}
+}  // namespace
 #include "gp_xchg.hpp"
 
 using namespace gp;
@@ -168,6 +182,7 @@ struct gp_sim {
     // in two halves of each rank's senders on xstream, overlapped with the send / coarse passes)
     int xhalves = 1;
     size_t halo_slots = 0;  // push-sum halo planes travel compacted (setup_halo): slots per buffer, else 0
+    uint32_t halo_cap = 0;  // ... slots per 1024-node chunk (halo_chunk_cap)
     // Imp3D push-sum lists: header words of chunk (h, a -> b) at [(a * xhalves + h) * world + b],
     // every slab's (each rank computes the whole table from the global random edges)
     std::vector<uint32_t> list_nw;
@@ -175,8 +190,6 @@ struct gp_sim {
     hipEvent_t ev_send[XMAXH] = {}, ev_xfer[XMAXH] = {};
     // region rounds (launch_round_regions): the packs' stream -- region h's pack runs beside the
     // round kernel's launch h + 1 -- and the events that release it
-    hipStream_t pstream = nullptr;
-    hipEvent_t ev_kern[XMAXH] = {};
     BlockPlan bplan{};  // KERNEL_BLOCK
 };
 
@@ -353,9 +366,7 @@ int alloc_slab(gp_sim* s, Slab& sl, int r) {
     if (S.topo == FULL && S.alg == PUSHSUM) {  // LDS-binned message staging of this rank's receivers (gp_fullbin.hip)
         // one rank: the fold of round r bins round r+1's messages (k_fb_fold<true>)
         bool fused = s->world == 1;
-#ifdef GP_EXPERIMENTS
-        if (const char* e = std::getenv("GP_FB_FUSED")) fused = fused && e[0] == '1';  // A/B: three passes
-#endif
+        if (const char* e = exp_env("GP_FB_FUSED")) fused = fused && e[0] == '1';  // A/B: three passes
         const FullBinPlan fp = full_bin_plan(S.nloc, fused);
         S.fb_s1 = fp.s1;
         S.fb_nb1 = fp.nb1;
@@ -373,9 +384,7 @@ int alloc_slab(gp_sim* s, Slab& sl, int r) {
         // byte counters, four per word (C3: 0.632 -> 0.600 ms per round, reads 16.5 -> 11.7 and
         // writes 11.2 -> 9.8 B/node; profiles/r04/c3_byte_counters.txt)
         S.rq8 = 1;
-#ifdef GP_EXPERIMENTS
-        if (const char* e = std::getenv("GP_RQ8")) S.rq8 = e[0] == '1' ? 1u : 0u;
-#endif
+        if (const char* e = exp_env("GP_RQ8")) S.rq8 = e[0] == '1' ? 1u : 0u;
         for (int q = 0; q < 2; ++q) {
             if ((rc = dev_alloc_t(s, &S.rq[q], (size_t)S.nloc + 64))) return rc;
             HIP_TRY(hipMemsetAsync(S.rq[q], 0, sizeof(uint32_t) * ((size_t)S.nloc + 64), s->stream));
@@ -392,16 +401,13 @@ int alloc_slab(gp_sim* s, Slab& sl, int r) {
 
 // Push-sum on a 3D / Imp3D lattice over several ranks: the halo planes' (s, w) travel compacted
 // (only the senders toward the neighbour, HaloArgs in gp_xchg.hpp): C5 at W = 8, 16 MB -> 3.9 MB
-// per direction and round.  (GP_HALO_FULL=1, experiments: the whole plane, as before round 5.)
+// per direction and round.
 int setup_halo(gp_sim* s) {
     s->halo_slots = 0;
     const bool lattice = s->cfg.topology == GP_3D || s->cfg.topology == GP_IMP3D;
     if (!lattice || s->cfg.algorithm != GP_PUSHSUM || s->world < 2 || s->halo < HALO_CHUNK) return GP_OK;
-#ifdef GP_EXPERIMENTS
-    if (const char* e = std::getenv("GP_HALO_FULL"))
-        if (e[0] == '1') return GP_OK;
-#endif
-    s->halo_slots = halo_buf_slots(s->halo);
+    s->halo_cap = halo_chunk_cap((uint32_t)s->g, s->cfg.topology == GP_IMP3D);
+    s->halo_slots = halo_buf_slots(s->halo, s->halo_cap);
     int rc;
     for (Slab& sl : s->slab) {
         for (int k = 0; k < 2; ++k) {
@@ -431,6 +437,7 @@ int halo_pack_expand(gp_sim* s, int b, bool pack, hipStream_t st) {
             h.sw = S.sw[b] + (at - S.base);
             h.buf = pack ? sl.hsend[k] : sl.hrecv[k];
             h.n = H;
+            h.cap = s->halo_cap;
             h.dir = pack ? (k == 0 ? 0u : 1u) : (k == 0 ? 1u : 0u);
             h.overflow = sl.overflow ? sl.overflow : &S.ctl->overflow;
             HIP_TRY(pack ? launch_halo_pack(h, st) : launch_halo_expand(h, st));
@@ -439,9 +446,6 @@ int halo_pack_expand(gp_sim* s, int b, bool pack, hipStream_t st) {
     return GP_OK;
 }
 
-#ifndef GP_PACK_STREAM
-#define GP_PACK_STREAM 0  // region rounds: packs on their own stream (s->pstream)
-#endif
 constexpr int XREGIONS = 4;  // Imp3D push-sum exchange regions (see exchange_regions)
 constexpr uint32_t RREG_MIN_NODES = 1u << 24;  // region rounds from this slab size on (round_regions)
 
@@ -460,11 +464,6 @@ int exchange_regions(const gp_sim* s) {
         std::min(s->bounds[1] - s->bounds[0], s->bounds[2] - s->bounds[1]) >= RREG_MIN_NODES)
         NH = 8;
     static_assert(XMAXH >= 8 && RREG_MAX >= 8, "eight regions for two ranks");
-#ifdef GP_EXPERIMENTS
-    if (const char* e = std::getenv("GP_XHALVES")) NH = std::max(1, std::min(2, std::atoi(e)));
-    if (const char* e = std::getenv("GP_XREGIONS"))
-        if (push && s->cfg.topology == GP_IMP3D) NH = std::max(1, std::min(XMAXH, std::atoi(e)));
-#endif
     return NH;
 }
 
@@ -484,9 +483,7 @@ uint32_t round_regions(const gp_sim* s, int kernel, uint32_t walk) {
     int on = 1;
     for (int w = 0; w < s->world; ++w)
         if (s->bounds[w + 1] - s->bounds[w] < RREG_MIN_NODES) on = 0;
-#ifdef GP_EXPERIMENTS
-    if (const char* e = std::getenv("GP_RREGIONS")) on = std::atoi(e);
-#endif
+    if (const char* e = exp_env("GP_RREGIONS")) on = std::atoi(e);
     const int NH = exchange_regions(s);
     if (!on || NH < 2 || NH > RREG_MAX) return 1;
     uint32_t rb[RREG_MAX + 1];
@@ -807,9 +804,7 @@ int build_imp3d(gp_sim* s) {
                                    hipMemcpyDeviceToDevice, s->stream));
         S.in_srcd = nullptr;
         bool pack = true;
-#ifdef GP_EXPERIMENTS
-        if (const char* np = std::getenv("GP_NO_PACK")) pack = np[0] != '1';  // force the unpacked (P > 2^30) path
-#endif
+        if (const char* np = exp_env("GP_NO_PACK")) pack = np[0] != '1';  // force the unpacked (P > 2^30) path
         if (S.alg == PUSHSUM && S.kernel == KERNEL_TILE && s->P <= (1ll << 30) && s->g >= 2 && pack) {
             if ((rc = dev_alloc_t(s, &S.in_srcd, (size_t)ne + 4))) return rc;
             if (ne) HIP_TRY(launch_pack_src_deg(S.in_src, S.in_srcd, ne, S.G, s->grid, s->stream));
@@ -818,9 +813,7 @@ int build_imp3d(gp_sim* s) {
         if (S.alg == PUSHSUM && S.kernel == KERNEL_TILE) {
             if ((rc = dev_alloc_t(s, &S.ind4, ind4_bytes_for(S.lo, S.nloc)))) return rc;
             uint32_t wide_at = 15;  // in-degree >= 15: the tile reads in_off (gp_round.hip)
-#ifdef GP_EXPERIMENTS
-            if (const char* e = std::getenv("GP_IND4_WIDE")) wide_at = (uint32_t)std::max(1, std::atoi(e));
-#endif
+            if (const char* e = exp_env("GP_IND4_WIDE")) wide_at = (uint32_t)std::max(1, std::atoi(e));
             HIP_TRY(launch_pack_ind4(S, wide_at, s->grid, s->stream));
         }
         if (W > 1 && !col_gossip_counts(S)) {  // (the gossip column kernel's bitmaps: build_bits)
@@ -930,12 +923,10 @@ int setup_exchange(gp_sim* s) {
             }
         }
     }
-#ifdef GP_EXPERIMENTS
-    if (const char* e = std::getenv("GP_XCAP")) {  // tests: force tiny buffers (overflow handling)
+    if (const char* e = exp_env("GP_XCAP")) {  // tests: force tiny buffers (overflow handling)
         const uint32_t cap = (uint32_t)std::max(1, std::atoi(e));
         for (auto& c : caps) c = std::min(c, cap);
     }
-#endif
     if (s->mode == MODE_RCCL && !full) {
         // every rank learns the capacities of the buffers it will receive (per region)
         uint32_t* d = nullptr;
@@ -1045,14 +1036,6 @@ int setup_exchange(gp_sim* s) {
     }
     if (NH > 1) {  // the second stream and the events that order it with the compute stream
         HIP_TRY(hipStreamCreateWithFlags(&s->xstream, hipStreamNonBlocking));
-        bool pk = s->slab[0].S.rregions > 1 && GP_PACK_STREAM;
-#ifdef GP_EXPERIMENTS
-        if (const char* e = std::getenv("GP_PSTREAM")) pk = s->slab[0].S.rregions > 1 && e[0] == '1';
-#endif
-        if (pk) {
-            HIP_TRY(hipStreamCreateWithFlags(&s->pstream, hipStreamNonBlocking));
-            for (int h = 0; h < NH; ++h) HIP_TRY(hipEventCreateWithFlags(&s->ev_kern[h], hipEventDisableTiming));
-        }
         for (int h = 0; h < NH; ++h) {
             HIP_TRY(hipEventCreateWithFlags(&s->ev_send[h], hipEventDisableTiming));
             HIP_TRY(hipEventCreateWithFlags(&s->ev_xfer[h], hipEventDisableTiming));
@@ -1252,7 +1235,7 @@ struct XchgCtx {
 };
 
 // The halo planes of round rn: compacted (s, w) packed; in-process ranks copy them here.
-// cs: the stream of the packs (the compute stream, or s->pstream in region rounds).
+// cs: the stream of the packs.
 int exchange_open(gp_sim* s, uint32_t rn, hipStream_t cs) {
     const XchgCtx x(s, rn);
     const int W = x.W, b = x.b;
@@ -1532,12 +1515,9 @@ int launch_round_regions(gp_sim* s, uint32_t r, hipEvent_t* ev) {
         if (ev) HIP_TRY(hipEventRecord(ev[2 * h], s->stream));
         for (Slab& sl : s->slab) HIP_TRY(launch_round_tile_region(sl.S, r, h, s->grid, s->stream));
         if (ev) HIP_TRY(hipEventRecord(ev[2 * h + 1], s->stream));
-        hipStream_t cs = s->stream;
-        if (s->pstream) {  // region h's pack beside launch h + 1
-            HIP_TRY(hipEventRecord(s->ev_kern[h], s->stream));
-            HIP_TRY(hipStreamWaitEvent(s->pstream, s->ev_kern[h], 0));
-            cs = s->pstream;
-        }
+        // (region h's pack on a stream of its own, beside launch h + 1: 2-5 % slower,
+        // profiles/r05/rejected/pack_stream.txt)
+        const hipStream_t cs = s->stream;
         if (h + 1 == NR && (rc = exchange_open(s, rn, cs))) return rc;
         if ((rc = exchange_region(s, rn, (int)h, (int)NR - 1, cs))) return rc;
     }
@@ -1601,8 +1581,8 @@ double alg_bytes(const gp_sim* s) {
     return 4.0 + 8.0 + 8.0 + 8.0;  // send: c + atomic RMW; recv: inc r+w, c r+w
 }
 
-// Kernel variant and grid for this run (measured defaults, GP_KERNEL / GP_GRID /
-// GP_XSEGS / GP_WALK override for experiments).
+// Kernel variant and grid for this run (measured defaults; GP_KERNEL / GP_XSEGS / GP_WALK /
+// GP_WX / GP_WIDE override them in the experiments build).
 void choose_kernel(gp_sim* s, int64_t nloc_max, int& kernel, uint32_t& col_xsegs, uint32_t& walk, uint32_t& wx,
                    uint32_t& wide) {
     hipDeviceProp_t prop;
@@ -1627,13 +1607,11 @@ void choose_kernel(gp_sim* s, int64_t nloc_max, int& kernel, uint32_t& col_xsegs
                           block_plan((uint32_t)g, prop.multiProcessorCount, bp) &&
                           block_plan_resident(bp, prop.multiProcessorCount);
     if (block_ok) kernel = KERNEL_BLOCK;
-#ifdef GP_EXPERIMENTS
-    if (const char* e = std::getenv("GP_KERNEL")) {
+    if (const char* e = exp_env("GP_KERNEL")) {
         if (!std::strcmp(e, "tile")) kernel = KERNEL_TILE;
         else if (!std::strcmp(e, "col") && lattice && !push) kernel = KERNEL_COL;
         else if (!std::strcmp(e, "block") && block_ok) kernel = KERNEL_BLOCK;
     }
-#endif
     s->bplan = bp;
     col_xsegs = 1;
     if (cfg->topology != GP_FULL && kernel == KERNEL_COL) {
@@ -1649,10 +1627,7 @@ void choose_kernel(gp_sim* s, int64_t nloc_max, int& kernel, uint32_t& col_xsegs
     }
     if (kernel == KERNEL_TILE)  // 1024-node tiles (+1: a slab may start mid-tile), a multiple of the 8 XCDs
         blocks = ((nloc_max + 1023) / 1024 + 1 + 7) / 8 * 8;
-#ifdef GP_EXPERIMENTS
-    if (const char* e = std::getenv("GP_GRID")) cap = std::max<int64_t>(1, std::atoll(e));
-    if (const char* e = std::getenv("GP_XSEGS")) col_xsegs = (uint32_t)std::max(1, std::atoi(e));
-#endif
+    if (const char* e = exp_env("GP_XSEGS")) col_xsegs = (uint32_t)std::max(1, std::atoi(e));
     s->grid = (int)std::max<int64_t>(1, std::min(kernel == KERNEL_COL ? cap : blocks, cap));
     // tile walk: x-windows of 8 planes once every XCD gets a few windows (measured,
     // profiles/r01: 18.2 -> 17.2 ms/round at P = 1e9), else XCD-contiguous eighths
@@ -1665,10 +1640,8 @@ void choose_kernel(gp_sim* s, int64_t nloc_max, int& kernel, uint32_t& col_xsegs
     // 13.34-13.36 / 13.17-13.28 / 13.17-13.22 / 13.22-13.25 / 13.15-13.17 ms/round
     // (profiles/r04/walk_window_nt.txt)
     wx = walk == 3 ? 16 : 8;
-#ifdef GP_EXPERIMENTS
-    if (const char* e = std::getenv("GP_WALK")) walk = (uint32_t)std::atoi(e);
-    if (const char* e = std::getenv("GP_WX")) wx = (uint32_t)std::max(1, std::atoi(e));
-#endif
+    if (const char* e = exp_env("GP_WALK")) walk = (uint32_t)std::atoi(e);
+    if (const char* e = exp_env("GP_WX")) wx = (uint32_t)std::max(1, std::atoi(e));
     // size class of the tiled kernels: line / 3D push-sum on a slab with at most two tiles per
     // resident block of the 4-nodes-per-thread kernel (~2500 tiles, P <~ 2.6e6 per slab) runs the
     // 1024-thread, one-node-per-thread build (gp_round_wide.hip): its node phase is one memory
@@ -1682,9 +1655,7 @@ void choose_kernel(gp_sim* s, int64_t nloc_max, int& kernel, uint32_t& col_xsegs
         const int64_t tiles = (nloc_max + 1023) / 1024 + 1;
         const int64_t res4 = ps_tile_resident_blocks(topo, s->world > 1 && topo == IMP3D, s->device);
         wide = res4 > 0 && tiles <= 2 * res4 ? 1u : 0u;
-#ifdef GP_EXPERIMENTS
-        if (const char* e = std::getenv("GP_WIDE")) wide = e[0] == '1' ? 1u : 0u;
-#endif
+        if (const char* e = exp_env("GP_WIDE")) wide = e[0] == '1' ? 1u : 0u;
     }
     if (walk == 3) {
         const int topo = cfg->topology == GP_LINE ? LINE : cfg->topology == GP_3D ? GRID3D : IMP3D;
@@ -1734,10 +1705,8 @@ int build_sim(gp_sim* s) {
                 return rc;
             HIP_TRY(block_kernel_setup(s->bplan));
         }
-#ifdef GP_EXPERIMENTS
-        if (const char* e = std::getenv("GP_FUSE")) sl.S.fuse_finalize = sl.S.fuse_finalize ? (uint32_t)(e[0] - '0') : 0u;
-        if (const char* e = std::getenv("GP_STAGE_CAP")) sl.S.tile_stage_cap = (uint32_t)std::max(0, std::atoi(e));
-#endif
+        if (const char* e = exp_env("GP_FUSE")) sl.S.fuse_finalize = sl.S.fuse_finalize ? (uint32_t)(e[0] - '0') : 0u;
+        if (const char* e = exp_env("GP_STAGE_CAP")) sl.S.tile_stage_cap = (uint32_t)std::max(0, std::atoi(e));
         if ((rc = alloc_slab(s, sl, sl.rank))) return rc;
         sl.S.rregions = rreg;
         if (sl.S.tile_walk == 3) {  // the tile list of the per-XCD queues
@@ -1991,11 +1960,9 @@ int gp_create_rank(const gp_config* cfg, int32_t rank, int32_t world, const uint
         return GP_EINVAL;
     }
     bool force = false;
-#ifdef GP_EXPERIMENTS
-    // GP_FORCE_RCCL=1: a one-rank RCCL communicator (test of the RCCL transport
+    // GP_FORCE_RCCL=1 (experiments): a one-rank RCCL communicator (test of the RCCL transport
     // on a single GPU: init, bookkeeping all-reduce, teardown)
-    if (const char* e = std::getenv("GP_FORCE_RCCL")) force = e[0] == '1';
-#endif
+    if (const char* e = exp_env("GP_FORCE_RCCL")) force = e[0] == '1';
     if (world == 1 && !force) return create_common(cfg, MODE_SINGLE, 1, 0, nullptr, out);
     if (!unique_id) {
         set_err("gp_create_rank: null unique id");
@@ -2099,8 +2066,7 @@ int64_t gp_step(gp_sim* s, int64_t nrounds, int64_t* alerts_out) {
         s->alerts_total = cum;
         s->done = hc.done != 0;
         executed += ex;
-#ifdef GP_EXPERIMENTS
-        if (s->mode != MODE_RCCL && std::getenv("GP_CHECK_CLOSE")) {  // tests: recount the alerts from the state
+        if (s->mode != MODE_RCCL && exp_env("GP_CHECK_CLOSE")) {  // tests: recount the alerts from the state
             Scratch tmp;
             unsigned long long* d = nullptr;
             HIP_TRY(tmp.alloc(&d, 1));
@@ -2120,7 +2086,6 @@ int64_t gp_step(gp_sim* s, int64_t nrounds, int64_t* alerts_out) {
                 return GP_ESTATE;
             }
         }
-#endif
     }
     return executed;
 }
@@ -2304,19 +2269,16 @@ void gp_destroy(gp_sim* s) {
     (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     if (s->xstream) (void)hipStreamSynchronize(s->xstream);
-    if (s->pstream) (void)hipStreamSynchronize(s->pstream);
     for (auto& e : s->ev) (void)hipEventDestroy(e);
     for (int h = 0; h < XMAXH; ++h) {
         if (s->ev_send[h]) (void)hipEventDestroy(s->ev_send[h]);
         if (s->ev_xfer[h]) (void)hipEventDestroy(s->ev_xfer[h]);
-        if (s->ev_kern[h]) (void)hipEventDestroy(s->ev_kern[h]);
     }
     if (s->comm) (void)ncclCommDestroy(s->comm);
     free_all(s);
     if (s->host_ctl) (void)hipHostFree(s->host_ctl);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     if (s->xstream) (void)hipStreamDestroy(s->xstream);
-    if (s->pstream) (void)hipStreamDestroy(s->pstream);
     delete s;
 }
 

@@ -35,9 +35,6 @@ namespace gp {
 
 namespace {
 
-#ifndef GP_BK_ABL
-#define GP_BK_ABL 0  // experiments (wrong results): skip the node work, time the faces and barriers alone
-#endif
 constexpr int BK_THREADS = 1024;
 constexpr int BK_NPT = 5;  // nodes per thread: boxes of at most 5120 nodes
 
@@ -292,7 +289,7 @@ __global__ __launch_bounds__(BK_THREADS) void k_ps_block(BlockArgs a) {
 #pragma unroll 1
         for (int q = 0; q < BK_NPT; ++q) {
             const uint32_t v = q * BK_THREADS + threadIdx.x;
-            if (v >= V || GP_BK_ABL) break;  // (GP_BK_ABL: timing only, no node work)
+            if (v >= V) break;
             double2 res;
             node(v, r, res, alerts, newly);
             if (q == 0) n0 = res;

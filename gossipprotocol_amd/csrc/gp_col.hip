@@ -24,22 +24,12 @@
 #include "gp_wavecommon.hpp"
 
 // gossip column kernel: waves per SIMD (measured 5..7 with the batched step loads,
-// profiles/r02/col_batch/: Imp3D best at 5, 3D at 7); GP_COL_WAVES (experiments)
-// sets one value for both
-#ifndef GP_COL_PRIO
-// wave priority raised (s_setprio 2) while a column step issues its loads, dropped for the
-// step's ALU work (as the push-sum tile kernel, gp_round.hip GP_SETPRIO).  C3, same box,
-// alternated: 0.596-0.603 -> 0.589-0.590 ms/round (profiles/r04/setprio_c3c4.txt)
-#define GP_COL_PRIO 1
-#endif
-#ifndef GP_COL_PRIO_VAL
-#define GP_COL_PRIO_VAL 2
-#endif
-#ifdef GP_COL_WAVES
-#define GP_COL_MINW(TOPO) GP_COL_WAVES
-#else
+// profiles/r02/col_batch/: Imp3D best at 5, 3D at 7)
 #define GP_COL_MINW(TOPO) ((TOPO) == IMP3D ? 5 : 7)
-#endif
+// wave priority raised (s_setprio 2) while a column step issues its loads, dropped for the
+// step's ALU work (as the push-sum tile kernel).  C3, same box, alternated: 0.596-0.603 ->
+// 0.589-0.590 ms/round (profiles/r04/setprio_c3c4.txt)
+constexpr int COL_PRIO = 2;
 
 namespace gp {
 namespace {
@@ -136,7 +126,7 @@ __global__ __launch_bounds__(BULK_THREADS, GP_COL_MINW(TOPO)) void k_gossip_col(
             uint32_t lnn[NR], led[NR], lrc[NR], lrd[NR];
             int32_t cv[NR];
             const bool ledge = (lane == 0 && z > 0) || (lane == 63 && z + 1 < g);
-            if (GP_COL_PRIO) __builtin_amdgcn_s_setprio(GP_COL_PRIO_VAL);
+            __builtin_amdgcn_s_setprio(COL_PRIO);
 #pragma unroll
             for (int k = 0; k < NR; ++k) {
                 const uint32_t jl = pxb + yo[k];  // yo = 0 on invalid lanes: the plane's first node
@@ -157,7 +147,7 @@ __global__ __launch_bounds__(BULK_THREADS, GP_COL_MINW(TOPO)) void k_gossip_col(
             for (int k = 0; k < NR; ++k)
                 asm volatile("" : "+v"(lnn[k]), "+v"(cv[k]), "+v"(led[k]), "+v"(lrc[k]), "+v"(lrd[k]));
             asm volatile("" : "+v"(hym), "+v"(hyp));
-            if (GP_COL_PRIO) __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_s_setprio(0);
             if (!hmv) hym = DIR_NONE;
             if (!hpv) hyp = DIR_NONE;
             // lane - 1's and lane + 1's bytes of plane x (wave_shr:1 / wave_shl:1)

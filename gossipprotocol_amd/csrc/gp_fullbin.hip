@@ -9,7 +9,7 @@
 // (Program.fs:114-123).
 //
 // Per round, three kernels:
-//   A  k_fb_send   ranges of senders (GP_FB_RANGE chunks of FBR_CHUNK, one
+//   A  k_fb_send   ranges of senders (FB_RANGE chunks of FBR_CHUNK, one
 //                  1024-thread block each): target t = U(P-1) mapped past i
 //                  (Philox); sweep 1 counts the range's messages per coarse bin
 //                  (t >> s1) in LDS and reserves one run per (range, bin); sweep
@@ -41,19 +41,8 @@ namespace gp {
 namespace {
 
 constexpr int FB_MAXBINS = 4096;                   // LDS counters of A and B
-#ifndef GP_FB_PRIO
-#define GP_FB_PRIO 0  // experiments: wave priority raised while the fold / split issue their loads and stores
-                      // (C4, same box: 3.17-3.18 vs 3.03-3.17 ms/round without; not adopted,
-                      // profiles/r04/setprio_c3c4.txt)
-#endif
-template <int P>
-__device__ __forceinline__ void fb_prio() {
-    if (GP_FB_PRIO == 1) __builtin_amdgcn_s_setprio(P);
-}
-template <int P>
-__device__ __forceinline__ void fb_prio_fold_loads() {  // GP_FB_PRIO 2: the fold's tile loads only
-    if (GP_FB_PRIO) __builtin_amdgcn_s_setprio(P);
-}
+// (No wave priority here: raised while the fold / split issue their loads and stores it measured
+// 3.17-3.18 against 3.03-3.17 ms/round, C4 same box, profiles/r04/setprio_c3c4.txt.)
 constexpr uint32_t FB_NONE = 0xFFFFu;
 
 
@@ -128,23 +117,14 @@ __device__ uint32_t lds_excl_scan(uint32_t* cnt, uint32_t n, uint32_t* tmp) {
 // No gather anywhere (the previous version gathered payloads in bin order from
 // an input window larger than the XCD's L2), and reservations drop from one per
 // (chunk, bin) to one per (range, bin).
-#ifndef GP_FBR_THREADS
-#define GP_FBR_THREADS 1024
-#endif
-constexpr int FBR_THREADS = GP_FBR_THREADS;
-#ifndef GP_FBR_PER
-#define GP_FBR_PER 4
-#endif
-#ifndef GP_FBR_MINB
-#define GP_FBR_MINB 1  // __launch_bounds__ minimum waves per SIMD (8: two 1024-thread blocks per CU)
-#endif
-constexpr int FBR_PER = GP_FBR_PER;
+// One 1024-thread block per CU (two per CU with spills: 4.40-4.52 against 3.70 ms/round; 512-
+// thread blocks 4.45), ranges of 4 chunks (best of 2 / 4 / 8 / 16; profiles/r02/c4_v2/).
+constexpr int FBR_THREADS = 1024;
+constexpr int FBR_PER = 4;
 constexpr int FBR_CHUNK = FBR_THREADS * FBR_PER;
-#ifndef GP_FB_RANGE
-#define GP_FB_RANGE 4
-#endif
-constexpr uint32_t FBR_ITEM = (uint32_t)GP_FB_RANGE * FBR_CHUNK;  // messages per work item
-static_assert(GP_FB_RANGE % 2 == 0, "sweep 1 takes two chunks at a time");
+constexpr int FB_RANGE = 4;
+constexpr uint32_t FBR_ITEM = (uint32_t)FB_RANGE * FBR_CHUNK;  // messages per work item
+static_assert(FB_RANGE % 2 == 0, "sweep 1 takes two chunks at a time");
 
 struct FbRangeLds {
     double2 pay[FBR_CHUNK];     // the chunk's payloads in bin order
@@ -182,14 +162,12 @@ __device__ __forceinline__ void fbr_emit_to(FbRangeLds& L, uint32_t* cnt, uint32
         base[b] += (b + 1 < nbins ? cnt[b + 1] : total) - cnt[b];
     // fixed trip count: a loop of unknown length would make the compiler wait for
     // every outstanding load (the next chunk's) before entering it
-    fb_prio<2>();
 #pragma unroll
     for (int k = 0; k < FBR_PER; ++k) {
         const uint32_t p = k * FBR_THREADS + threadIdx.x;
         if (p >= total) break;
         store(L.key[p], L.pos[p], L.hdr[p], L.pay[p]);
     }
-    fb_prio<0>();
     lds_barrier();
 }
 
@@ -238,7 +216,7 @@ struct SendIn {
     }
 };
 
-__global__ __launch_bounds__(FBR_THREADS, GP_FBR_MINB) void k_fb_send(FullBinArgs a, uint32_t r) {
+__global__ __launch_bounds__(FBR_THREADS, 1) void k_fb_send(FullBinArgs a, uint32_t r) {
     __shared__ FbRangeLds L;
     if (ld_agent(&a.ctl->done)) return;
     const uint32_t P = a.P;
@@ -257,7 +235,7 @@ __global__ __launch_bounds__(FBR_THREADS, GP_FBR_MINB) void k_fb_send(FullBinArg
     // registers for sweep 2 (16-bit, two per word), so each message's Philox draw
     // is computed once per pass
     constexpr int P2 = 2 * FBR_PER;
-    constexpr int NCH = GP_FB_RANGE;  // chunks per work item
+    constexpr int NCH = FB_RANGE;  // chunks per work item
     uint32_t keys[NCH * FBR_PER / 2];
 #pragma unroll
     for (int it = 0; it < NCH / 2; ++it) {
@@ -326,7 +304,7 @@ struct SplitIn {
     }
 };
 
-__global__ __launch_bounds__(FBR_THREADS, GP_FBR_MINB) void k_fb_split(FullBinArgs a, uint32_t r) {
+__global__ __launch_bounds__(FBR_THREADS, 1) void k_fb_split(FullBinArgs a, uint32_t r) {
     __shared__ FbRangeLds L;
     if (ld_agent(&a.ctl->done)) return;
     const uint32_t per_bin = (a.cap1 + FBR_ITEM - 1) / FBR_ITEM;
@@ -346,7 +324,7 @@ __global__ __launch_bounds__(FBR_THREADS, GP_FBR_MINB) void k_fb_split(FullBinAr
     // sweep 1: fine tile of every message (target recomputed from the sender's
     // draw), two chunks per iteration; the tiles stay in registers for sweep 2
     constexpr int P2 = 2 * FBR_PER;
-    constexpr int NCH = GP_FB_RANGE;
+    constexpr int NCH = FB_RANGE;
     uint32_t keys[NCH * FBR_PER / 2];
 #pragma unroll
     for (int it = 0; it < NCH / 2; ++it) {
@@ -391,9 +369,7 @@ __global__ __launch_bounds__(FBR_THREADS, GP_FBR_MINB) void k_fb_split(FullBinAr
             key[k] = (keys[m / 2] >> (16 * (m & 1))) & 0xFFFFu;
             rank[k] = key[k] != FB_NONE ? atomicAdd(&cnt[key[k]], 1u) : 0u;
         }
-        fb_prio<2>();
         cur.load(a, ibase, c0 + FBR_CHUNK < q1 ? c0 + FBR_CHUNK : c0, q1);
-        fb_prio<0>();
         lds_barrier();  // ranks counted
         fbr_emit(L, cnt, base, nfine, key, rank, node, pay, a.hdr2, a.pay2, a.cap2, f0, a.nb2, a.overflow);
     }
@@ -411,7 +387,7 @@ __device__ __forceinline__ uint32_t owner_of(const uint32_t* bounds, int W, uint
 // into the exchange buffers (slots = sender id, vals = (s/2, w/2); one counter per
 // buffer, one reservation per (range, rank)); rank me's share goes to its own
 // receive buffer.  Receivers recompute targets from the sender's Philox draw.
-__global__ __launch_bounds__(FBR_THREADS, GP_FBR_MINB) void k_fbm_send(FullBinArgs a, uint32_t r) {
+__global__ __launch_bounds__(FBR_THREADS, 1) void k_fbm_send(FullBinArgs a, uint32_t r) {
     __shared__ FbRangeLds L;
     __shared__ uint32_t* o_slots[XMAXW];
     __shared__ double2* o_vals[XMAXW];
@@ -508,7 +484,7 @@ struct CoarseIn {
     }
 };
 
-__global__ __launch_bounds__(FBR_THREADS, GP_FBR_MINB) void k_fbm_coarse(FullBinArgs a, uint32_t r) {
+__global__ __launch_bounds__(FBR_THREADS, 1) void k_fbm_coarse(FullBinArgs a, uint32_t r) {
     __shared__ FbRangeLds L;
     if (ld_agent(&a.ctl->done)) return;
     int p = 0;
@@ -571,16 +547,7 @@ __global__ __launch_bounds__(FBR_THREADS, GP_FBR_MINB) void k_fbm_coarse(FullBin
 // sender ids and payloads in receiver order; each receiver's (few) messages are
 // put in ascending sender order (insertion sort of (sender, LDS position)) and
 // folded from LDS -- no gather of the bin's payloads from global memory.
-#ifndef GP_FB_SORT_ILP
-#define GP_FB_SORT_ILP 0  // k_fb_fold: the lock-step receivers' insertion sorts in lock step too
-#endif
-#ifndef GP_FB_ILP
-#define GP_FB_ILP 2  // receivers of a thread folded in lock step (k_fb_fold), 1: one after the other
-#endif
-#ifndef GP_FBF_THREADS
-#define GP_FBF_THREADS 1024
-#endif
-constexpr int FBF_THREADS = GP_FBF_THREADS;
+constexpr int FBF_THREADS = 1024;  // (256-thread fold blocks: 3.76 against 3.70 ms/round, profiles/r02/c4_v2/)
 
 //
 // SEND (one rank, FullBinArgs::fused): after a tile is folded, its nodes' sends of
@@ -591,18 +558,6 @@ constexpr int FBF_THREADS = GP_FBF_THREADS;
 // (reusing the fold's arrays), one reservation per (tile, bin), coalesced runs.
 // The next round then starts at B: no send pass re-reads the state (18 B/node).
 constexpr uint32_t FBF_MAXB1 = 1024;  // coarse bins the fused send can bin into (LDS reservation slots)
-#ifndef GP_FB_STAMPS
-#define GP_FB_STAMPS 0  // experiments, diagnostics: per-phase cycle sums of the fused fold (gp_debug_fb_stamps)
-#endif
-#if GP_FB_STAMPS
-__device__ unsigned long long gp_fb_stamp_acc[8];
-#define FB_STAMP(v) const uint64_t v = __builtin_amdgcn_s_memtime()
-#else
-#define FB_STAMP(v)
-#endif
-#ifndef GP_FB_PF
-#define GP_FB_PF 1  // fused fold: the next tile's messages loaded during this tile's send phase
-#endif
 
 template <bool SEND>
 __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t r) {
@@ -627,8 +582,9 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
     uint32_t alerts = 0, newly = 0;
     for (uint32_t v = threadIdx.x; v < TILE; v += FBF_THREADS) cnt[v] = 0u;
     __syncthreads();
-    // the tile's messages (sender ids, payloads) -- with GP_FB_PF, the next tile's are
-    // loaded while this tile's messages of round r+1 are scattered and written out
+    // the tile's messages (sender ids, payloads) -- fused: the next tile's are loaded while
+    // this tile's messages of round r+1 are scattered and written out (round 5: C4 3.158 /
+    // 3.165 -> 3.083 / 3.079 ms/round, same box, profiles/r05/c4/)
     uint32_t snd[FQ];
     double ps[FQ], pw[FQ];  // (two scalar arrays: a double2 array here went to scratch)
     auto load_msgs = [&](uint32_t f, uint32_t n) {
@@ -642,17 +598,13 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
             pw[k] = m.y;
         }
     };
-#if GP_FB_STAMPS
-    uint64_t ph[6] = {0, 0, 0, 0, 0, 0};
-#endif
     uint32_t n_pf = 0;
-    if (GP_FB_PF && SEND && blockIdx.x < a.nb2) {
+    if (SEND && blockIdx.x < a.nb2) {
         n_pf = min(ld_agent(&a.cnt2[blockIdx.x]), (uint32_t)a.cap2);
         load_msgs(blockIdx.x, n_pf);
     }
     for (uint32_t f = blockIdx.x; f < a.nb2; f += gridDim.x) {
-        FB_STAMP(t0);
-        const bool pf = GP_FB_PF && SEND;
+        constexpr bool pf = SEND;
         const uint32_t n = pf ? n_pf : min(ld_agent(&a.cnt2[f]), (uint32_t)a.cap2);
         // the next tile's message count, early (a scalar load; its messages are loaded later)
         const uint32_t fn = f + gridDim.x;
@@ -663,7 +615,6 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
         double2 svk[NPT];
         uint32_t nfl[NPT];  // fused send: active in round r+1, and the half it sends
         double2 nsw[NPT];
-        fb_prio_fold_loads<2>();
         if (!pf) load_msgs(f, n);
 #pragma unroll
         for (int k = 0; k < NPT; ++k) {
@@ -671,7 +622,6 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
             bk[k] = nbp[j];
             svk[k] = swc[j];
         }
-        fb_prio_fold_loads<0>();
         // fused send: the coarse bin of each of this thread's nodes' round-r+1 targets, drawn
         // while the tile's loads are in flight (whether the node sends is known after the fold)
         uint32_t nkey[SEND ? NPT / 2 : 1];
@@ -695,7 +645,6 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
             rk[k] = q < n ? atomicAdd(&cnt[vr[k]], 1u) : 0u;
         }
         lds_barrier();
-        FB_STAMP(t1);
         lds_excl_scan<FBF_THREADS, true>(cnt, TILE, tmp);
         if (threadIdx.x == 0) cnt[TILE] = n;
 #pragma unroll
@@ -708,7 +657,6 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
             }
         }
         lds_barrier();
-        FB_STAMP(t2);
         // per receiver after its fold: ratio test, flags, state out (and the fused send's inputs)
         auto close_receiver = [&](int k, uint32_t p0, uint32_t p1, double acc_s, double acc_w) {
             const uint32_t j = f * TILE + k * FBF_THREADS + threadIdx.x;
@@ -753,9 +701,11 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
                 idx[q] = xi;
             }
         };
-        // GP_FB_ILP receivers folded in lock step (one LDS chain each in flight, each receiver's
-        // own order kept); 1: one receiver after the other
-        constexpr int FG = GP_FB_ILP;
+        // FG receivers folded in lock step (one LDS chain each in flight, each receiver's own
+        // order kept): C4 3.177 -> 3.165 ms/round against one after the other, same box
+        // (profiles/r05/c4/ilp.txt); their insertion sorts in lock step too +10 %
+        // (profiles/r05/rejected/c4_sort_ilp.txt)
+        constexpr int FG = 2;
         static_assert(FG >= 1 && NPT % FG == 0, "fold groups");
 #pragma unroll
         for (int g0 = 0; g0 < NPT; g0 += FG) {
@@ -769,56 +719,12 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
                 const uint32_t j = f * TILE + v;
                 fp0[i] = cnt[v];
                 fp1[i] = j < a.nloc ? cnt[v + 1] : fp0[i];
-                if (!GP_FB_SORT_ILP) sort_receiver(fp0[i], fp1[i]);
+                sort_receiver(fp0[i], fp1[i]);
                 most = max(most, fp1[i] - fp0[i]);
                 const bool active = (bk[k] & B_ACTIVE) != 0;
                 fs[i] = active && P > 1 ? svk[k].x * 0.5 : svk[k].x;
                 fw[i] = active && P > 1 ? svk[k].y * 0.5 : svk[k].y;
             }
-#if GP_FB_SORT_ILP
-            // the FG insertion sorts in lock step too (disjoint LDS ranges): element t of each
-            // receiver sinks into its sorted prefix
-            for (uint32_t t = 1; t < most; ++t) {
-                uint32_t sv_[FG], q[FG];
-                uint16_t xv[FG];
-                bool go[FG];
-#pragma unroll
-                for (int i = 0; i < FG; ++i) {
-                    q[i] = fp0[i] + t;
-                    go[i] = q[i] < fp1[i];
-                    const uint32_t qc = min(q[i], (uint32_t)FB_CAP2 - 1u);
-                    sv_[i] = src[qc];
-                    xv[i] = idx[qc];
-                }
-                bool moved[FG];
-#pragma unroll
-                for (int i = 0; i < FG; ++i) moved[i] = false;
-                for (;;) {
-                    bool any = false;
-#pragma unroll
-                    for (int i = 0; i < FG; ++i)
-                        if (go[i]) {
-                            const uint32_t prev = q[i] > fp0[i] ? src[q[i] - 1] : 0u;
-                            if (q[i] > fp0[i] && prev > sv_[i]) {
-                                src[q[i]] = prev;
-                                idx[q[i]] = idx[q[i] - 1];
-                                --q[i];
-                                moved[i] = true;
-                                any = true;
-                            } else {
-                                go[i] = false;
-                            }
-                        }
-                    if (!any) break;
-                }
-#pragma unroll
-                for (int i = 0; i < FG; ++i)
-                    if (moved[i]) {
-                        src[q[i]] = sv_[i];
-                        idx[q[i]] = xv[i];
-                    }
-            }
-#endif
             for (uint32_t t = 0; t < most; ++t) {
                 uint16_t xi[FG];
 #pragma unroll
@@ -837,10 +743,6 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
         lds_barrier();
         for (uint32_t v = threadIdx.x; v < TILE; v += FBF_THREADS) cnt[v] = 0u;
         lds_barrier();
-        FB_STAMP(t3);
-#if GP_FB_STAMPS
-        uint64_t t4 = t3;
-#endif
         if (SEND) {
             // round r+1: coarse bin of every active node's target (drawn above), LDS rank per bin
             uint32_t node[NPT], key[NPT], rank[NPT];
@@ -868,11 +770,7 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
             }
             // the next tile's messages, issued after the reservation (so that waiting for its
             // result does not wait for them) and in flight through the scatter and write-out
-            if (GP_FB_PF && fn < a.nb2) {
-                fb_prio<2>();
-                load_msgs(fn, n_pf);
-                fb_prio<0>();
-            }
+            if (fn < a.nb2) load_msgs(fn, n_pf);
 #pragma unroll
             for (int k = 0; k < NPT; ++k) {
                 if (key[k] == FB_NONE) continue;
@@ -883,11 +781,7 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
             }
             if (q0 < a.nb1) sbase[q0] = res;
             lds_barrier();
-#if GP_FB_STAMPS
-            t4 = __builtin_amdgcn_s_memtime();
-#endif
             // write-out in bin order: consecutive threads, consecutive slots of one run
-            fb_prio<2>();
 #pragma unroll
             for (int k = 0; k < NPT; ++k) {
                 const uint32_t p = k * FBF_THREADS + threadIdx.x;
@@ -902,25 +796,11 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
                     atomicOr(a.overflow, 1u);
                 }
             }
-            fb_prio<0>();
             lds_barrier();
             for (uint32_t v = threadIdx.x; v < a.nb1; v += FBF_THREADS) cnt[v] = 0u;
             lds_barrier();
         }
-#if GP_FB_STAMPS
-        FB_STAMP(t5);
-        ph[0] += t1 - t0;  // message count + state loads issued, Philox, LDS receiver counts
-        ph[1] += t2 - t1;  // scan, messages into LDS in receiver order
-        ph[2] += t3 - t2;  // per receiver: sort, fold, ratio test, state out
-        ph[3] += t4 - t3;  // send: LDS bin counts, scan, reservations, next tile's loads issued, LDS scatter
-        ph[4] += t5 - t4;  // send: write-out
-        ph[5] += 1;
-#endif
     }
-#if GP_FB_STAMPS
-    if (threadIdx.x == 0)
-        for (int q = 0; q < 6; ++q) atomicAdd(&gp_fb_stamp_acc[q], (unsigned long long)ph[q]);
-#endif
     uint32_t x = alerts, y = newly;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -944,24 +824,6 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
 }
 
 // ---------------------------------------------------------------- host side
-#if GP_FB_STAMPS
-}  // namespace gp
-// Experiments build, diagnostics: mean cycles (s_memtime) per tile of the fused fold's phases
-// since the last reset (see k_fb_fold); out[5] = tiles counted.
-extern "C" int gp_debug_fb_stamps(double* out, int reset) {
-    unsigned long long h[8] = {0};
-    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(gp::gp_fb_stamp_acc), sizeof(h)) != hipSuccess) return -3;
-    const double n = h[5] ? (double)h[5] : 1.0;
-    for (int q = 0; q < 5; ++q) out[q] = (double)h[q] / n;
-    out[5] = (double)h[5];
-    if (reset) {
-        unsigned long long z[8] = {0};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(gp::gp_fb_stamp_acc), z, sizeof(z)) != hipSuccess) return -3;
-    }
-    return 0;
-}
-namespace gp {
-#endif
 // Bins for the nrecv receivers of a rank (one rank: nrecv = P).
 FullBinPlan full_bin_plan(uint32_t P, bool fused) {
     FullBinPlan p{};
@@ -973,9 +835,6 @@ FullBinPlan full_bin_plan(uint32_t P, bool fused) {
     // longer and the fold's shorter; P = 1e8, same box: rule 3.37, -1 3.26, -2 3.25,
     // -3 3.38-3.40 ms/round (profiles/r04/c4_fused/s1_sweep.txt)
     uint32_t s1 = (bits + FB_TB + 1) / 2 - (fused ? 1u : 0u);
-#ifdef GP_EXPERIMENTS
-    if (const char* e = std::getenv("GP_FB_S1D")) s1 += (uint32_t)std::atoi(e);  // coarse-bin size sweep
-#endif
     if (s1 < FB_TB) s1 = FB_TB;
     while (((uint64_t)P >> s1) >= FB_MAXBINS) ++s1;
     while (fused && (((uint64_t)P + (1ull << s1) - 1) >> s1) > FBF_MAXB1) ++s1;
@@ -1052,10 +911,7 @@ hipError_t launch_full_bin_round(const FullBinArgs& a, uint32_t round, int grid,
     const uint32_t items_b = split_items(a);
     hipLaunchKernelGGL(k_fb_split, dim3(items_b), dim3(FBR_THREADS), 2 * sizeof(uint32_t) * (1u << (a.s1 - FB_TB)), st,
                        a, round);
-    uint32_t nfold = fold_blocks(a, grid);
-#ifdef GP_EXPERIMENTS
-    if (const char* e = std::getenv("GP_FOLD_BLOCKS")) nfold = std::max<uint32_t>(1, std::min<uint32_t>(a.nb2, (uint32_t)std::atoi(e)));
-#endif
+    const uint32_t nfold = fold_blocks(a, grid);
     const dim3 gc(nfold);
     if (a.fused) {
         if ((e = hipMemsetAsync(a.cnt1, 0, sizeof(uint32_t) * a.nb1, st)) != hipSuccess) return e;

@@ -6,10 +6,9 @@
 
 namespace gp {
 
-#ifndef GP_FB_TB
-#define GP_FB_TB 12  // 4096 receivers per fold block (measured: 10 / 11 / 12 -> 3.65 / 3.63 / 3.60 ms at P = 1e8)
-#endif
-constexpr int FB_TB = GP_FB_TB;  // fine tile = 2^FB_TB receivers (one fold block)
+// fine tile = 2^FB_TB receivers (one fold block); 4096 (measured: 10 / 11 / 12 -> 3.65 / 3.63 /
+// 3.60 ms at P = 1e8)
+constexpr int FB_TB = 12;
 // messages per fine tile: expected 2^FB_TB + 12 sigma + 128 (4992 at 4096 receivers)
 constexpr int FB_CAP2 = ((1 << FB_TB) + 12 * (1 << (FB_TB / 2)) * (FB_TB % 2 ? 1414 : 1000) / 1000 + 128 + 63) / 64 * 64;
 

@@ -33,72 +33,35 @@ namespace gp {
 namespace wide {
 #endif
 
-// Experiment knobs (tools/ablate.py); the product build uses the defaults.
-#ifndef GP_TPB
+// Size class: gp_round_wide.hip defines these before including this file.
+#ifndef GP_ROUND_WIDE
 #define GP_TPB 256
-#endif
-#ifndef GP_NPT
 #define GP_NPT 4
+// __launch_bounds__ minimum waves per SIMD (= resident 256-thread blocks per CU): the LDS
+// tile allows 5, so keep VGPRs <= 96 to not lose the fifth
+#define GP_MINB 5
 #endif
-#ifndef GP_NT_LOADS
-#define GP_NT_LOADS 1
-#endif
-#ifndef GP_NT_STORES
-#define GP_NT_STORES 1
-#endif
-#ifndef GP_FMA_FOLD
-#define GP_FMA_FOLD 1    // fold as fma(m, 0.5, acc) (exact for |m| >= 2^-1021, guarded)
-#endif
-#ifndef GP_ABL_DIRS
-#define GP_ABL_DIRS 0    // ablation (wrong results, timing only): bit d set = skip the lattice gathers of slot d
-#endif
-#ifndef GP_STAMPS
-#define GP_STAMPS 0      // diagnostics (experiments build): per-phase cycle counts of the push-sum tile kernel
-#endif
-#ifndef GP_ZDPP
-#define GP_ZDPP 1        // push-sum tile kernel: the j+-1 messages from the neighbour lane's registers (DPP)
-#endif
-#ifndef GP_SETPRIO
-// push-sum tile kernel: wave priority raised (s_setprio GP_PRIO) while a wave issues its memory
-// operations -- each node slot's loads (1), also the in-edge pass's gathers (2), and on
-// through the staging copies (3) -- and dropped for the fold and the direction draws, so
-// waves about to issue loads win the SIMD over waves with ALU work and more loads are in
-// flight.  P = 1e9, same box, alternated (profiles/r04/setprio_ab.txt): 0 13.19-13.68,
-// 1 13.11-13.15, 2 12.94-13.18, 3 12.93-13.15 ms/round; on another box 0 13.34-13.45,
-// 3 13.08-13.26, 3 with priority 1 13.10-13.15, with 3 13.24-13.29, raised from the
-// in-edge pass's start (4) 13.18-13.30
-#define GP_SETPRIO 3
-#endif
-#ifndef GP_PRIO
-#define GP_PRIO 1        // the raised priority (experiments: 1..3)
-#endif
-#ifndef GP_STEAL
-// walk 3: a block whose XCD's queue is empty takes items from the other XCDs' queues.  Slabs
-// whose planes do not split evenly over the 8 XCDs (W = 8: 125 planes) and tiles of uneven
-// cost otherwise leave XCDs idle at the round's tail.  P = 1e9, same box, alternated: 12.85-12.87
-// -> 12.75-12.81 ms/round; W = 8 slab 1.714 -> 1.699 ms (profiles/r04/walk_steal.txt)
-#define GP_STEAL 1
-#endif
-#ifndef GP_NG
-#define GP_NG 1          // push-sum tile kernel: node slots whose loads are in flight together
-#endif
-#ifndef GP_RK_EARLY
-#define GP_RK_EARLY 0    // REMOTE push-sum: list keys loaded with the in-edge senders (before the draws)
-#endif
-#ifndef GP_MINB
-#define GP_MINB 5  // __launch_bounds__ minimum waves per SIMD (= resident 256-thread blocks per CU):
-                   // the LDS tile allows 5, so keep VGPRs <= 96 to not lose the fifth
-#endif
+
+// Measured choices of the push-sum tile kernel (the rejected alternatives and their
+// records are in DESIGN.md §5.1 and profiles/; git history has their code):
+//  * wave priority: raised (s_setprio PRIO) while a wave issues its memory operations --
+//    the in-edge pass's gathers, the staging copies, each node slot's loads -- and dropped
+//    for the fold and the direction draws, so waves about to issue loads win the SIMD over
+//    waves with ALU work and more loads are in flight (P = 1e9, same box, alternated:
+//    13.19-13.68 -> 12.93-13.15 ms/round, profiles/r04/setprio_ab.txt);
+//  * walk 3 work stealing: a block whose XCD's queue is empty takes items from the other
+//    XCDs' queues (12.85-12.87 -> 12.75-12.81 ms/round; W = 8 slab 1.714 -> 1.699 ms,
+//    profiles/r04/walk_steal.txt);
+//  * the j +- 1 messages from the neighbour lanes' registers by DPP, one node slot's loads
+//    in flight at a time (two spilled), non-temporal staging loads and state stores.
+constexpr int PRIO = 1;  // the raised wave priority
 
 namespace {
 
-constexpr int TPB = GP_TPB;                // 256 (experiments: 128)
+constexpr int TPB = GP_TPB;                // 256 (wide size class: 1024)
 constexpr int NPT = GP_NPT;                // nodes per thread per tile
 constexpr int TILE = TPB * NPT;            // 1024
-#ifndef GP_HMAX
-#define GP_HMAX 1625
-#endif
-constexpr int HMAX = GP_HMAX;              // largest lattice edge with g^3 < 2^32 (experiments: smaller)
+constexpr int HMAX = 1625;                 // largest lattice edge with g^3 < 2^32
 constexpr int W_ROWS = (TILE + 2 * HMAX) / 4 + 4;
 constexpr int W_PLANE = TILE / 4 + 4;
 constexpr int SRC_CAP = TILE * 3 / 2;       // gossip: staged in-list entries per tile (mean TILE)
@@ -120,31 +83,37 @@ struct TileLds {
 // k_ps_tile: the tile decides its in-edges itself.  The used in-edges' (s, w) are gathered by LDS-DMA straight into per-edge
 // slots (edge q's message at slot q -- lane-linear, so one global_load_lds per
 // edge batch, no registers, no compaction).  A tile with more than SLOTS
-// in-edges (6 sigma above the mean TILE: ~1e-9 of tiles) takes the unstaged path,
-// so the node fold reads LDS only (no global fallback inside its loop, whose
-// join would cost a vmcnt(0) wait per message).
-#ifndef GP_SND_PF
-// Imp3D push-sum: the next tile's in-edge senders LDS-DMA'd during this tile's node phase, so a
-// tile's in-edge pass starts from LDS (C5, same box, alternated: 12.92-13.07 -> 12.78-12.86 ms on
-// one box, 12.78-12.82 -> 12.74-12.77 on another, profiles/r05/sndpf/; 0 builds the round-4 form)
-#define GP_SND_PF 1
-#endif
-// 1216 at TILE = 1024: the LDS of 5 blocks per CU (GP_SND_PF: 1152, room for the senders' buffer)
-constexpr int SLOTS = GP_SND_PF ? TILE + TILE / 8 : TILE + TILE / 8 + TILE / 16;
-constexpr int SLOT_FU = (SLOTS + TPB - 1) / TPB;  // in-edges per thread in the in-edge pass
+// in-edges takes the unstaged path, so the node fold reads LDS only (no global
+// fallback inside its loop, whose join would cost a vmcnt(0) wait per message).
+//
+// One rank (SNDPF): the next tile's in-edge senders are LDS-DMA'd during this tile's node phase,
+// so a tile's in-edge pass starts from LDS (C5, same box, alternated: 12.92-13.07 -> 12.78-12.86
+// ms on one box, 12.78-12.82 -> 12.74-12.77 on another, profiles/r05/sndpf/).  Their buffer takes
+// LDS from the slots: 1152 slots (a tile's in-degree is ~Poisson(1024); 4 sigma, ~4e-5 of tiles
+// -- about 40 per C5 round -- take the unstaged path).  The REMOTE kernel (several ranks) has no
+// such buffer (measured within noise there, profiles/r05/sndpf/w8.txt) and keeps 1216 slots (6
+// sigma, ~2.5e-9 of tiles): both fill the LDS of 5 blocks per CU.
+template <bool REMOTE>
+struct PsSlots {
+    static constexpr bool SNDPF = !REMOTE;
+    static constexpr int SLOTS = SNDPF ? TILE + TILE / 8 : TILE + TILE / 8 + TILE / 16;
+    static constexpr int FU = (SLOTS + TPB - 1) / TPB;  // in-edges per thread in the in-edge pass
+};
 
+template <bool REMOTE>
 struct TileLdsP {
+    static constexpr int SLOTS = PsSlots<REMOTE>::SLOTS, SLOT_FU = PsSlots<REMOTE>::FU;
     uint32_t rows[W_ROWS + DMA_SLACK];
     uint32_t xm[W_PLANE + DMA_SLACK];
     uint32_t xp[W_PLANE + DMA_SLACK];
     uint32_t ind[TILE / 8 + DMA_SLACK];  // in-degrees of the tile's nodes, a nibble each (DevState::ind4)
-    uint32_t snd[GP_SND_PF ? SLOTS + DMA_SLACK : 1];  // GP_SND_PF: the next tile's in-edge senders
+    uint32_t snd[PsSlots<REMOTE>::SNDPF ? SLOTS + DMA_SLACK : 1];  // one rank: the next tile's in-edge senders
     unsigned long long bits[SLOT_FU * (TPB / 64) + 1];  // bit q: in-edge q (tile order) was used by its sender; then 0
     double2 msg[SLOTS];               // edge q's message at slot q
     uint32_t out[TILE / 4];
     uint32_t red[2][TPB / 64];
     uint32_t qn[2];                   // walk 3: the block's next item, by iteration parity
-    double2 zb[TPB / 64][NPT][2];     // GP_ZDPP: (s, w) across each wave's ends, slot k: [0] node - 1, [1] node + 64
+    double2 zb[TPB / 64][NPT][2];     // (s, w) across each wave's ends, slot k: [0] node - 1, [1] node + 64
 };
 
 // set bits of m below this lane
@@ -174,7 +143,7 @@ __device__ __forceinline__ void dma_copy(void* lds, const char* g16, uint32_t nb
     }
 }
 // cache-policy bits of a single-use (streamed once per round) staging copy: nt
-constexpr int DMA_ONCE = GP_NT_LOADS ? 2 : 0;
+constexpr int DMA_ONCE = 2;
 
 // Node bytes nb[lo, hi) clamped to [ext_lo,
 // ext_hi); returns the node id of LDS byte 0 (up to 15 bytes below lo).  Reads
@@ -203,15 +172,6 @@ template <typename T>
 __device__ __forceinline__ T ld_agent(const T* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-
-#if GP_STAMPS
-// Phase cycle counters (block 0's wave 0 lane 0 of every block sums its own
-// tiles); read by gp_debug_stamps (experiments build only).
-__device__ unsigned long long gp_stamp_acc[8];
-#define GP_STAMP(v) const uint64_t v = __builtin_amdgcn_s_memtime()
-#else
-#define GP_STAMP(v)
-#endif
 
 // Tile walks (speed only -- any placement is correct; every tile of the slab
 // is visited exactly once).  Blocks with equal blockIdx % 8 share an XCD.
@@ -340,20 +300,10 @@ __device__ __forceinline__ double2 dpp_double2(double2 v) {
 // stores keep it from displacing the current round's (s, w) in the XCD's L2,
 // where the neighbouring tiles' lattice gathers look for it.
 __device__ __forceinline__ void st_stream(double2* p, double2 v) {
-#if GP_NT_STORES
     __builtin_nontemporal_store(v.x, &p->x);
     __builtin_nontemporal_store(v.y, &p->y);
-#else
-    *p = v;
-#endif
 }
-__device__ __forceinline__ void st_stream(uint32_t* p, uint32_t v) {
-#if GP_NT_STORES
-    __builtin_nontemporal_store(v, p);
-#else
-    *p = v;
-#endif
-}
+__device__ __forceinline__ void st_stream(uint32_t* p, uint32_t v) { __builtin_nontemporal_store(v, p); }
 
 }  // namespace
 
@@ -378,8 +328,8 @@ __device__ __forceinline__ void st_stream(uint32_t* p, uint32_t v) {
 //   4. next-round directions of the thread's NPT nodes as one Philox batch;
 //      node bytes out as words, random-edge bits as one ballot per wave.
 template <int TOPO, bool REMOTE>
-__device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLdsP& L, bool all_active, uint32_t& alerts,
-                                         uint32_t& newly, bool& tiny) {
+__device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLdsP<REMOTE>& L, bool all_active,
+                                         uint32_t& alerts, uint32_t& newly, bool& tiny) {
     const double2* __restrict__ swc = a.swc;
     double2* __restrict__ swn = a.swn;
     const uint64_t* __restrict__ rbc = a.rbc;
@@ -388,23 +338,18 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
     const uint32_t* __restrict__ srcp = packed ? a.in_srcd : in_src;
     const Geom G = a.G;
     const uint32_t H = TOPO == LINE ? 1u : G.g;
-    constexpr int FU = SLOT_FU;
-    const uint32_t cap = min((uint32_t)SLOTS, a.stage_cap);
+    constexpr int FU = PsSlots<REMOTE>::FU;
+    const uint32_t cap = min((uint32_t)PsSlots<REMOTE>::SLOTS, a.stage_cap);
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
 
     // loaded one tile ahead: the next tile's in-edge range (two uniform loads); the
     // staged tile's senders, FU words per thread (loaded at the tile's start)
     uint32_t pf_tile = 0xFFFFFFFFu, pf_lo = 0, pf_hi = 0;
-    uint32_t snd_tile = 0xFFFFFFFFu, snd_off = 0;  // GP_SND_PF: L.snd holds tile snd_tile's senders from word snd_off
-    // (one rank only: with REMOTE slabs at W = 8 it measured 1.88-1.90 against 1.90-1.93 ms per slab without,
-    // same box -- within noise, not adopted there; profiles/r05/sndpf/w8.txt)
-    constexpr bool SNDPF = GP_SND_PF && !REMOTE;
+    uint32_t snd_tile = 0xFFFFFFFFu, snd_off = 0;  // SNDPF: L.snd holds tile snd_tile's senders from word snd_off
+    constexpr bool SNDPF = PsSlots<REMOTE>::SNDPF;
     uint32_t raw[FU];
 #pragma unroll
     for (int m = 0; m < FU; ++m) raw[m] = 0u;
-#if GP_STAMPS
-    uint64_t ph[7] = {0, 0, 0, 0, 0, 0, 0};
-#endif
     TileWalk tw(a);
     const bool dyn = tw.mode == 3;  // block-uniform
     uint32_t it = 0;                // iteration: parity selects the LDS slot of the next claim
@@ -415,12 +360,10 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
         tw.t = L.qn[0];
         ++it;
     }
-#if GP_STEAL
     // walk 3: once this XCD's list is exhausted, the block takes items from the other
     // XCDs' queues in turn (their tiles' lattice lines are in another L2, but only
     // the round's tail runs this way), so no XCD idles while another has work
     for (uint32_t victim = 0;;) {
-#endif
     while (tw.t < tw.end) {
         uint32_t ti;
         // walk 3: thread 0 claims the next item now; it is published in LDS at the
@@ -438,7 +381,6 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
             }
             continue;
         }
-        GP_STAMP(t0);
         // tiles sit on global multiples of TILE (4-aligned word I/O, 64-aligned
         // ballot words); the slab's first and last tile may be partial
         const uint32_t T = (a.lo / TILE + ti) * TILE;
@@ -471,7 +413,6 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
         }
         if constexpr (TOPO == IMP3D) {
             if (staged) {
-                if (GP_SETPRIO >= 4) __builtin_amdgcn_s_setprio(GP_PRIO);
                 // in-edge q = m * TPB + wave * 64 + lane is bit `lane` of bitmap word
                 // m * 4 + wave; its message (if used) lands in slot q
                 if (SNDPF && snd_tile == ti) {  // (block-uniform) prefetched during the last tile
@@ -487,18 +428,6 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                         raw[m] = q < cnt ? __builtin_nontemporal_load(srcp + e_lo + q) : 0u;
                     }
                 }
-                uint32_t rkv[REMOTE ? FU : 1];
-#if GP_RK_EARLY
-                // REMOTE: the list keys of the tile's in-edges (meaningful for remote senders),
-                // streamed with the senders
-                if constexpr (REMOTE) {
-#pragma unroll
-                    for (int m = 0; m < FU; ++m) {
-                        const uint32_t q = threadIdx.x + m * TPB;
-                        rkv[m] = q < cnt ? __builtin_nontemporal_load(a.rk + e_lo + q) : 0u;
-                    }
-                }
-#endif
                 uint32_t isrc[FU];
                 bool sent[FU], pick[FU];
 #pragma unroll
@@ -574,15 +503,14 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                 // so no load waits under a branch.
                 uint32_t ridx[REMOTE ? FU : 1];
                 if constexpr (REMOTE) {
-#if !GP_RK_EARLY
                     // the list keys of the tile's in-edges (meaningful for remote senders), after
                     // the draws: live across the Philox batch they cost spills
+                    uint32_t rkv[FU];
 #pragma unroll
                     for (int m = 0; m < FU; ++m) {
                         const uint32_t q = threadIdx.x + m * TPB;
                         rkv[m] = q < cnt ? __builtin_nontemporal_load(a.rk + e_lo + q) : 0u;
                     }
-#endif
                     uint2 hm[FU];
                     uint32_t hb[FU];
 #pragma unroll
@@ -605,7 +533,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                         }
                     }
                 }
-                if (GP_SETPRIO >= 2) __builtin_amdgcn_s_setprio(GP_PRIO);
+                __builtin_amdgcn_s_setprio(PRIO);
 #pragma unroll
                 for (int m = 0; m < FU; ++m) {
                     const unsigned long long bal = __ballot(sent[m]);
@@ -626,10 +554,8 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                     }
                 }
                 if (threadIdx.x == 0) L.bits[FU * (TPB / 64)] = 0ull;
-                if (GP_SETPRIO == 2) __builtin_amdgcn_s_setprio(0);
             }
         }
-        GP_STAMP(t1);
         // own (s, w): loaded with the node's lattice gathers (ahead of the staging
         // copies it kept 12 more VGPRs live and measured slower)
         double2 own[NPT];
@@ -642,7 +568,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
         }
         // (s, w) across every wave's ends, slot k: node T + k*TPB + 64 wave - 1 and + 64
         // (clamped into the node arrays; used only where that neighbour sent)
-        if (GP_ZDPP && lane < 2u * NPT) {
+        if (lane < 2u * NPT) {
             int64_t jn = (int64_t)T + (int64_t)((lane >> 1) * TPB + wv * 64u) + ((lane & 1u) ? 64 : -1);
             if (jn < (int64_t)a.ext_lo) jn = a.ext_lo;
             if (jn > (int64_t)a.ext_hi) jn = a.ext_hi;
@@ -651,11 +577,9 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
         // the tile's in-degrees, a nibble per node (512 bytes; the slab's arrays
         // cover whole tiles, ids outside the slab are 0)
         if (TOPO == IMP3D) dma_copy<DMA_ONCE>(L.ind, reinterpret_cast<const char*>(a.ind4 + T / 2), TILE / 2);
-        GP_STAMP(t2);
         if (dyn && threadIdx.x == 0) L.qn[it & 1] = claim;
-        if (GP_SETPRIO >= 3) __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_setprio(0);
         __syncthreads();  // staging copies, in-edge bitmap and gathered messages retired
-        GP_STAMP(t3);
         // Imp3D: node jl's in-edges are [e_lo + pre(jl), + d(jl)), pre = exclusive
         // prefix of the nibble in-degrees.  Every wave sums all 16 64-node chunks
         // (lane L: nodes 16L..16L+15) and keeps the prefixes of its own chunks
@@ -717,15 +641,13 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                 wcy = fastdiv(rem, G.div_g);
                 wcz = rem - wcy * G.g;
             }
-            constexpr uint32_t ND = TOPO == LINE ? 2 : 6;
-            // lattice directions gathered from HBM / L2; with GP_ZDPP the j +- 1 ones
-            // (z +- 1, or both line neighbours) are the neighbour lanes' own (s, w)
-            constexpr uint32_t NDG = GP_ZDPP ? (TOPO == LINE ? 0u : 4u) : ND;
-            constexpr int NG = GP_NG;  // node slots per group in flight (2 at 5 waves/SIMD spilled 49 VGPRs)
-            static_assert(NPT % NG == 0, "node groups must divide the nodes per thread");
+            // lattice directions gathered from HBM / L2; the j +- 1 ones (z +- 1, or both
+            // line neighbours) are the neighbour lanes' own (s, w)
+            constexpr uint32_t NDG = TOPO == LINE ? 0u : 4u;
+            constexpr int NG = 1;  // node slots per group in flight (2 at 5 waves/SIMD spilled 49 VGPRs)
 #pragma unroll
             for (int k0 = 0; k0 < NPT; k0 += NG) {
-                if (GP_SETPRIO) __builtin_amdgcn_s_setprio(GP_PRIO);
+                __builtin_amdgcn_s_setprio(PRIO);
                 // phase A: node byte, present mask, lattice senders (from the staged
                 // direction bytes), one gather per direction -- a direction without a
                 // sender reads the zero sentinel swc[ext_hi] (adding +0.0 is exact)
@@ -800,13 +722,9 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                     own[k] = swc[min(max(j, j0), j1 - 1u)];
 #pragma unroll
                     for (uint32_t d = 0; d < NDG; ++d)
-                        if ((GP_ABL_DIRS >> d) & 1) {  // ablation (timing only): no gathers in slot d
-                            m[h][d] = make_double2(0.0, 0.0);
-                        } else {
-                            m[h][d] = ld_sw(swc + ((from >> d) & 1u ? nbr<TOPO>(j, d, G) : a.ext_hi));
-                        }
+                        m[h][d] = ld_sw(swc + ((from >> d) & 1u ? nbr<TOPO>(j, d, G) : a.ext_hi));
                 }
-                if (GP_SETPRIO) __builtin_amdgcn_s_setprio(0);
+                __builtin_amdgcn_s_setprio(0);
                 // phase B: canonical fold (own half, lattice slots in slot order, random
                 // edges by ascending sender; every message contributes the sender's half),
                 // ratio test, next-round state
@@ -821,7 +739,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                     // only where that lane's node is outside the tile's valid range
                     // (partial tiles at slab ends)
                     double2 zP = make_double2(0.0, 0.0), zM = zP;
-                    if (GP_ZDPP) {
+                    {
                         constexpr uint32_t dP = TOPO == LINE ? 1u : 4u, dM = TOPO == LINE ? 0u : 5u;
                         const uint32_t from = (gst[h] >> 14) & 63u;
                         zP = dpp_double2<0x130>(own[k]);  // wave_shl:1 -- lane + 1's (s, w)
@@ -848,27 +766,20 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                         // node checks its own round-start (s, w) -- the values its messages
                         // carry this round -- against 2^-1020 (Ctl::tiny, gp_step fails)
                         auto fold = [&](const double2 mi) {
-#if GP_FMA_FOLD
                             acc_s = __builtin_fma(mi.x, 0.5, acc_s);
                             acc_w = __builtin_fma(mi.y, 0.5, acc_w);
-#else
-                            acc_s = acc_s + mi.x * 0.5;
-                            acc_w = acc_w + mi.y * 0.5;
-#endif
                         };
                         tiny |= (sv.y < 0x1p-1020) | (sv.x != 0.0 && sv.x < 0x1p-1020);
                         bool recv = from != 0;
                         // lattice slots in slot order: line j-1, j+1; 3D x-1, x+1, y+1, y-1, z+1, z-1
-                        if (GP_ZDPP && TOPO == LINE) {
+                        if (TOPO == LINE) {
                             fold(zM);
                             fold(zP);
                         } else {
 #pragma unroll
                             for (uint32_t d = 0; d < NDG; ++d) fold(m[h][d]);
-                            if (GP_ZDPP) {
-                                fold(zP);
-                                fold(zM);
-                            }
+                            fold(zP);
+                            fold(zM);
                         }
                         if (TOPO == IMP3D) {
                             uint32_t e_b = e_lo + epre[h], e_e = e_b + (gst[h] >> 20);
@@ -939,12 +850,10 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                         }
                         // next-round direction drawn below, one Philox batch for the thread's nodes
                         pend[k >> 1] |= (mask | (active && deg > 0 ? 64u : 0u) | ((flags >> 3) << 7)) << (16 * (k & 1));
-                        if (GP_SETPRIO >= 5) __builtin_amdgcn_s_setprio(GP_PRIO);
                         st_stream(swn + j, make_double2(acc_s, acc_w));
-                        if (GP_SETPRIO >= 5) __builtin_amdgcn_s_setprio(0);
                     }
                 }
-                // GP_SND_PF: after the first node slot (the next tile's in-edge range has arrived by
+                // SNDPF: after the first node slot (the next tile's in-edge range has arrived by
                 // then), its senders by LDS-DMA; this tile's were read in its in-edge pass, and the
                 // tile's closing barrier retires the copy before the next tile reads it
                 if (SNDPF && TOPO == IMP3D && k0 == 0) {
@@ -956,7 +865,6 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                 }
             }
         }
-        GP_STAMP(t4);
         // next-round directions of this thread's nodes: one Philox batch
         {
             uint32_t node[NPT], x[NPT], y[NPT];
@@ -982,7 +890,6 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
             }
         }
         __syncthreads();
-        GP_STAMP(t5);
         // node bytes out as words (allocations are padded past P)
         for (uint32_t w = threadIdx.x; w < (uint32_t)(TILE / 4); w += TPB) {
             const uint32_t jw = T + w * 4;
@@ -993,22 +900,11 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                     if (jw + b >= j0 && jw + b < j1) a.nbn[jw + b] = reinterpret_cast<const uint8_t*>(L.out)[w * 4 + b];
             }
         }
-#if GP_STAMPS
-        GP_STAMP(t6);
-        ph[0] += t1 - t0;
-        ph[1] += t2 - t1;
-        ph[2] += t3 - t2;
-        ph[3] += t4 - t3;
-        ph[4] += t5 - t4;
-        ph[5] += t6 - t5;
-        ph[6] += 1;
-#endif
         // no barrier here: the next tile's in-edge pass and staging copies write
         // bits / msg / rows / xm / xp / off, none of which this byte output reads,
         // and its node phase writes L.out only after its staging barrier
         tw.t = t_next;
     }
-#if GP_STEAL
         if (!dyn || ++victim >= 8u) break;
         const uint32_t c = (blockIdx.x + victim) & 7u;
         tw.qc = a.tq + c * TQ_STRIDE;
@@ -1019,11 +915,6 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
         tw.t = L.qn[it & 1];
         ++it;
     }
-#endif
-#if GP_STAMPS
-    if (threadIdx.x == 0)
-        for (int q = 0; q < 7; ++q) atomicAdd(&gp_stamp_acc[q], (unsigned long long)ph[q]);
-#endif
 }
 
 // Block sums of this block's alerts / newly active nodes (valid in thread 0).
@@ -1066,7 +957,7 @@ __device__ __forceinline__ void add_round_counts(Ctl* ctl, uint32_t x, uint32_t 
 
 template <int TOPO, bool REMOTE>
 __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t r) {
-    __shared__ TileLdsP L;
+    __shared__ TileLdsP<REMOTE> L;
     Ctl* ctl = a.ctl;
     if (ld_agent(&ctl->done)) return;
     const bool all_active = ld_agent(&ctl->all_active) != 0;
@@ -1310,19 +1201,11 @@ RoundArgs make_round_args(const DevState& S, uint32_t round) {
     return a;
 }
 
-#ifndef GP_RLAST
-#define GP_RLAST 0  // the last region half the size of the others (region_plane)
-#endif
-// First plane (relative to the slab's) of region h of NR over nx planes: equal regions, or with
-// GP_RLAST the last one half the size of the others (its pack and transfer are the round's
-// exposed tail) -- region h starts at nx 2h / (2 NR - 1).
+// First plane (relative to the slab's) of region h of NR equal regions over nx planes.  (A last
+// region half the size of the others measured within noise, profiles/r05/rejected/rlast.txt.)
 uint32_t region_plane(uint32_t nx, int NR, int h) {
-    bool half = GP_RLAST;
-#ifdef GP_EXPERIMENTS
-    if (const char* e = std::getenv("GP_RLAST")) half = e[0] == '1';
-#endif
     if (h >= NR) return nx;
-    return half && NR > 1 ? (uint32_t)((uint64_t)nx * 2 * h / (2 * NR - 1)) : (uint32_t)((uint64_t)nx * h / NR);
+    return (uint32_t)((uint64_t)nx * h / NR);
 }
 
 // Region h of NR of a plane-aligned slab: planes [x0 + region_plane(h), x0 + region_plane(h + 1)),
@@ -1493,21 +1376,3 @@ hipError_t launch_rbits_init(const DevState& S, int grid, hipStream_t st) {
 }  // namespace wide
 #endif
 }  // namespace gp
-
-#if GP_STAMPS
-// Experiments build, diagnostics: mean cycles per tile of each push-sum tile
-// phase since the last reset (in-edge pass, staging issue, staging wait, node
-// phase, direction batch, byte-out barrier), out[6] = tiles counted.
-extern "C" int gp_debug_stamps(double* out, int reset) {
-    unsigned long long h[8] = {0};
-    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(gp::gp_stamp_acc), sizeof(h)) != hipSuccess) return -3;
-    const double n = h[6] ? (double)h[6] : 1.0;
-    for (int q = 0; q < 6; ++q) out[q] = (double)h[q] / n;
-    out[6] = (double)h[6];
-    if (reset) {
-        unsigned long long z[8] = {0};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(gp::gp_stamp_acc), z, sizeof(z)) != hipSuccess) return -3;
-    }
-    return 0;
-}
-#endif

@@ -56,15 +56,12 @@ struct SlabTable {
 // only senders with a message cost bytes.  The destination buffers' addresses
 // sit in LDS (indexing the kernel arguments by a per-lane rank was a global
 // load per message).
-#ifndef GP_XCHG_PRIO
-// wave priority raised (s_setprio 1) while k_pack / k_unpack issue their loads.  C5 at W = 8
+// Wave priority raised (s_setprio 1) while k_pack / k_unpack issue their loads.  C5 at W = 8
 // virtual ranks, same box, alternated: pack 4.97-4.99 -> 4.83 ms and unpack 5.59-5.73 ->
 // 5.36-5.71 ms over the 8 slabs (profiles/r04/setprio_xchg.txt)
-#define GP_XCHG_PRIO 1
-#endif
 template <int P>
 __device__ __forceinline__ void xchg_prio() {
-    if (GP_XCHG_PRIO) __builtin_amdgcn_s_setprio(P);
+    __builtin_amdgcn_s_setprio(P);
 }
 
 constexpr int PACK_PER = 32;                     // senders per thread
@@ -326,20 +323,9 @@ __global__ __launch_bounds__(256) void k_list_key(ListKeyArgs a) {
 // at once, ONE reservation per destination (a reservation per tile queued ~60 k
 // returning atomics on each of a C5 slab's 14 counters per round: 0.73 ms per region),
 // the header words and the messages in list order.  Two barriers per block.
-#ifndef GP_LP_STAMPS
-#define GP_LP_STAMPS 0  // experiments, diagnostics: per-phase cycle sums of k_list_pack (gp_debug_lp_stamps)
-#endif
-#if GP_LP_STAMPS
-__device__ unsigned long long gp_lp_stamp_acc[8];
-#define LP_STAMP(v) const uint64_t v = __builtin_amdgcn_s_memtime()
-#else
-#define LP_STAMP(v)
-#endif
 constexpr int LIST_LW = XTILE / 64 + XMAXW;  // LDS words of one tile's segments (<= 16 full + 1 partial each)
-#ifndef GP_LP_TILES
-#define GP_LP_TILES 8  // experiments: tiles per block (16: 0.52 -> 0.59 ms per C5 slab at W = 8, profiles/r05/rejected/pack_shapes.txt)
-#endif
-constexpr int LP_TILES = GP_LP_TILES;        // tiles per block, one per wave
+// tiles per block, one per wave (16: 0.52 -> 0.59 ms per C5 slab at W = 8, profiles/r05/rejected/pack_shapes.txt)
+constexpr int LP_TILES = 8;
 constexpr int LP_WT = 1;                     // tiles per wave
 constexpr int LP_THREADS = 64 * LP_TILES / LP_WT;
 constexpr int LP_SLOTS = XTILE / 64;         // 64-id slots per tile
@@ -351,7 +337,6 @@ __global__ __launch_bounds__(LP_THREADS) void k_list_pack(ListPackArgs a) {
     __shared__ uint32_t off[XMAXW];                 // the block's reserved run in each destination's chunk
     __shared__ double2* ovals[XMAXW];
     __shared__ uint32_t ocap[XMAXW];
-    LP_STAMP(t0);
     const uint32_t tb = a.t0 + blockIdx.x * LP_TILES;
     if (tb >= a.t1) return;
     const int ntl = (int)min((uint32_t)LP_TILES, a.t1 - tb);
@@ -368,7 +353,6 @@ __global__ __launch_bounds__(LP_THREADS) void k_list_pack(ListPackArgs a) {
         if ((int)tt < ntl) lw[tt][d] = a.lwt[(size_t)(tb + tt) * (W + 1) + d];
     }
     __syncthreads();
-    LP_STAMP(t1);
     // per tile of this wave and slot: used ? 1 << 31 | d << 11 | rho : 0 (rho < 1024)
     uint32_t st[LP_WT][LP_SLOTS];
 #pragma unroll
@@ -422,9 +406,7 @@ __global__ __launch_bounds__(LP_THREADS) void k_list_pack(ListPackArgs a) {
         const uint32_t a0 = __shfl(incl, (int)(e0 > 0 ? e0 - 1 : 0), 64);
         if (l < (uint32_t)W) tn[tt][l] = e1 > e0 ? a1 - (e0 > 0 ? a0 : 0u) : 0u;
     }
-    LP_STAMP(t2);
     __syncthreads();
-    LP_STAMP(t3);
     if (threadIdx.x < (uint32_t)W) {  // the block's run per destination: one reservation
         const uint32_t d = threadIdx.x;
         uint32_t r = 0;
@@ -436,7 +418,6 @@ __global__ __launch_bounds__(LP_THREADS) void k_list_pack(ListPackArgs a) {
         off[d] = d != me && r ? atomicAdd(a.peer[d].cnt, r) : 0u;
     }
     __syncthreads();
-    LP_STAMP(t4);
 #pragma unroll
     for (int u = 0; u < LP_WT; ++u) {
         const int tt = (int)wv * LP_WT + u;
@@ -454,12 +435,6 @@ __global__ __launch_bounds__(LP_THREADS) void k_list_pack(ListPackArgs a) {
                 a.peer[seg].hdr[a.gw[(size_t)(tb + tt) * W + seg] + (l - lw[tt][seg])] = h;
             }
         }
-#if GP_LP_STAMPS
-        if (u == 0) {
-            LP_STAMP(t5);
-            if (threadIdx.x == 0) atomicAdd(&gp_lp_stamp_acc[4], (unsigned long long)(t5 - t4));
-        }
-#endif
         // the used entries' (s, w): buffer loads over the tile's ids, past the end for the
         // others (no memory touched, no load under a branch), four slots in flight.  (A compacted
         // outbox of the random-edge senders' (s, w), written by the round kernel, cut the pack's
@@ -494,17 +469,6 @@ __global__ __launch_bounds__(LP_THREADS) void k_list_pack(ListPackArgs a) {
             }
         }
     }
-#if GP_LP_STAMPS
-    LP_STAMP(t6);
-    if (threadIdx.x == 0) {
-        atomicAdd(&gp_lp_stamp_acc[0], (unsigned long long)(t1 - t0));  // LDS init, tile layouts
-        atomicAdd(&gp_lp_stamp_acc[1], (unsigned long long)(t2 - t1));  // wave 0's tile: loads, bitmap, scans
-        atomicAdd(&gp_lp_stamp_acc[2], (unsigned long long)(t3 - t2));  // waiting for the block's other tiles
-        atomicAdd(&gp_lp_stamp_acc[3], (unsigned long long)(t4 - t3));  // reservations
-        atomicAdd(&gp_lp_stamp_acc[5], (unsigned long long)(t6 - t4));  // headers + payloads (wave 0)
-        atomicAdd(&gp_lp_stamp_acc[6], 1ull);
-    }
-#endif
 }
 
 // A halo plane's senders toward the neighbour: their (s, w) compacted per 1024-node chunk, in
@@ -532,8 +496,8 @@ __global__ __launch_bounds__(256) void k_halo(HaloArgs a) {
         uint32_t rank = below[k];
         for (uint32_t q = 0; q < (uint32_t)k * 4u + wv; ++q) rank += wc[q];
         const uint32_t i = c0 + k * 256u + threadIdx.x;
-        double2* slot = a.buf + (size_t)blockIdx.x * HALO_CAP + rank;
-        if (rank >= HALO_CAP) {
+        double2* slot = a.buf + (size_t)blockIdx.x * a.cap + rank;
+        if (rank >= a.cap) {
             if (PACK) atomicOr(a.overflow, 1u);
         } else if (PACK) {
             *slot = a.sw[i];
@@ -717,6 +681,30 @@ hipError_t launch_halo_expand(const HaloArgs& a, hipStream_t st) {
     if (a.n) hipLaunchKernelGGL(k_halo<false>, dim3((a.n + HALO_CHUNK - 1) / HALO_CHUNK), dim3(256), 0, st, a);
     return hipGetLastError();
 }
+
+// Slots per 1024-node chunk of a slab-boundary plane (HaloArgs): the senders toward one x
+// neighbour in a chunk are a sum of Bernoulli(1 / deg) over its nodes (Program.fs:246-260: a
+// boundary plane's nodes have both x neighbours, y / z ones unless on the lattice's edge, and
+// Imp3D's random edge); the largest mean + 12 sigma over the plane's chunks, rounded up to 8.
+// g = 1000: 3D 360 (the chunk of row y = 0), Imp3D 320.
+uint32_t halo_chunk_cap(uint32_t g, bool imp3d) {
+    const uint64_t n = (uint64_t)g * g;
+    double best = 0.0, mu = 0.0, var = 0.0;
+    for (uint64_t i = 0; i <= n; ++i) {
+        if (i == n || (i % HALO_CHUNK == 0 && i > 0)) {
+            best = std::max(best, mu + 12.0 * std::sqrt(var));
+            mu = var = 0.0;
+            if (i == n) break;
+        }
+        const uint32_t y = (uint32_t)(i / g), z = (uint32_t)(i % g);
+        const uint32_t deg = 2u + (y > 0) + (y + 1 < g) + (z > 0) + (z + 1 < g) + (imp3d ? 1u : 0u);
+        const double p = 1.0 / deg;
+        mu += p;
+        var += p * (1.0 - p);
+    }
+    const uint32_t c = (uint32_t)std::ceil(best);
+    return std::min<uint32_t>(HALO_CHUNK, std::max<uint32_t>(8u, (c + 7u) & ~7u));
+}
 hipError_t launch_gather_keys(const uint32_t* key, const uint32_t* src, uint32_t n, uint32_t* out, int grid,
                               hipStream_t st) {
     if (n) hipLaunchKernelGGL(k_gather_keys, dim3(grid), dim3(256), 0, st, key, src, n, out);
@@ -754,21 +742,3 @@ hipError_t launch_expect(const ExpectArgs& a, int grid, hipStream_t st) {
 
 }  // namespace gp
 
-#if GP_LP_STAMPS
-// Experiments build, diagnostics: mean cycles (s_memtime) per k_list_pack block of its phases
-// since the last reset: LDS init, wave 0's tile (loads, bitmap, scans), the wait for the
-// block's other tiles, the reservations, wave 0's header words, wave 0's headers + payloads;
-// out[6] = blocks counted.
-extern "C" int gp_debug_lp_stamps(double* out, int reset) {
-    unsigned long long h[8] = {0};
-    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(gp::gp_lp_stamp_acc), sizeof(h)) != hipSuccess) return -3;
-    const double n = h[6] ? (double)h[6] : 1.0;
-    for (int q = 0; q < 6; ++q) out[q] = (double)h[q] / n;
-    out[6] = (double)h[6];
-    if (reset) {
-        unsigned long long z[8] = {0};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(gp::gp_lp_stamp_acc), z, sizeof(z)) != hipSuccess) return -3;
-    }
-    return 0;
-}
-#endif

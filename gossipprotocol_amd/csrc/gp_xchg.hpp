@@ -168,19 +168,24 @@ struct BitsEndsArgs {         // this rank's encodings
 
 // Push-sum halo planes over several ranks (3D / Imp3D): a neighbour's round kernel reads the
 // (s, w) of a halo node only when that node sends to it (its direction byte, which travels in
-// full), so only those (s, w) travel -- ~1/7 of the plane, compacted per 1024-node chunk into
-// HALO_CAP slots (mean 146 at 1/7, 171 at 1/6; 256 is > 7 sigma; a fuller chunk sets the
-// overflow flag).  k_halo_pack on the sender, k_halo_expand into the receiver's halo plane.
-constexpr uint32_t HALO_CHUNK = 1024, HALO_CAP = 256;
+// full), so only those (s, w) travel, compacted per 1024-node chunk into `cap` slots (a fuller
+// chunk sets the overflow flag).  k_halo_pack on the sender, k_halo_expand into the receiver's
+// halo plane.  The capacity is sized for the lattice's worst chunk (halo_chunk_cap): a node of
+// degree d sends toward the neighbour with probability 1/d, so a chunk made of a plane's
+// boundary row y = 0 (3D: degree 5; Imp3D: 6) expects 205 / 171 senders where an interior
+// chunk expects 146 (Imp3D) -- 12 sigma over the worst, as the other exchange buffers.
+constexpr uint32_t HALO_CHUNK = 1024;
 struct HaloArgs {
     const uint8_t* nb;      // direction bytes of the plane's nodes
     double2* sw;            // the plane's (s, w): read by the pack, written by the expand
-    double2* buf;           // [chunk * HALO_CAP + rank]: the senders' (s, w), in id order per chunk
+    double2* buf;           // [chunk * cap + rank]: the senders' (s, w), in id order per chunk
     uint32_t n;             // nodes in the plane
+    uint32_t cap;           // slots per chunk
     uint32_t dir;           // the direction whose senders' (s, w) travel
     unsigned int* overflow;
 };
-inline size_t halo_buf_slots(uint32_t n) { return (size_t)((n + HALO_CHUNK - 1) / HALO_CHUNK) * HALO_CAP; }
+inline size_t halo_buf_slots(uint32_t n, uint32_t cap) { return (size_t)((n + HALO_CHUNK - 1) / HALO_CHUNK) * cap; }
+uint32_t halo_chunk_cap(uint32_t g, bool imp3d);
 hipError_t launch_halo_pack(const HaloArgs& a, hipStream_t st);
 hipError_t launch_halo_expand(const HaloArgs& a, hipStream_t st);
 

@@ -107,7 +107,12 @@ def test_product_library_has_no_environment_switches():
     test overrides live only in the experiments build (-DGP_EXPERIMENTS)."""
     prod = open(L.LIB_PATH, "rb").read()
     exp = open(os.path.join(os.path.dirname(L.LIB_PATH), "libgossip_hip_exp.so"), "rb").read()
-    for knob in (b"GP_KERNEL", b"GP_GRID", b"GP_XSEGS", b"GP_WALK", b"GP_WX", b"GP_STAGE_CAP", b"GP_NO_PACK",
-                 b"GP_FORCE_RCCL", b"GP_XCAP", b"GP_WIDE", b"GP_RQ8"):
+    for knob in (b"GP_KERNEL", b"GP_XSEGS", b"GP_WALK", b"GP_WX", b"GP_STAGE_CAP", b"GP_NO_PACK",
+                 b"GP_FORCE_RCCL", b"GP_XCAP", b"GP_WIDE", b"GP_RQ8", b"GP_CHECK_CLOSE", b"GP_FUSE",
+                 b"GP_RREGIONS", b"GP_FB_FUSED", b"GP_IND4_WIDE"):
         assert knob not in prod, knob
         assert knob in exp, knob
+    # overrides of variants measured and rejected are gone from both builds (round 6)
+    for knob in (b"GP_PSTREAM", b"GP_XREGIONS", b"GP_XHALVES", b"GP_HALO_FULL", b"GP_RLAST", b"GP_FB_S1D",
+                 b"GP_FOLD_BLOCKS", b"GP_GRID"):
+        assert knob not in prod and knob not in exp, knob

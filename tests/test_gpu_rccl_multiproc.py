@@ -100,17 +100,12 @@ def test_rccl_processes_match_single(world, n, topo, alg, seed, rounds):
     assert all(a + c == b for (a, c), (b, _) in zip(firsts, firsts[1:]))
 
 
-_MPROC_FULL = pytest.mark.skipif(
-    os.environ.get("GP_MPROC_FULL") != "1",
-    reason="BASELINE sizes over the socket transport (minutes; scripts/gpu_r3_mproc.sh sets GP_MPROC_FULL=1)")
-
-
 @pytest.mark.parametrize("world,n,topo,alg,rounds", [
-    # C5, the headline workload sharded: always in the -m gpu suite (~40 s), so the
-    # driver's own run sees the two-rank path bit-exact at 1e9
-    (2, 10**9, "Imp3D", "push-sum", 140),   # past activation into steady state
-    pytest.param(2, 10**8, "full", "push-sum", 60, marks=_MPROC_FULL),   # C4: the two-half exchange
-    pytest.param(2, 10**8, "Imp3D", "gossip", 100, marks=_MPROC_FULL),   # C3: counts + halo planes
+    # the BASELINE configurations that shard, each as two rank processes at its full size, in the
+    # default -m gpu suite (~70 s together), so the driver's own run sees them bit-exact
+    (2, 10**9, "Imp3D", "push-sum", 140),   # C5, the headline: past activation into steady state
+    (2, 10**8, "full", "push-sum", 60),     # C4: the two-half exchange
+    (2, 10**8, "Imp3D", "gossip", 100),     # C3: counts as bitmaps + halo planes
 ])
 def test_rccl_processes_baseline_size(world, n, topo, alg, rounds):
     """BASELINE configurations as rank processes: per-round alerts and an xxh3-128 digest of every

@@ -210,3 +210,44 @@ def test_fused_full_bin_plan_fits(P):
     assert nb1 >= nb1_rule  # one size smaller bins (more of them), unless the 1024 cap binds
     if P == 100000001:
         assert (nb1, nb1_rule) == (191, 96)
+
+
+def halo_chunk_cap(g, imp3d):
+    """gp_xchg.hip halo_chunk_cap: the senders toward one x neighbour in a 1024-node chunk of a
+    slab-boundary plane are a sum of Bernoulli(1 / deg); the largest mean + 12 sigma over the
+    plane's chunks, rounded up to 8."""
+    y, z = np.divmod(np.arange(g * g), g)
+    deg = 2 + (y > 0) + (y < g - 1) + (z > 0) + (z < g - 1) + (1 if imp3d else 0)
+    p = 1.0 / deg
+    best = 0.0
+    for c0 in range(0, g * g, 1024):
+        q = p[c0:c0 + 1024]
+        best = max(best, q.sum() + 12.0 * math.sqrt((q * (1 - q)).sum()))
+    return min(1024, max(8, (math.ceil(best) + 7) // 8 * 8)), p
+
+
+def poisson_binomial_tail(q, k):
+    """P(sum of Bernoulli(q_i) > k), exactly (dynamic programme over the chunk's nodes)."""
+    dist = np.zeros(len(q) + 2)
+    dist[0] = 1.0
+    for n, qi in enumerate(q):
+        dist[1:n + 2] = dist[1:n + 2] * (1 - qi) + dist[0:n + 1] * qi
+        dist[0] *= 1 - qi
+    return float(dist[k + 1:].sum())
+
+
+@pytest.mark.parametrize("g,imp3d", [(1000, False), (1000, True), (465, True), (100, False), (1625, False)])
+def test_halo_chunk_capacity_covers_boundary_rows(g, imp3d):
+    """A chunk made of a plane's boundary row (y = 0: degree 5 on 3D, 6 on Imp3D) sends toward
+    x -+ 1 with probability 1/5 (1/6), not the interior 1/7: round 5's fixed 256 slots overflowed
+    with probability ~3e-5 per chunk and round on 3D at g = 1000 (a loud but spurious GP_ESTATE).
+    The capacity rule keeps every chunk's exact overflow probability negligible over a
+    convergence run (every round, both directions, every slab boundary)."""
+    cap, p = halo_chunk_cap(g, imp3d)
+    worst = max(poisson_binomial_tail(p[c0:c0 + 1024], cap) for c0 in (0, 1024, (g * g // 1024) * 1024 - 1024))
+    assert worst < 1e-25
+    if g == 1000:
+        assert cap == (360 if not imp3d else 320)
+        row0 = p[0:1024]
+        if not imp3d:
+            assert 3e-5 < poisson_binomial_tail(row0, 256) < 4e-5  # the round-5 capacity

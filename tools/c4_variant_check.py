@@ -1,4 +1,4 @@
-"""Full push-sum parity of the experiments build under the current GP_* knobs (e.g. GP_FB_S1D):
+"""Full push-sum parity of the experiments build under the current GP_* overrides (e.g. GP_FB_FUSED=0):
 small populations against the C oracle through convergence, and P = 1e8 against the product
 library (itself oracle-checked at that size, tests/test_gpu_baseline_sizes.py) state for state."""
 import os
