@@ -111,7 +111,8 @@ def measure_traffic(args):
 
 
 def cpu_baseline(args):
-    """SRS v1 C oracle on the host cores, steady-state rounds, bounded to ~cpu_seconds.
+    """SRS v1 C oracle on the host cores, steady-state rounds: at least cpu_rounds (3) and
+    ~cpu_seconds.
 
     Default sample: the benchmarked workload itself (--nodes, P = 1e9 for C5).  The
     activation pre-roll at that size would take minutes of full-population passes, so
@@ -149,7 +150,7 @@ def cpu_baseline(args):
     t_setup = time.perf_counter() - t0
     log(f"[bench] cpu baseline: oracle P={P} ready ({t_setup:.1f} s, {threads} threads)")
     rounds, t = 0, 0.0
-    while (t < args.cpu_seconds or rounds == 0) and rounds < 400:
+    while (t < args.cpu_seconds or rounds < args.cpu_rounds) and rounds < 400:
         t1 = time.perf_counter()
         rounds += len(orc.step(1 if direct else 2))
         t += time.perf_counter() - t1
@@ -226,6 +227,8 @@ def main():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-nodes", type=int, default=0, help="CPU-baseline sample size (0: --nodes)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-rounds", type=int, default=3,
+                    help="CPU-baseline rounds at least (a 10^9-node round takes ~16 s on 256 cores)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU-baseline OpenMP threads (0: every core in the scheduler affinity mask)")
     ap.add_argument("--no-cpu", action="store_true")

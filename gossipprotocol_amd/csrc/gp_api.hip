@@ -123,6 +123,12 @@ struct Slab {
     size_t xr_stride = 0;              // the receive buffer of odd rounds at xrecv + xr_stride (region-by-region
                                        // rounds: the next round's lists arrive during this one), else 0
     std::vector<uint32_t> vbase;       // [h * W + d]: index of my chunk's first slot in d's vals region
+    // full push-sum over several ranks: this rank's own share of region h's bins, by round parity:
+    // parity 0 in xrecv (its receive region from itself), parity 1 in xown -- the fold of round r
+    // fills parity r + 1 while the split of round r has read parity r, and a round's counters are
+    // all cleared at its start (launch_round_full_multi)
+    uint8_t* xown = nullptr;
+    size_t ooff[FB_REGIONS] = {};
     // Imp3D gossip (column kernel) over several ranks: random-edge sends as bitmaps (gp_xchg.hpp)
     bool bits = false;
     uint32_t* rbits_in = nullptr;      // receive bitmap: source a's chunk at bit ro[a]
@@ -161,6 +167,7 @@ struct gp_sim {
     int device = 0;
     hipStream_t stream = nullptr;
     int grid = 1;
+    int cus = 1;  // compute units of the device
     int64_t P = 0, T = 0, g = 0;
     int mode = MODE_SINGLE;
     int world = 1, rank = 0;  // ranks sharing the population; this process's rank (RCCL)
@@ -364,21 +371,38 @@ int alloc_slab(gp_sim* s, Slab& sl, int r) {
         }
     }
     if (S.topo == FULL && S.alg == PUSHSUM) {  // LDS-binned message staging of this rank's receivers (gp_fullbin.hip)
-        // one rank: the fold of round r bins round r+1's messages (k_fb_fold<true>)
-        bool fused = s->world == 1;
-        if (const char* e = exp_env("GP_FB_FUSED")) fused = fused && e[0] == '1';  // A/B: three passes
-        const FullBinPlan fp = full_bin_plan(S.nloc, fused);
-        S.fb_s1 = fp.s1;
-        S.fb_nb1 = fp.nb1;
+        const FullBinPlan fp = full_bin_plan(S.nloc, W == 1);
         S.fb_nb2 = fp.nb2;
-        S.fb_cap1 = fp.cap1;
         S.fb_cap2 = fp.cap2;
-        S.fb_fused = fused && fp.nb1 <= full_bin_fused_max_bins() ? 1u : 0u;
-        const size_t m1 = (size_t)fp.nb1 * fp.cap1, m2 = (size_t)fp.nb2 * fp.cap2;
-        if ((rc = dev_alloc_t(s, &S.fb_cnt1, fp.nb1)) || (rc = dev_alloc_t(s, &S.fb_cnt2, fp.nb2)) ||
-            (rc = dev_alloc_t(s, &S.fb_hdr1, m1)) || (rc = dev_alloc_t(s, &S.fb_pay1, m1)) ||
-            (rc = dev_alloc_t(s, &S.fb_hdr2, m2)) || (rc = dev_alloc_t(s, &S.fb_pay2, m2)))
+        const size_t m2 = (size_t)fp.nb2 * fp.cap2;
+        if ((rc = dev_alloc_t(s, &S.fb_cnt2, fp.nb2)) || (rc = dev_alloc_t(s, &S.fb_hdr2, m2)) ||
+            (rc = dev_alloc_t(s, &S.fb_pay2, m2)))
             return rc;
+        if (W == 1) {
+            // one rank: coarse bins hdr1 / pay1; the fold of round r bins round r+1's messages
+            // into them (k_fb_fold<FOLD_SEND>; GP_FB_FUSED=0, experiments: three passes)
+            bool fused = true;
+            if (const char* e = exp_env("GP_FB_FUSED")) fused = e[0] == '1';
+            const FullBinPlan f1 = full_bin_plan(S.nloc, fused);
+            S.fb_s1 = f1.s1;
+            S.fb_nb1 = f1.nb1;
+            S.fb_cap1 = f1.cap1;
+            S.fb_fused = fused && f1.nb1 <= full_bin_fused_max_bins() ? 1u : 0u;
+            const size_t m1 = (size_t)f1.nb1 * f1.cap1;
+            if ((rc = dev_alloc_t(s, &S.fb_cnt1, f1.nb1)) || (rc = dev_alloc_t(s, &S.fb_hdr1, m1)) ||
+                (rc = dev_alloc_t(s, &S.fb_pay1, m1)))
+                return rc;
+        } else {
+            // several ranks (round 6): the coarse bins are the exchange buffers (setup_exchange) --
+            // the fold bins the next round's messages by destination rank and coarse bin into them,
+            // and each rank's split reads them where they arrive (k_fb_fold<FOLD_SEND_RANKS>)
+            S.fb_s1 = full_bin_multi_s1(s->bounds.data(), W);
+            S.fb_nb1 = (uint32_t)(((uint64_t)S.nloc + (1ull << S.fb_s1) - 1) >> S.fb_s1);
+            S.fb_cap1 = 0;
+            S.fb_fused = 1;
+            S.fb_cnt1 = S.fb_hdr1 = nullptr;
+            S.fb_pay1 = nullptr;
+        }
     }
     if (col_gossip_counts(S)) {  // senders count their random-edge deliveries at the target (k_gossip_col)
         // byte counters, four per word (C3: 0.632 -> 0.600 ms per round, reads 16.5 -> 11.7 and
@@ -451,7 +475,7 @@ constexpr uint32_t RREG_MIN_NODES = 1u << 24;  // region rounds from this slab s
 
 // Exchange regions of a slab's senders: push-sum runs two (one's transfer overlaps the
 // other's packing), gossip one.  Imp3D push-sum cuts them at a tile boundary (the lists'
-// tiles); the full topology at the slab's middle id.
+// tiles); the full topology at a fine-tile boundary (full_region).
 int exchange_regions(const gp_sim* s) {
     const bool push = s->cfg.algorithm == GP_PUSHSUM;
     // Imp3D push-sum lists: XREGIONS regions of the slab's tiles (the last one's transfer is what
@@ -459,7 +483,7 @@ int exchange_regions(const gp_sim* s) {
     // regions, where one link carries half of every rank's messages -- C5, region rounds, same box
     // (profiles/r05/rregions/reg8.txt): W = 2 10.72 -> 10.21 ms at 128 GB/s, 12.53 -> 11.50 at
     // 64; at W = 4 and 8 eight were slower (5.50 -> 5.69, 2.82 -> 3.00 ms at 128 GB/s)
-    int NH = push ? (s->cfg.topology == GP_IMP3D ? XREGIONS : 2) : 1;
+    int NH = push ? (s->cfg.topology == GP_IMP3D ? XREGIONS : FB_REGIONS) : 1;
     if (push && s->cfg.topology == GP_IMP3D && s->world == 2 && s->bounds.size() == 3 &&
         std::min(s->bounds[1] - s->bounds[0], s->bounds[2] - s->bounds[1]) >= RREG_MIN_NODES)
         NH = 8;
@@ -490,6 +514,18 @@ uint32_t round_regions(const gp_sim* s, int kernel, uint32_t walk) {
     for (int w = 0; w < s->world; ++w)
         if (!region_tiles(s->bounds[w], s->bounds[w + 1] - s->bounds[w], (uint64_t)s->g * s->g, NH, rb)) return 1;
     return (uint32_t)NH;
+}
+
+// Full-topology push-sum over several ranks: region h of NH of a slab is its fine tiles
+// [t0, t1) (2^FB_TB local ids each, counted from lo) -- the fold of those tiles bins their
+// next-round messages into region h's exchange buffers -- whose senders are the local ids
+// [s0, s1).
+void full_region(uint32_t nloc, int NH, int h, uint32_t& t0, uint32_t& t1, uint32_t& s0, uint32_t& s1) {
+    const uint32_t nt = (uint32_t)(((uint64_t)nloc + (1u << FB_TB) - 1) >> FB_TB);
+    t0 = (uint32_t)((uint64_t)nt * h / NH);
+    t1 = (uint32_t)((uint64_t)nt * (h + 1) / NH);
+    s0 = (uint32_t)std::min<uint64_t>(nloc, (uint64_t)t0 << FB_TB);
+    s1 = (uint32_t)std::min<uint64_t>(nloc, (uint64_t)t1 << FB_TB);
 }
 
 uint32_t slab_tiles(uint32_t lo, uint32_t nloc) {
@@ -873,19 +909,30 @@ int setup_exchange(gp_sim* s) {
     unsigned long long* n = nullptr;
     HIP_TRY(tmp_mem.alloc(&mu, XMAXW));
     HIP_TRY(tmp_mem.alloc(&n, XMAXW));
+    // full push-sum: the coarse bins of every destination travel as the exchange buffers
+    // (FbBins, gp_fullbin.hpp); the coarse-bin size every rank uses, and a rank's bin count
+    const uint32_t fs1 = full && push ? full_bin_multi_s1(s->bounds.data(), W) : 0;
+    auto fnb = [&](int b) { return (uint32_t)(((uint64_t)s->bounds[b + 1] - s->bounds[b] + (1ull << fs1) - 1) >> fs1); };
     if (full) {
-        // every active sender picks a uniform target among P-1: messages a -> b from a's half h are
-        // at most Binomial(na_h, nb / (P-1)); a function of the slab bounds only, so every rank
-        // computes the whole table
+        // every active sender picks a uniform target among P-1: a function of the slab bounds
+        // only, so every rank computes the whole table
         for (int a = 0; a < W; ++a) {
             const uint32_t na = s->bounds[a + 1] - s->bounds[a];
             for (int h = 0; h < NH; ++h) {
-                const double nah = (double)(NH == 1 ? na : h == 0 ? na / 2 : na - na / 2);
+                uint32_t t0, t1, s0, s1;
+                full_region(na, NH, h, t0, t1, s0, s1);
+                const double nah = (double)(s1 - s0);
                 for (int b = 0; b < W; ++b) {
-                    // push-sum: a rank's messages to itself also pass through a buffer (its
-                    // own receive buffer, gp_fullbin.hip k_fbm_send)
-                    if (b == a && !push) continue;
-                    const double nb = (double)(s->bounds[b + 1] - s->bounds[b]) - (b == a ? 1.0 : 0.0);
+                    if (push) {
+                        // push-sum: messages from a's region h to one coarse bin of b (2^fs1
+                        // receivers; a rank's messages to itself included, they pass through its
+                        // own receive buffer) are at most Binomial(na_h, 2^fs1 / (P-1))
+                        caps[((size_t)h * W + a) * W + b] = full_bin_multi_cap(s1 - s0, fs1, (uint32_t)s->P);
+                        continue;
+                    }
+                    // gossip: messages a -> b at most Binomial(na, nb / (P-1))
+                    if (b == a) continue;
+                    const double nb = (double)(s->bounds[b + 1] - s->bounds[b]);
                     const double m = nah * nb / (double)(s->P - 1);
                     const double c = std::ceil(m + 12.0 * std::sqrt(m) + 64.0);
                     caps[((size_t)h * W + a) * W + b] = (uint32_t)std::min(c, nah);
@@ -1023,15 +1070,25 @@ int setup_exchange(gp_sim* s) {
                 sl.cap_out[i] = caps[((size_t)h * W + a) * W + b];
                 sl.cap_in[i] = caps[((size_t)h * W + b) * W + a];
                 sl.soff[i] = so;
-                sl.sbytes[i] = b == a ? 0 : xbuf_bytes(sl.cap_out[i], push);  // own messages: straight to xrecv
+                // (own messages: straight to xrecv; full push-sum: b's coarse bins, FbBins)
+                sl.sbytes[i] = b == a ? 0 : full && push ? fb_bins_bytes(fnb(b), sl.cap_out[i]) : xbuf_bytes(sl.cap_out[i], push);
                 so += sl.sbytes[i];
                 sl.roff[i] = ro;
-                sl.rbytes[i] = xbuf_bytes(sl.cap_in[i], push);
+                sl.rbytes[i] = full && push ? fb_bins_bytes(fnb(a), sl.cap_in[i]) : xbuf_bytes(sl.cap_in[i], push);
                 ro += sl.rbytes[i];
             }
         if ((rc = dev_alloc_t(s, &sl.xsend, so)) || (rc = dev_alloc_t(s, &sl.xrecv, ro))) return rc;
         HIP_TRY(hipMemsetAsync(sl.xsend, 0, so ? so : 16, s->stream));
         HIP_TRY(hipMemsetAsync(sl.xrecv, 0, ro ? ro : 16, s->stream));
+        if (full && push) {  // the own share's second parity (Slab::xown)
+            size_t oo = 0;
+            for (int h = 0; h < NH && h < FB_REGIONS; ++h) {
+                sl.ooff[h] = oo;
+                oo += sl.rbytes[(size_t)h * W + a];
+            }
+            if ((rc = dev_alloc_t(s, &sl.xown, oo))) return rc;
+            HIP_TRY(hipMemsetAsync(sl.xown, 0, oo ? oo : 16, s->stream));
+        }
         sl.overflow = &sl.S.ctl->overflow;
     }
     if (NH > 1) {  // the second stream and the events that order it with the compute stream
@@ -1100,13 +1157,22 @@ FullArgs make_full_args(gp_sim* s, Slab& sl, uint32_t round) {
 }
 
 // Push-sum on the full topology, one rank of several (gp_fullbin.hip): this
-// rank's receivers [lo, lo + nloc), node arrays indexed by id - lo, region h of
-// the exchange buffers as the destination-rank bins of k_fbm_send (senders of
-// half h) and the sources of k_fbm_coarse.
-FullBinArgs make_fullbin_args(gp_sim* s, Slab& sl, uint32_t round, int h) {
+// rank's receivers [lo, lo + nloc), node arrays indexed by id - lo; exchange region h:
+// the fold's tiles and senders (full_region), the bins it sends to every rank (out;
+// its own share into its own receive region) and the bins received from every rank (in).
+// This rank's own share of region h's bins, round parity `par` (Slab::xown).
+FbBins own_bins(gp_sim* s, Slab& sl, int h, uint32_t par) {
+    const size_t i = (size_t)h * s->world + sl.rank;
+    uint8_t* base = par & 1u ? sl.xown + sl.ooff[h] : sl.xrecv + sl.roff[i];
+    return fb_bins_at(base, sl.S.fb_nb1, sl.cap_in[i]);
+}
+
+// send_pass: round 0's send pass fills this round's own bins (the fold fills the next round's).
+FullBinArgs make_fullbin_args(gp_sim* s, Slab& sl, uint32_t round, int h, bool send_pass = false) {
     DevState& S = sl.S;
     const int cur = round & 1;
     const uint32_t d = S.lo - S.base;
+    const int W = s->world;
     FullBinArgs a{};
     a.swc = S.sw[cur] + d;
     a.swn = S.sw[cur ^ 1] + d;
@@ -1119,40 +1185,39 @@ FullBinArgs make_fullbin_args(gp_sim* s, Slab& sl, uint32_t round, int h) {
     a.s1 = S.fb_s1;
     a.nb1 = S.fb_nb1;
     a.nb2 = S.fb_nb2;
-    a.cap1 = S.fb_cap1;
     a.cap2 = S.fb_cap2;
-    a.cnt1 = S.fb_cnt1;
     a.cnt2 = S.fb_cnt2;
-    a.hdr1 = S.fb_hdr1;
-    a.pay1 = S.fb_pay1;
     a.hdr2 = S.fb_hdr2;
     a.pay2 = S.fb_pay2;
     a.lo = S.lo;
     a.nloc = S.nloc;
-    const int NH = s->xhalves;
-    a.s_lo = NH == 1 || h == 0 ? 0u : S.nloc / 2;
-    a.s_hi = NH == 1 || h == 1 ? S.nloc : S.nloc / 2;
-    a.W = s->world;
+    full_region(S.nloc, s->xhalves, h, a.t_lo, a.t_hi, a.s_lo, a.s_hi);
+    a.fused = 1;
+    a.W = W;
     a.me = sl.rank;
-    for (int w = 0; w <= s->world; ++w) a.bounds[w] = s->bounds[w];
+    for (int w = 0; w <= W; ++w) a.bounds[w] = s->bounds[w];
     const uint32_t item = full_bin_item_messages();
     a.in_item0[0] = 0;
-    for (int p = 0; p < s->world; ++p) {
-        const size_t i = (size_t)h * s->world + p;
-        a.in[p] = xpeer(sl.xrecv, sl.roff[i], sl.cap_in[i]);
-        a.out[p] = p == sl.rank ? a.in[p] : xpeer(sl.xsend, sl.soff[i], sl.cap_out[i]);
-        a.in_item0[p + 1] = a.in_item0[p] + (item ? (sl.cap_in[i] + item - 1) / item : 0u);
+    for (int p = 0; p < W; ++p) {
+        const size_t i = (size_t)h * W + p;
+        const uint32_t nbp = (uint32_t)(((uint64_t)s->bounds[p + 1] - s->bounds[p] + (1ull << S.fb_s1) - 1) >> S.fb_s1);
+        a.in[p] = p == sl.rank ? own_bins(s, sl, h, round) : fb_bins_at(sl.xrecv + sl.roff[i], S.fb_nb1, sl.cap_in[i]);
+        a.out[p] = p == sl.rank ? own_bins(s, sl, h, send_pass ? round : round + 1)
+                                : fb_bins_at(sl.xsend + sl.soff[i], nbp, sl.cap_out[i]);
+        a.in_item0[p + 1] = a.in_item0[p] + (sl.cap_in[i] ? S.fb_nb1 * ((sl.cap_in[i] + item - 1) / item) : 0u);
     }
     return a;
 }
 
 // Full topology on several ranks: one round (push-sum gp_fullbin.hip, gossip gp_full.hip).
-// Push-sum runs as a two-stage pipeline: the senders' first half is binned by
-// destination and handed to the exchange stream (xstream), whose transfer
-// overlaps the second half's binning; the receivers bin half 0's messages by
-// coarse bin while half 1 is in flight, then half 1's, then split and fold.
-// Events order the two streams; every RCCL operation stays serialised in one
-// order on every rank (group half 0, group half 1, then the finalize all-reduce).
+// Push-sum (round 6): the messages of round r reach this rank as the coarse bins of its
+// receivers in the exchange buffers of every region and source, where the split reads them;
+// the fold then runs region by region, and region h's fold bins its tiles' round-(r+1)
+// messages by destination rank and coarse bin straight into region h's buffers, which travel
+// (exchange stream, one RCCL group) while the next region's fold runs.  Round 0's messages
+// come from the send pass (only the seed sends).  Events order the streams; every RCCL
+// operation is issued in one order on every rank (group region 0, 1, then the finalize
+// all-reduce, which waits for the last group).
 int launch_round_full_multi(gp_sim* s, uint32_t r, hipEvent_t e0, hipEvent_t e1) {
     const bool push = s->cfg.algorithm == GP_PUSHSUM;
     int rc;
@@ -1160,30 +1225,59 @@ int launch_round_full_multi(gp_sim* s, uint32_t r, hipEvent_t e0, hipEvent_t e1)
     if (push) {
         const int NH = s->xhalves;
         hipStream_t xs = s->xstream ? s->xstream : s->stream;
-        for (int h = 0; h < NH; ++h) {
-            for (Slab& sl : s->slab) {
-                const FullBinArgs a = make_fullbin_args(s, sl, r, h);
-                ZeroArgs z{};
-                for (int p = 0; p < s->world; ++p) z.cnt[p] = a.out[p].cnt;
-                z.n = s->world;
-                HIP_TRY(launch_zero_counts(z, s->stream));
-                HIP_TRY(launch_full_bin_send_multi(a, r, s->stream));
-            }
+        auto send_region = [&](int h) -> int {  // region h's buffers to the exchange stream
             if (xs != s->stream) {
                 HIP_TRY(hipEventRecord(s->ev_send[h], s->stream));
                 HIP_TRY(hipStreamWaitEvent(xs, s->ev_send[h], 0));
             }
-            if ((rc = transfer_xbufs(s, h, xs))) return rc;
+            int rc2;
+            if ((rc2 = transfer_xbufs(s, h, xs))) return rc2;
             if (xs != s->stream) HIP_TRY(hipEventRecord(s->ev_xfer[h], xs));
+            return GP_OK;
+        };
+        // the counters this round fills, in one launch: the fine tiles', every region's send bins'
+        // (their last transfer is done: finalize waited for it), the own next-round bins' (the
+        // split of round r - 1 read them); round 0 also this round's own bins, for the send pass
+        // (zero_send: the send bins alone -- round 0's send pass has used them once already)
+        auto zero_counts = [&](bool zero_send) -> int {
+            for (Slab& sl : s->slab) {
+                ZeroList z{};
+                auto add = [&](uint32_t* p, uint32_t n) {
+                    if (p && n && z.k < ZeroList::MAX) {
+                        z.p[z.k] = p;
+                        z.n[z.k++] = n;
+                    }
+                };
+                if (!zero_send) add(sl.S.fb_cnt2, sl.S.fb_nb2);
+                for (int h = 0; h < NH; ++h) {
+                    const FullBinArgs a = make_fullbin_args(s, sl, r, h);
+                    for (int p = 0; p < s->world; ++p)
+                        if (p != sl.rank || !zero_send) add(a.out[p].cnt, a.out[p].nb);  // (own: next parity)
+                    if (r == 0 && !zero_send) add(a.in[sl.rank].cnt, a.in[sl.rank].nb);
+                }
+                HIP_TRY(launch_zero_list(z, s->stream));
+            }
+            return GP_OK;
+        };
+        if ((rc = zero_counts(false))) return rc;
+        if (r == 0) {  // round 0's messages: the send pass
+            for (int h = 0; h < NH; ++h) {
+                for (Slab& sl : s->slab) HIP_TRY(launch_full_bin_send_multi(make_fullbin_args(s, sl, r, h, true), r, s->stream));
+                if ((rc = send_region(h))) return rc;
+            }
         }
-        for (Slab& sl : s->slab) HIP_TRY(launch_full_bin_recv_reset(make_fullbin_args(s, sl, r, 0), s->stream));
-        for (int h = 0; h < NH; ++h) {
+        for (int h = 0; h < NH; ++h) {  // region h's bins into the fine tiles once they are here
             if (xs != s->stream) HIP_TRY(hipStreamWaitEvent(s->stream, s->ev_xfer[h], 0));
-            for (Slab& sl : s->slab) HIP_TRY(launch_full_bin_coarse(make_fullbin_args(s, sl, r, h), r, s->stream));
+            for (Slab& sl : s->slab) HIP_TRY(launch_full_bin_split_multi(make_fullbin_args(s, sl, r, h), r, s->stream));
         }
-        for (Slab& sl : s->slab)
-            HIP_TRY(launch_full_bin_split_fold(make_fullbin_args(s, sl, r, 0), r, s->grid, s->stream));
+        if (r == 0 && (rc = zero_counts(true))) return rc;  // (the send pass's transfers are done)
+        for (int h = 0; h < NH; ++h) {  // the fold, region by region; round r+1's messages travel behind it
+            for (Slab& sl : s->slab)
+                HIP_TRY(launch_full_bin_fold_multi(make_fullbin_args(s, sl, r, h), r, s->cus, s->stream));
+            if ((rc = send_region(h))) return rc;
+        }
         if (e1) HIP_TRY(hipEventRecord(e1, s->stream));
+        if (xs != s->stream) HIP_TRY(hipStreamWaitEvent(s->stream, s->ev_xfer[NH - 1], 0));
         return finalize(s, r, r + 1);
     }
     for (Slab& sl : s->slab) {
@@ -1587,6 +1681,7 @@ void choose_kernel(gp_sim* s, int64_t nloc_max, int& kernel, uint32_t& col_xsegs
                    uint32_t& wide) {
     hipDeviceProp_t prop;
     (void)hipGetDeviceProperties(&prop, s->device);
+    s->cus = std::max(1, prop.multiProcessorCount);
     const gp_config* cfg = &s->cfg;
     const int64_t g = s->g;
     int64_t blocks = (nloc_max + BULK_THREADS - 1) / BULK_THREADS;

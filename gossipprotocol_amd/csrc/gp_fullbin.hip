@@ -294,32 +294,62 @@ __global__ __launch_bounds__(FBR_THREADS, 1) void k_fb_send(FullBinArgs a, uint3
 struct SplitIn {
     uint32_t node[FBR_PER];
     double2 pv[FBR_PER];
-    __device__ __forceinline__ void load(const FullBinArgs& a, size_t base, uint32_t c0, uint32_t q1) {
+    __device__ __forceinline__ void load(const uint32_t* hdr, const double2* pay, size_t base, uint32_t c0, uint32_t q1) {
 #pragma unroll
         for (int k = 0; k < FBR_PER; ++k) {
             const uint32_t q = min(c0 + k * FBR_THREADS + threadIdx.x, q1 - 1);
-            node[k] = a.hdr1[base + q];
-            pv[k] = a.pay1[base + q];
+            node[k] = hdr[base + q];
+            pv[k] = pay[base + q];
         }
     }
 };
 
+// One rank: work items are ranges of each coarse bin of hdr1 / pay1.  MULTI (several ranks, one
+// launch per exchange region): ranges of every source rank's bins in the region's received
+// buffers (in[p], items from in_item0[p]) -- a coarse bin's messages arrive from every source
+// and region, each range reserves its own runs in the fine tiles.
+template <bool MULTI>
 __global__ __launch_bounds__(FBR_THREADS, 1) void k_fb_split(FullBinArgs a, uint32_t r) {
     __shared__ FbRangeLds L;
     if (ld_agent(&a.ctl->done)) return;
-    const uint32_t per_bin = (a.cap1 + FBR_ITEM - 1) / FBR_ITEM;
-    const uint32_t b = blockIdx.x / per_bin, c = blockIdx.x % per_bin;
-    const uint32_t n_bin = min(ld_agent(&a.cnt1[b]), a.cap1);
+    uint32_t b, c, n_bin;
+    const uint32_t* bin_hdr;  // the coarse bins' sender ids and payloads; this bin's from ibase on
+    const double2* bin_pay;
+    size_t ibase;
+    if constexpr (MULTI) {
+        int p = 0;
+        while (p + 1 < a.W && blockIdx.x >= a.in_item0[p + 1]) ++p;  // block-uniform
+        p = __builtin_amdgcn_readfirstlane(p);
+        const uint32_t cap = a.in[p].cap;
+        if (!cap) return;
+        const uint32_t per_bin = (cap + FBR_ITEM - 1) / FBR_ITEM, item = blockIdx.x - a.in_item0[p];
+        b = item / per_bin;
+        c = item % per_bin;
+        if (b >= a.in[p].nb) return;
+        n_bin = min(ld_agent(&a.in[p].cnt[b]), cap);
+        bin_hdr = a.in[p].hdr;
+        bin_pay = a.in[p].pay;
+        ibase = (size_t)b * cap;
+    } else {
+        const uint32_t per_bin = (a.cap1 + FBR_ITEM - 1) / FBR_ITEM;
+        b = blockIdx.x / per_bin;
+        c = blockIdx.x % per_bin;
+        n_bin = min(ld_agent(&a.cnt1[b]), a.cap1);
+        bin_hdr = a.hdr1;
+        bin_pay = a.pay1;
+        ibase = (size_t)b * a.cap1;
+    }
+    // (ranges of whole items: dealing a bin's messages evenly over its items measured slower,
+    // C4 at W = 8 0.087 -> 0.095 ms per region's split -- more partly filled chunks)
     const uint32_t q0 = c * FBR_ITEM;
     if (q0 >= n_bin) return;
     const uint32_t q1 = min(n_bin, q0 + FBR_ITEM);
     const uint32_t nfine = 1u << (a.s1 - FB_TB), f0 = b << (a.s1 - FB_TB);
-    const size_t ibase = (size_t)b * a.cap1;
     uint32_t* const cnt = fbr_dyn;
     uint32_t* const base = fbr_dyn + nfine;
     for (uint32_t f = threadIdx.x; f < nfine; f += FBR_THREADS) base[f] = 0u;
     SplitIn cur;  // sweep 2's first chunk, in flight through sweep 1 and the reservations
-    cur.load(a, ibase, q0, q1);
+    cur.load(bin_hdr, bin_pay, ibase, q0, q1);
     __syncthreads();
     // sweep 1: fine tile of every message (target recomputed from the sender's
     // draw), two chunks per iteration; the tiles stay in registers for sweep 2
@@ -331,7 +361,7 @@ __global__ __launch_bounds__(FBR_THREADS, 1) void k_fb_split(FullBinArgs a, uint
         const uint32_t c0 = q0 + it * 2 * FBR_CHUNK;
         uint32_t node[P2], x[P2], y[P2];
 #pragma unroll
-        for (int k = 0; k < P2; ++k) node[k] = a.hdr1[ibase + min(c0 + k * FBR_THREADS + threadIdx.x, q1 - 1)];
+        for (int k = 0; k < P2; ++k) node[k] = bin_hdr[ibase + min(c0 + k * FBR_THREADS + threadIdx.x, q1 - 1)];
         philox2_batch<P2>(node, r, S_PUSHSUM, a.k0, a.k1, x, y);
 #pragma unroll
         for (int k = 0; k < P2; k += 2) {
@@ -369,49 +399,94 @@ __global__ __launch_bounds__(FBR_THREADS, 1) void k_fb_split(FullBinArgs a, uint
             key[k] = (keys[m / 2] >> (16 * (m & 1))) & 0xFFFFu;
             rank[k] = key[k] != FB_NONE ? atomicAdd(&cnt[key[k]], 1u) : 0u;
         }
-        cur.load(a, ibase, c0 + FBR_CHUNK < q1 ? c0 + FBR_CHUNK : c0, q1);
+        cur.load(bin_hdr, bin_pay, ibase, c0 + FBR_CHUNK < q1 ? c0 + FBR_CHUNK : c0, q1);
         lds_barrier();  // ranks counted
         fbr_emit(L, cnt, base, nfine, key, rank, node, pay, a.hdr2, a.pay2, a.cap2, f0, a.nb2, a.overflow);
     }
 }
 
 // ---------------------------------------------------------------- several ranks
-// Contiguous id slabs (gp_api.hip make_bounds); W <= XMAXW.
-__device__ __forceinline__ uint32_t owner_of(const uint32_t* bounds, int W, uint32_t t) {
-    uint32_t b = 0;
-    for (int w = 1; w < W; ++w) b += t >= bounds[w] ? 1u : 0u;
-    return b;
+// Contiguous id slabs (gp_api.hip make_bounds); W <= XMAXW.  Every rank's coarse bins
+// have the size 2^s1 (full_bin_multi_s1), so a message to target t has the LDS key
+// kb(b) + ((t - bounds[b]) >> s1), b = owner of t, kb(b) = the bins of the ranks below b:
+// key order = destination rank, then the destination's coarse bin.
+__device__ __forceinline__ uint32_t multi_key(const FullBinArgs& a, uint32_t t) {
+    uint32_t base = 0, kb = 0;
+    for (int w = 1; w < a.W; ++w)
+        if (t >= a.bounds[w]) {
+            base = a.bounds[w];
+            kb += a.out[w - 1].nb;
+        }
+    return kb + ((t - base) >> a.s1);
 }
 
-// A on several ranks: this rank's senders binned by destination rank straight
-// into the exchange buffers (slots = sender id, vals = (s/2, w/2); one counter per
-// buffer, one reservation per (range, rank)); rank me's share goes to its own
-// receive buffer.  Receivers recompute targets from the sender's Philox draw.
+constexpr uint32_t FBF_MAXB1 = 1024;  // keys (coarse bins) the fold's send phase can bin into (LDS reservation slots)
+
+// A block's destination bins, in LDS: indexing the kernel arguments by a per-lane rank
+// would be a global load per message.
+struct MultiOutLds {
+    uint32_t* cnt[XMAXW];
+    uint32_t* hdr[XMAXW];
+    double2* pay[XMAXW];
+    uint32_t cap[XMAXW];
+    uint32_t kb[XMAXW + 1];   // first key of rank b; kb[W] = keys
+    uint8_t keyb[FBF_MAXB1];  // the rank of every key
+    __device__ void init(const FullBinArgs& a) {
+        if (threadIdx.x == 0) {
+            uint32_t k = 0;
+            for (int b = 0; b < a.W; ++b) {
+                cnt[b] = a.out[b].cnt;
+                hdr[b] = a.out[b].hdr;
+                pay[b] = a.out[b].pay;
+                cap[b] = a.out[b].cap;
+                kb[b] = k;
+                k += a.out[b].nb;
+            }
+            kb[a.W] = k;
+        }
+        __syncthreads();
+        for (uint32_t q = threadIdx.x; q < kb[a.W] && q < FBF_MAXB1; q += blockDim.x) {
+            uint32_t b = 0;
+            for (int w = 1; w < a.W; ++w) b += q >= kb[w] ? 1u : 0u;
+            keyb[q] = (uint8_t)b;
+        }
+        __syncthreads();
+    }
+    // message `pos` of key q's run: false (and the overflow flag) beyond the bin's capacity
+    __device__ __forceinline__ void store(uint32_t q, uint32_t pos, uint32_t h, double2 v, unsigned int* overflow) {
+        const uint32_t b = keyb[q], c = q - kb[b];
+        if (pos >= cap[b]) {
+            atomicOr(overflow, 1u);
+            return;
+        }
+        const size_t o = (size_t)c * cap[b] + pos;
+        hdr[b][o] = h;
+        pay[b][o] = v;
+    }
+};
+
+// A on several ranks, round 0 (later rounds' messages are binned by the fold): the senders
+// lo + [s_lo, s_hi) (one exchange region) binned by key straight into the region's exchange
+// buffers -- {sender id | s/2, w/2}, one reservation per (range, key) on the bin's in-band
+// counter; rank me's share goes to its own receive region.  Receivers recompute targets from
+// the sender's Philox draw.
 __global__ __launch_bounds__(FBR_THREADS, 1) void k_fbm_send(FullBinArgs a, uint32_t r) {
     __shared__ FbRangeLds L;
-    __shared__ uint32_t* o_slots[XMAXW];
-    __shared__ double2* o_vals[XMAXW];
-    __shared__ uint32_t o_cap[XMAXW];
-    __shared__ uint32_t bnd[XMAXW + 1];
+    __shared__ MultiOutLds O;
     if (ld_agent(&a.ctl->done)) return;
     const uint32_t P = a.P;
-    const int W = a.W;
     const uint64_t i0 = (uint64_t)a.s_lo + (uint64_t)blockIdx.x * FBR_ITEM;
     if (i0 >= a.s_hi || P < 2) return;
     const uint64_t i1 = std::min<uint64_t>(a.s_hi, i0 + FBR_ITEM);
+    O.init(a);
+    const uint32_t nk = O.kb[a.W];
     uint32_t* const cnt = fbr_dyn;
-    uint32_t* const base = fbr_dyn + W;
-    if (threadIdx.x < (uint32_t)W) {
-        o_slots[threadIdx.x] = a.out[threadIdx.x].slots;
-        o_vals[threadIdx.x] = a.out[threadIdx.x].vals;
-        o_cap[threadIdx.x] = a.out[threadIdx.x].cap;
-        base[threadIdx.x] = 0u;
-    }
-    if (threadIdx.x <= (uint32_t)W) bnd[threadIdx.x] = a.bounds[threadIdx.x];
+    uint32_t* const base = fbr_dyn + nk;
+    for (uint32_t q = threadIdx.x; q < nk; q += FBR_THREADS) base[q] = 0u;
     SendIn cur;
     cur.load(a, i0, i1);
     __syncthreads();
-    // sweep 1: destination rank of every active sender, counted
+    // sweep 1: key of every active sender, counted
     for (uint64_t c0 = i0; c0 < i1; c0 += FBR_CHUNK) {
         uint32_t node[FBR_PER], x[FBR_PER], y[FBR_PER];
         uint8_t nbv[FBR_PER];
@@ -425,18 +500,16 @@ __global__ __launch_bounds__(FBR_THREADS, 1) void k_fbm_send(FullBinArgs a, uint
 #pragma unroll
         for (int k = 0; k < FBR_PER; ++k)
             if ((nbv[k] & B_ACTIVE) && c0 + k * FBR_THREADS + threadIdx.x < i1)  // Program.fs:213-215
-                atomicAdd(&base[owner_of(bnd, W, full_target(node[k], uniform_from(x[k], y[k], P - 1)))], 1u);
+                atomicAdd(&base[multi_key(a, full_target(node[k], uniform_from(x[k], y[k], P - 1)))], 1u);
     }
     __syncthreads();
-    if (threadIdx.x < (uint32_t)W) {
-        const uint32_t n = base[threadIdx.x];
-        uint32_t* c = a.out[threadIdx.x].cnt;  // null: no buffer (capacity 0)
-        base[threadIdx.x] = n && c ? atomicAdd(c, n) : 0u;
-        if (n && !c) atomicOr(a.overflow, 1u);
+    for (uint32_t q = threadIdx.x; q < nk; q += FBR_THREADS) {
+        const uint32_t n = base[q], b = O.keyb[q];
+        base[q] = n ? atomicAdd(O.cnt[b] + (q - O.kb[b]), n) : 0u;
     }
-    // sweep 2: into the buffers' runs
+    // sweep 2: into the bins' runs
     for (uint64_t c0 = i0; c0 < i1; c0 += FBR_CHUNK) {
-        if (threadIdx.x < (uint32_t)W) cnt[threadIdx.x] = 0u;
+        for (uint32_t q = threadIdx.x; q < nk; q += FBR_THREADS) cnt[q] = 0u;
         uint32_t node[FBR_PER], x[FBR_PER], y[FBR_PER], key[FBR_PER], rank[FBR_PER];
         double2 pay[FBR_PER];
 #pragma unroll
@@ -448,98 +521,26 @@ __global__ __launch_bounds__(FBR_THREADS, 1) void k_fbm_send(FullBinArgs a, uint
             key[k] = FB_NONE;
             rank[k] = 0;
             if ((cur.nbv[k] & B_ACTIVE) && c0 + k * FBR_THREADS + threadIdx.x < i1) {
-                key[k] = owner_of(bnd, W, full_target(node[k], uniform_from(x[k], y[k], P - 1)));
+                key[k] = multi_key(a, full_target(node[k], uniform_from(x[k], y[k], P - 1)));
                 rank[k] = atomicAdd(&cnt[key[k]], 1u);
             }
             pay[k] = make_double2(cur.sv[k].x * 0.5, cur.sv[k].y * 0.5);
         }
         cur.load(a, c0 + FBR_CHUNK < i1 ? c0 + FBR_CHUNK : c0, i1);
         lds_barrier();  // ranks counted
-        fbr_emit_to(L, cnt, base, (uint32_t)W, key, rank, node, pay,
-                    [&](uint32_t b, uint32_t pos, uint32_t h, double2 v) {
-                        if (pos >= o_cap[b]) {
-                            atomicOr(a.overflow, 1u);
-                            return;
-                        }
-                        o_slots[b][pos] = h;
-                        o_vals[b][pos] = v;
-                    });
+        fbr_emit_to(L, cnt, base, nk, key, rank, node, pay,
+                    [&](uint32_t q, uint32_t pos, uint32_t h, double2 v) { O.store(q, pos, h, v, a.overflow); });
     }
 }
 
-// A' on several ranks: every received message (this rank's own buffer included)
-// binned by coarse bin of its receiver ((t - lo) >> s1, the target recomputed
-// from the sender's draw) into hdr1 / pay1; then k_fb_split and k_fb_fold as on
-// one rank.  Work items: ranges of each source's buffer (in_item0).
-struct CoarseIn {
-    uint32_t node[FBR_PER];
-    double2 pv[FBR_PER];
-    __device__ __forceinline__ void load(const uint32_t* slots, const double2* vals, uint32_t c0, uint32_t q1) {
-#pragma unroll
-        for (int k = 0; k < FBR_PER; ++k) {
-            const uint32_t q = min(c0 + k * FBR_THREADS + threadIdx.x, q1 - 1);
-            node[k] = slots[q];
-            pv[k] = vals[q];
-        }
-    }
-};
-
-__global__ __launch_bounds__(FBR_THREADS, 1) void k_fbm_coarse(FullBinArgs a, uint32_t r) {
-    __shared__ FbRangeLds L;
-    if (ld_agent(&a.ctl->done)) return;
-    int p = 0;
-    while (p + 1 < a.W && blockIdx.x >= a.in_item0[p + 1]) ++p;  // block-uniform
-    p = __builtin_amdgcn_readfirstlane(p);
-    const uint32_t* __restrict__ slots = a.in[p].slots;
-    const double2* __restrict__ vals = a.in[p].vals;
-    const uint32_t cap = a.in[p].cap;
-    if (!cap) return;
-    const uint32_t n_in = min(ld_agent(a.in[p].cnt), cap);
-    const uint32_t q0 = (blockIdx.x - a.in_item0[p]) * FBR_ITEM;
-    if (q0 >= n_in) return;
-    const uint32_t q1 = min(n_in, q0 + FBR_ITEM);
-    uint32_t* const cnt = fbr_dyn;
-    uint32_t* const base = fbr_dyn + a.nb1;
-    for (uint32_t b = threadIdx.x; b < a.nb1; b += FBR_THREADS) base[b] = 0u;
-    CoarseIn cur;
-    cur.load(slots, vals, q0, q1);
-    __syncthreads();
-    for (uint32_t c0 = q0; c0 < q1; c0 += FBR_CHUNK) {
-        uint32_t node[FBR_PER], x[FBR_PER], y[FBR_PER];
-#pragma unroll
-        for (int k = 0; k < FBR_PER; ++k) node[k] = slots[min(c0 + k * FBR_THREADS + threadIdx.x, q1 - 1)];
-        philox2_batch<FBR_PER>(node, r, S_PUSHSUM, a.k0, a.k1, x, y);
-#pragma unroll
-        for (int k = 0; k < FBR_PER; ++k)
-            if (c0 + k * FBR_THREADS + threadIdx.x < q1)
-                atomicAdd(&base[(full_target(node[k], uniform_from(x[k], y[k], a.P - 1)) - a.lo) >> a.s1], 1u);
-    }
-    fbr_reserve(base, a.nb1, a.cnt1, 0, a.nb1);
-    for (uint32_t c0 = q0; c0 < q1; c0 += FBR_CHUNK) {
-        for (uint32_t b = threadIdx.x; b < a.nb1; b += FBR_THREADS) cnt[b] = 0u;
-        uint32_t node[FBR_PER], x[FBR_PER], y[FBR_PER], key[FBR_PER], rank[FBR_PER];
-        double2 pay[FBR_PER];
-#pragma unroll
-        for (int k = 0; k < FBR_PER; ++k) {
-            node[k] = cur.node[k];
-            pay[k] = cur.pv[k];
-        }
-        philox2_batch<FBR_PER>(node, r, S_PUSHSUM, a.k0, a.k1, x, y);
-        lds_barrier();  // counters zeroed
-#pragma unroll
-        for (int k = 0; k < FBR_PER; ++k) {
-            key[k] = FB_NONE;
-            rank[k] = 0;
-            if (c0 + k * FBR_THREADS + threadIdx.x < q1) {
-                key[k] = (full_target(node[k], uniform_from(x[k], y[k], a.P - 1)) - a.lo) >> a.s1;
-                rank[k] = atomicAdd(&cnt[key[k]], 1u);
-            }
-        }
-        cur.load(slots, vals, c0 + FBR_CHUNK < q1 ? c0 + FBR_CHUNK : c0, q1);
-        lds_barrier();  // ranks counted
-        fbr_emit(L, cnt, base, a.nb1, key, rank, node, pay, a.hdr1, a.pay1, a.cap1, 0, a.nb1, a.overflow);
-    }
+// Several ranks: the counters a round fills, cleared in one launch (ZeroList: block k clears
+// list entry k).
+__global__ __launch_bounds__(256) void k_zero_list(ZeroList z) {
+    uint32_t* p = z.p[blockIdx.x];
+    const uint32_t n = z.n[blockIdx.x];
+    for (uint32_t c = threadIdx.x; c < n; c += 256) p[c] = 0u;
 }
+
 // ---------------------------------------------------------------- C: fold per fine tile
 // One fine tile per block.  The tile's messages (sender id + payload) are loaded
 // in bin order, coalesced, together with the receivers' own bytes and (s, w);
@@ -550,17 +551,23 @@ __global__ __launch_bounds__(FBR_THREADS, 1) void k_fbm_coarse(FullBinArgs a, ui
 constexpr int FBF_THREADS = 1024;  // (256-thread fold blocks: 3.76 against 3.70 ms/round, profiles/r02/c4_v2/)
 
 //
-// SEND (one rank, FullBinArgs::fused): after a tile is folded, its nodes' sends of
-// round r+1 are binned straight from the registers that hold the new state --
-// the active flag and (s, w) the fold just wrote (Program.fs:104-106,125-128 one
-// round on) -- into the coarse bins of A, as k_fb_send would bin them: target
-// from the node's Philox draw for round r+1, {id | s/2, w/2}, LDS bin order
-// (reusing the fold's arrays), one reservation per (tile, bin), coalesced runs.
-// The next round then starts at B: no send pass re-reads the state (18 B/node).
-constexpr uint32_t FBF_MAXB1 = 1024;  // coarse bins the fused send can bin into (LDS reservation slots)
+// Send phase (FOLD_SEND, one rank, FullBinArgs::fused): after a tile is folded, its
+// nodes' sends of round r+1 are binned straight from the registers that hold the new
+// state -- the active flag and (s, w) the fold just wrote (Program.fs:104-106,125-128
+// one round on) -- into the coarse bins of A, as k_fb_send would bin them: target
+// from the node's Philox draw for round r+1, {id | s/2, w/2}, LDS bin order (reusing
+// the fold's arrays), one reservation per (tile, bin), coalesced runs.  The next round
+// then starts at B: no send pass re-reads the state (18 B/node).
+// FOLD_SEND_RANKS (several ranks, round 6): the same send phase with the destination
+// rank as the first level of the key (multi_key), into the exchange region's buffers
+// (out[b]) -- the fold of a region's tiles produces that region's exchange, so no send
+// pass re-reads the state and no coarse pass re-bins the received messages.
+enum FoldMode { FOLD = 0, FOLD_SEND = 1, FOLD_SEND_RANKS = 2 };
 
-template <bool SEND>
+template <int MODE>
 __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t r) {
+    constexpr bool SEND = MODE != FOLD;
+    constexpr bool RANKS = MODE == FOLD_SEND_RANKS;
     constexpr int TILE = 1 << FB_TB;
     constexpr int NPT = TILE / FBF_THREADS;
     constexpr int FQ = (FB_CAP2 + FBF_THREADS - 1) / FBF_THREADS;
@@ -572,7 +579,8 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
     __shared__ uint16_t idx[FB_CAP2];             // the message's slot in msg, permuted with src
     __shared__ uint32_t tmp[FBF_THREADS / 64];
     __shared__ uint32_t red[2][FBF_THREADS / 64];
-    __shared__ uint32_t sbase[SEND ? FBF_MAXB1 : 1];  // fused send: the tile's run start per coarse bin
+    __shared__ uint32_t sbase[SEND ? FBF_MAXB1 : 1];  // send phase: the tile's run start per key
+    __shared__ MultiOutLds O[1];  // (FOLD_SEND_RANKS only; unreferenced otherwise)
     Ctl* ctl = a.ctl;
     if (ld_agent(&ctl->done)) return;
     const uint32_t P = a.P;
@@ -580,11 +588,16 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
     double2* __restrict__ swn = a.swn;
     uint8_t* __restrict__ nbp = a.nb;
     uint32_t alerts = 0, newly = 0;
+    uint32_t nkeys = a.nb1;  // send phase: keys of the LDS bins
+    if constexpr (RANKS) {
+        O[0].init(a);
+        nkeys = O[0].kb[a.W];
+    }
     for (uint32_t v = threadIdx.x; v < TILE; v += FBF_THREADS) cnt[v] = 0u;
     __syncthreads();
-    // the tile's messages (sender ids, payloads) -- fused: the next tile's are loaded while
-    // this tile's messages of round r+1 are scattered and written out (round 5: C4 3.158 /
-    // 3.165 -> 3.083 / 3.079 ms/round, same box, profiles/r05/c4/)
+    // the tile's messages (sender ids, payloads) -- send phase: the next tile's are loaded
+    // while this tile's messages of round r+1 are scattered and written out (round 5: C4
+    // 3.158 / 3.165 -> 3.083 / 3.079 ms/round, same box, profiles/r05/c4/)
     uint32_t snd[FQ];
     double ps[FQ], pw[FQ];  // (two scalar arrays: a double2 array here went to scratch)
     auto load_msgs = [&](uint32_t f, uint32_t n) {
@@ -598,22 +611,23 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
             pw[k] = m.y;
         }
     };
+    const uint32_t t_hi = a.t_hi;
     uint32_t n_pf = 0;
-    if (SEND && blockIdx.x < a.nb2) {
-        n_pf = min(ld_agent(&a.cnt2[blockIdx.x]), (uint32_t)a.cap2);
-        load_msgs(blockIdx.x, n_pf);
+    if (SEND && a.t_lo + blockIdx.x < t_hi) {
+        n_pf = min(ld_agent(&a.cnt2[a.t_lo + blockIdx.x]), (uint32_t)a.cap2);
+        load_msgs(a.t_lo + blockIdx.x, n_pf);
     }
-    for (uint32_t f = blockIdx.x; f < a.nb2; f += gridDim.x) {
+    for (uint32_t f = a.t_lo + blockIdx.x; f < t_hi; f += gridDim.x) {
         constexpr bool pf = SEND;
         const uint32_t n = pf ? n_pf : min(ld_agent(&a.cnt2[f]), (uint32_t)a.cap2);
         // the next tile's message count, early (a scalar load; its messages are loaded later)
         const uint32_t fn = f + gridDim.x;
-        if (pf) n_pf = fn < a.nb2 ? min(ld_agent(&a.cnt2[fn]), (uint32_t)a.cap2) : 0u;
+        if (pf) n_pf = fn < t_hi ? min(ld_agent(&a.cnt2[fn]), (uint32_t)a.cap2) : 0u;
         // every load of the tile in flight at once (indices clamped, validity at use)
         uint32_t x[FQ], y[FQ], vr[FQ], rk[FQ];
         uint8_t bk[NPT];
         double2 svk[NPT];
-        uint32_t nfl[NPT];  // fused send: active in round r+1, and the half it sends
+        uint32_t nfl[NPT];  // send phase: active in round r+1, and the half it sends
         double2 nsw[NPT];
         if (!pf) load_msgs(f, n);
 #pragma unroll
@@ -622,20 +636,22 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
             bk[k] = nbp[j];
             svk[k] = swc[j];
         }
-        // fused send: the coarse bin of each of this thread's nodes' round-r+1 targets, drawn
-        // while the tile's loads are in flight (whether the node sends is known after the fold)
+        // send phase: the key of each of this thread's nodes' round-r+1 targets, drawn while
+        // the tile's loads are in flight (whether the node sends is known after the fold)
         uint32_t nkey[SEND ? NPT / 2 : 1];
         if (SEND) {
             uint32_t node[NPT], xs[NPT], ys[NPT];
 #pragma unroll
             for (int k = 0; k < NPT; ++k) node[k] = a.lo + f * TILE + k * FBF_THREADS + threadIdx.x;
             philox2_batch<NPT>(node, r + 1, S_PUSHSUM, a.k0, a.k1, xs, ys);
+            auto key_of = [&](int k) -> uint32_t {
+                if (P < 2) return 0u;
+                const uint32_t t = full_target(node[k], uniform_from(xs[k], ys[k], P - 1));
+                if constexpr (RANKS) return multi_key(a, t);
+                return t >> a.s1;
+            };
 #pragma unroll
-            for (int k = 0; k < NPT; k += 2)
-                nkey[k / 2] = (P > 1 ? full_target(node[k], uniform_from(xs[k], ys[k], P - 1)) >> a.s1 : 0u) |
-                              ((P > 1 ? full_target(node[k + 1], uniform_from(xs[k + 1], ys[k + 1], P - 1)) >> a.s1
-                                      : 0u)
-                               << 16);
+            for (int k = 0; k < NPT; k += 2) nkey[k / 2] = key_of(k) | (key_of(k + 1) << 16);
         }
         philox2_batch<FQ>(snd, r, S_PUSHSUM, a.k0, a.k1, x, y);
 #pragma unroll
@@ -657,7 +673,7 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
             }
         }
         lds_barrier();
-        // per receiver after its fold: ratio test, flags, state out (and the fused send's inputs)
+        // per receiver after its fold: ratio test, flags, state out (and the send phase's inputs)
         auto close_receiver = [&](int k, uint32_t p0, uint32_t p1, double acc_s, double acc_w) {
             const uint32_t j = f * TILE + k * FBF_THREADS + threadIdx.x;
             const uint8_t b = bk[k];
@@ -744,7 +760,7 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
         for (uint32_t v = threadIdx.x; v < TILE; v += FBF_THREADS) cnt[v] = 0u;
         lds_barrier();
         if (SEND) {
-            // round r+1: coarse bin of every active node's target (drawn above), LDS rank per bin
+            // round r+1: the key of every active node's target (drawn above), LDS rank per key
             uint32_t node[NPT], key[NPT], rank[NPT];
 #pragma unroll
             for (int k = 0; k < NPT; ++k) {
@@ -757,20 +773,27 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
                 }
             }
             lds_barrier();
-            const uint32_t total = lds_excl_scan<FBF_THREADS, true>(cnt, a.nb1, tmp);  // count -> first LDS position
-            // one reservation per (tile, bin), thread q for bin q (nb1 <= FBF_MAXB1 <= threads);
+            const uint32_t total = lds_excl_scan<FBF_THREADS, true>(cnt, nkeys, tmp);  // count -> first LDS position
+            // one reservation per (tile, key), thread q for key q (keys <= FBF_MAXB1 <= threads);
             // the returned offset is stored after the LDS scatter, so the atomic's round
             // trip overlaps it
-            static_assert(FBF_MAXB1 <= FBF_THREADS, "one coarse bin per thread");
+            static_assert(FBF_MAXB1 <= FBF_THREADS, "one key per thread");
             uint32_t res = 0u;
             const uint32_t q0 = threadIdx.x;
-            if (q0 < a.nb1) {
-                const uint32_t n = (q0 + 1 < a.nb1 ? cnt[q0 + 1] : total) - cnt[q0];
-                if (n) res = atomicAdd(&a.cnt1[q0], n);
+            if (q0 < nkeys) {
+                const uint32_t n = (q0 + 1 < nkeys ? cnt[q0 + 1] : total) - cnt[q0];
+                if (n) {
+                    if constexpr (RANKS) {
+                        const uint32_t b = O[0].keyb[q0];
+                        res = atomicAdd(O[0].cnt[b] + (q0 - O[0].kb[b]), n);
+                    } else {
+                        res = atomicAdd(&a.cnt1[q0], n);
+                    }
+                }
             }
             // the next tile's messages, issued after the reservation (so that waiting for its
             // result does not wait for them) and in flight through the scatter and write-out
-            if (fn < a.nb2) load_msgs(fn, n_pf);
+            if (fn < t_hi) load_msgs(fn, n_pf);
 #pragma unroll
             for (int k = 0; k < NPT; ++k) {
                 if (key[k] == FB_NONE) continue;
@@ -779,16 +802,18 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
                 msg[p] = nsw[k];
                 idx[p] = (uint16_t)key[k];
             }
-            if (q0 < a.nb1) sbase[q0] = res;
+            if (q0 < nkeys) sbase[q0] = res;
             lds_barrier();
-            // write-out in bin order: consecutive threads, consecutive slots of one run
+            // write-out in key order: consecutive threads, consecutive slots of one run
 #pragma unroll
             for (int k = 0; k < NPT; ++k) {
                 const uint32_t p = k * FBF_THREADS + threadIdx.x;
                 if (p >= total) break;
                 const uint32_t q = idx[p];
                 const uint32_t slot = sbase[q] + (p - cnt[q]);
-                if (slot < a.cap1) {
+                if constexpr (RANKS) {
+                    O[0].store(q, slot, src[p], msg[p], a.overflow);
+                } else if (slot < a.cap1) {
                     const size_t o = (size_t)q * a.cap1 + slot;
                     a.hdr1[o] = src[p];
                     a.pay1[o] = msg[p];
@@ -797,7 +822,7 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
                 }
             }
             lds_barrier();
-            for (uint32_t v = threadIdx.x; v < a.nb1; v += FBF_THREADS) cnt[v] = 0u;
+            for (uint32_t v = threadIdx.x; v < nkeys; v += FBF_THREADS) cnt[v] = 0u;
             lds_barrier();
         }
     }
@@ -848,26 +873,63 @@ FullBinPlan full_bin_plan(uint32_t P, bool fused) {
     return p;
 }
 
+// Several ranks: the smallest coarse-bin size (>= a fine tile) that keeps the keys of all ranks'
+// bins together at most FBM_KEYS -- about the one-rank fused fold's 191 bins at C4, whose runs
+// (~21 messages per (tile, key)) measured best there; larger bins also carry less 12-sigma
+// padding through the exchange (C4 at W = 8: 2^19 receivers, 24 bins per rank, +6.8 %).
+constexpr uint32_t FBM_KEYS = 192;
+uint32_t full_bin_multi_s1(const uint32_t* bounds, int W) {
+    uint32_t s1 = FB_TB;
+    for (;; ++s1) {
+        uint64_t keys = 0;
+        for (int b = 0; b < W; ++b) keys += ((uint64_t)(bounds[b + 1] - bounds[b]) + (1ull << s1) - 1) >> s1;
+        if (keys <= FBM_KEYS || s1 - FB_TB >= 12) break;
+    }
+    return s1;
+}
+
+uint32_t full_bin_multi_cap(uint32_t n, uint32_t s1, uint32_t P) {
+    const double m = (double)n * (double)(1ull << s1) / (double)(P > 1 ? P - 1 : 1);
+    return (uint32_t)std::min<double>(std::ceil(m + 12.0 * std::sqrt(m) + 64.0), (double)n);
+}
+
+size_t fb_bins_bytes(uint32_t nb, uint32_t cap) {
+    if (!nb || !cap) return 0;
+    const size_t c = ((size_t)nb * 4 + 15) & ~(size_t)15, h = ((size_t)nb * cap * 4 + 15) & ~(size_t)15;
+    return c + h + (size_t)nb * cap * 16;
+}
+
+FbBins fb_bins_at(uint8_t* base, uint32_t nb, uint32_t cap) {
+    FbBins f{};
+    if (!nb || !cap) return f;
+    const size_t c = ((size_t)nb * 4 + 15) & ~(size_t)15, h = ((size_t)nb * cap * 4 + 15) & ~(size_t)15;
+    f.cnt = reinterpret_cast<uint32_t*>(base);
+    f.hdr = reinterpret_cast<uint32_t*>(base + c);
+    f.pay = reinterpret_cast<double2*>(base + c + h);
+    f.cap = cap;
+    f.nb = nb;
+    return f;
+}
+
 uint32_t full_bin_item_messages() {
     return FBR_ITEM;
 }
 
 hipError_t launch_full_bin_send_multi(const FullBinArgs& a, uint32_t round, hipStream_t st) {
     const uint32_t items = (uint32_t)(((uint64_t)(a.s_hi - a.s_lo) + FBR_ITEM - 1) / FBR_ITEM);
-    if (items) hipLaunchKernelGGL(k_fbm_send, dim3(items), dim3(FBR_THREADS), 2 * sizeof(uint32_t) * a.W, st, a, round);
+    if (items) hipLaunchKernelGGL(k_fbm_send, dim3(items), dim3(FBR_THREADS), 2 * sizeof(uint32_t) * FBF_MAXB1, st, a, round);
     return hipGetLastError();
 }
 
-hipError_t launch_full_bin_recv_reset(const FullBinArgs& a, hipStream_t st) {
-    hipError_t e;
-    if ((e = hipMemsetAsync(a.cnt1, 0, sizeof(uint32_t) * a.nb1, st)) != hipSuccess) return e;
-    return hipMemsetAsync(a.cnt2, 0, sizeof(uint32_t) * a.nb2, st);
+hipError_t launch_zero_list(const ZeroList& z, hipStream_t st) {
+    if (z.k > 0) hipLaunchKernelGGL(k_zero_list, dim3(z.k), dim3(256), 0, st, z);
+    return hipGetLastError();
 }
 
-hipError_t launch_full_bin_coarse(const FullBinArgs& a, uint32_t round, hipStream_t st) {
+hipError_t launch_full_bin_split_multi(const FullBinArgs& a, uint32_t round, hipStream_t st) {
     if (a.in_item0[a.W])
-        hipLaunchKernelGGL(k_fbm_coarse, dim3(a.in_item0[a.W]), dim3(FBR_THREADS), 2 * sizeof(uint32_t) * a.nb1, st, a,
-                           round);
+        hipLaunchKernelGGL(k_fb_split<true>, dim3(a.in_item0[a.W]), dim3(FBR_THREADS),
+                           2 * sizeof(uint32_t) * (1u << (a.s1 - FB_TB)), st, a, round);
     return hipGetLastError();
 }
 
@@ -875,23 +937,24 @@ hipError_t launch_full_bin_coarse(const FullBinArgs& a, uint32_t round, hipStrea
 // CU), each walking ~P / 2^FB_TB / 512 tiles.  P = 1e8, same box: 4096 / 2048 / 1024 / 512 / 256 blocks
 // 3.16-3.18 / 3.145-3.147 / 3.137-3.145 / 3.130-3.138 / 3.143-3.147 ms/round once the GPU is
 // warm, one tile per block 3.28 (profiles/r04/c4_fused/fold_grid.txt)
-static uint32_t fold_blocks(const FullBinArgs& a, int grid) {
-    return std::max<uint32_t>(1, std::min<uint32_t>(a.nb2, (uint32_t)grid * 256 / FBF_THREADS / 8));
+static uint32_t fold_blocks(uint32_t tiles, int grid) {
+    return std::max<uint32_t>(1, std::min<uint32_t>(tiles, (uint32_t)grid * 256 / FBF_THREADS / 8));
+}
+
+// Several ranks: the fold of one exchange region's tiles [t_lo, t_hi), binning their next-round
+// messages into the region's exchange buffers; one block per CU (the block holds the CU's LDS),
+// each walking its ~tiles / CUs tiles with the next one's messages prefetched -- a region has
+// only ~1500 tiles at C4 / W = 8, so a second wave of blocks would pay every block's start-up
+// and unprefetched first tile twice.
+hipError_t launch_full_bin_fold_multi(const FullBinArgs& a, uint32_t round, int cus, hipStream_t st) {
+    if (a.t_hi > a.t_lo)
+        hipLaunchKernelGGL(k_fb_fold<FOLD_SEND_RANKS>, dim3(std::max<uint32_t>(1, std::min<uint32_t>(a.t_hi - a.t_lo, (uint32_t)cus))),
+                           dim3(FBF_THREADS), 0, st, a, round);
+    return hipGetLastError();
 }
 
 // B's grid: every coarse bin's ranges
 static uint32_t split_items(const FullBinArgs& a) { return a.nb1 * ((a.cap1 + FBR_ITEM - 1) / FBR_ITEM); }
-
-hipError_t launch_full_bin_split_fold(const FullBinArgs& a, uint32_t round, int grid, hipStream_t st) {
-    const uint32_t items_b = split_items(a);
-    hipLaunchKernelGGL(k_fb_split, dim3(items_b), dim3(FBR_THREADS), 2 * sizeof(uint32_t) * (1u << (a.s1 - FB_TB)), st,
-                       a, round);
-    // several ranks: a slab's few tiles (3052 at C4 / W = 8) one per block -- 512 blocks of ~6 tiles
-    // measured 0.246 vs 0.214 ms per slab (profiles/r04/final4/)
-    hipLaunchKernelGGL(k_fb_fold<false>, dim3(std::min<uint32_t>(a.nb2, (uint32_t)grid * 256 / FBF_THREADS)),
-                       dim3(FBF_THREADS), 0, st, a, round);
-    return hipGetLastError();
-}
 
 uint32_t full_bin_fused_max_bins() {
     return FBF_MAXB1;
@@ -909,15 +972,14 @@ hipError_t launch_full_bin_round(const FullBinArgs& a, uint32_t round, int grid,
     }
     if ((e = hipMemsetAsync(a.cnt2, 0, sizeof(uint32_t) * a.nb2, st)) != hipSuccess) return e;
     const uint32_t items_b = split_items(a);
-    hipLaunchKernelGGL(k_fb_split, dim3(items_b), dim3(FBR_THREADS), 2 * sizeof(uint32_t) * (1u << (a.s1 - FB_TB)), st,
-                       a, round);
-    const uint32_t nfold = fold_blocks(a, grid);
-    const dim3 gc(nfold);
+    hipLaunchKernelGGL(k_fb_split<false>, dim3(items_b), dim3(FBR_THREADS), 2 * sizeof(uint32_t) * (1u << (a.s1 - FB_TB)),
+                       st, a, round);
+    const dim3 gc(fold_blocks(a.nb2, grid));
     if (a.fused) {
         if ((e = hipMemsetAsync(a.cnt1, 0, sizeof(uint32_t) * a.nb1, st)) != hipSuccess) return e;
-        hipLaunchKernelGGL(k_fb_fold<true>, gc, dim3(FBF_THREADS), 0, st, a, round);
+        hipLaunchKernelGGL(k_fb_fold<FOLD_SEND>, gc, dim3(FBF_THREADS), 0, st, a, round);
     } else {
-        hipLaunchKernelGGL(k_fb_fold<false>, gc, dim3(FBF_THREADS), 0, st, a, round);
+        hipLaunchKernelGGL(k_fb_fold<FOLD>, gc, dim3(FBF_THREADS), 0, st, a, round);
     }
     return hipGetLastError();
 }

@@ -483,6 +483,8 @@ hipError_t launch_full_pushsum_round(const DevState& S, uint32_t round, int grid
     a.pay2 = S.fb_pay2;
     a.lo = S.lo;      // one rank: 0
     a.nloc = S.nloc;  // one rank: P
+    a.t_lo = 0;
+    a.t_hi = S.fb_nb2;
     a.W = 1;
     a.fused = S.fb_fused;
     return launch_full_bin_round(a, round, grid, st);

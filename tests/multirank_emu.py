@@ -241,6 +241,37 @@ def full_capacity(na, nb, P):
     return int(min(np.ceil(m + 12.0 * np.sqrt(m) + 64.0), na))
 
 
+FB_TB = 12       # gp_fullbin.hpp: fine tiles of 4096 receivers
+FBM_KEYS = 192   # gp_fullbin.hip: keys of all ranks' coarse bins together, at most
+
+
+def full_bin_multi_s1(bounds):
+    """Coarse-bin size 2^s1 every rank uses on the full topology (gp_fullbin.hip
+    full_bin_multi_s1): the smallest >= a fine tile that keeps all ranks' bins together at
+    most FBM_KEYS."""
+    s1 = FB_TB
+    while True:
+        keys = sum(-(-(bounds[b + 1] - bounds[b]) // (1 << s1)) for b in range(len(bounds) - 1))
+        if keys <= FBM_KEYS or s1 - FB_TB >= 12:
+            return s1
+        s1 += 1
+
+
+def full_bin_multi_cap(n, s1, P):
+    """Messages a region of n senders sends to one coarse bin (2^s1 receivers) of any rank,
+    at most (gp_fullbin.hip full_bin_multi_cap): Binomial(n, 2^s1 / (P - 1)) + 12 sigma + 64."""
+    m = n * (1 << s1) / max(P - 1, 1)
+    return int(min(np.ceil(m + 12.0 * np.sqrt(m) + 64.0), n))
+
+
+def full_region(n, NH, h):
+    """Region h of NH of a slab of n ids (gp_api.hip full_region): fine tiles [t0, t1),
+    local sender ids [s0, s1)."""
+    nt = -(-n // (1 << FB_TB))
+    t0, t1 = nt * h // NH, nt * (h + 1) // NH
+    return min(n, t0 << FB_TB), min(n, t1 << FB_TB)
+
+
 def full_target(i, k):
     """Slot k of node i on the full topology: the k-th of all j != i (Program.fs:211-216)."""
     return np.where(k < i, k, k + 1)
@@ -579,23 +610,27 @@ class RankSim:
 
     def _full_pushsum_exchange(self, snd, t, payload):
         """Push-sum messages -> this rank's receivers (gp_fullbin.hip several ranks,
-        gp_api.hip launch_round_full_multi): the senders of each half of the slab
-        ([lo, lo + n/2), [lo + n/2, hi)) are binned by destination rank in arbitrary
-        order into their own fixed-capacity region (own share included) and
-        exchanged separately; the receiver recomputes the targets and puts each
-        receiver's messages in ascending sender order.  Returns local receiver ids
-        and payload columns."""
+        gp_api.hip launch_round_full_multi, round 6): the senders of each of the slab's two
+        exchange regions (whole fine tiles, full_region) are binned by destination rank and
+        the destination's coarse bin (2^s1 receivers, the same size on every rank) in
+        arbitrary order into fixed-capacity bins (own share included), which are exchanged
+        per region; the receiver recomputes the targets and puts each receiver's messages in
+        ascending sender order.  Returns local receiver ids and payload columns."""
         owner = np.searchsorted(np.array(self.bounds), t, side="right") - 1
         rng = np.random.default_rng(self.round * 7919 + self.rank)  # buffer order is arbitrary
         n = self.hi - self.lo
-        cut = self.lo + n // 2
+        s1 = full_bin_multi_s1(self.bounds)
         parts = []
-        for h, (h_lo, h_hi) in enumerate(((self.lo, cut), (cut, self.hi))):
+        for h in range(2):
+            r0, r1 = full_region(n, 2, h)
+            h_lo, h_hi = self.lo + r0, self.lo + r1
+            cap = full_bin_multi_cap(h_hi - h_lo, s1, self.P)
             packets = {}
             for b in range(self.W):
                 sel = np.nonzero((owner == b) & (snd >= h_lo) & (snd < h_hi))[0]
-                nb = self.bounds[b + 1] - self.bounds[b] - (1 if b == self.rank else 0)
-                assert len(sel) <= full_capacity(h_hi - h_lo, nb, self.P), "exchange capacity exceeded"
+                if len(sel):
+                    per_bin = np.bincount((t[sel] - self.bounds[b]) >> s1)
+                    assert per_bin.max() <= cap, "exchange bin capacity exceeded"
                 sel = rng.permutation(sel)
                 packets[b] = (snd[sel],) + tuple(p[sel] for p in payload)
             got = [None] * self.W

@@ -17,7 +17,8 @@ import pytest
 
 import numpy as np
 
-from tests.multirank_emu import DIR_RANDOM, Geometry, S_PUSHSUM, S_TOPO, full_capacity, resolve, slab_bounds, uniform
+from tests.multirank_emu import (DIR_RANDOM, Geometry, S_PUSHSUM, S_TOPO, full_bin_multi_cap, full_bin_multi_s1,
+                                 full_region, resolve, slab_bounds, uniform)
 
 HBM_BYTES = 288e9
 GAUSS_12SIGMA_TAIL = 1.8e-33  # P(Z > 12)
@@ -124,36 +125,45 @@ def full_bin_plan(nrecv, fused=False):
     return nb1, int(m1 + 12.0 * math.sqrt(m1) + 1024.0), nb2, cap2
 
 
-def test_c4_full_pushsum_1e8_world8_plan():
-    """Several ranks (gp_fullbin.hip k_fbm_send / k_fbm_coarse): every rank's messages to
-    rank b -- itself included -- go through fixed-capacity buffers, one region per half of
-    the sender's slab (the two halves are exchanged separately, gp_api.hip
-    launch_round_full_multi), then the receiver bins them by coarse bin and fine tile of
-    its own receivers."""
+def fb_bins_bytes(nb, cap):
+    """gp_fullbin.hip fb_bins_bytes: [counts | sender ids | payloads], 16-B aligned parts."""
+    return (nb * 4 + 15) // 16 * 16 + (nb * cap * 4 + 15) // 16 * 16 + nb * cap * 16
+
+
+@pytest.mark.parametrize("W", [2, 4, 8])
+def test_c4_full_pushsum_1e8_plan(W):
+    """Several ranks (round 6, gp_fullbin.hip k_fb_fold<FOLD_SEND_RANKS>): the fold of each of a
+    slab's two exchange regions (whole fine tiles) bins its nodes' next-round messages by
+    destination rank and the destination's coarse bin -- 2^s1 receivers, one size on every rank
+    -- into fixed-capacity bins that travel as the exchange buffers (own share into the rank's
+    own receive region), and the receiver's split reads them where they arrive.  The capacity
+    per (region, pair, bin) is Binomial(n_region, 2^s1 / (P - 1)) + 12 sigma + 64."""
     P, T, _ = resolve(10**8, "full")
-    W = 8
     bounds, halo = slab_bounds(P, 0, "full", W)
     assert halo == 0 and bounds[-1] == P
-
-    def halves(n):
-        return (n // 2, n - n // 2)
-
+    s1 = full_bin_multi_s1(bounds)
+    nb = [-(-(bounds[b + 1] - bounds[b]) // (1 << s1)) for b in range(W)]
+    assert s1 == 19 and sum(nb) <= 192  # within the fold's LDS keys (1024), runs of ~21 per (tile, key)
+    q = (1 << s1) / (P - 1)
     for a in range(W):
         na = bounds[a + 1] - bounds[a]
-        caps_in = []
-        for b in range(W):
-            nb = bounds[b + 1] - bounds[b] - (1 if b == a else 0)  # no message to oneself
-            for nah in halves(na):
-                m = nah * nb / (P - 1)
-                sd = math.sqrt(m * (1 - nb / (P - 1)))
-                assert (full_capacity(nah, nb, P) - m) / sd >= 12.0
-            nsrc = bounds[b + 1] - bounds[b]
-            caps_in += [full_capacity(nsh, na - (1 if b == a else 0), P) for nsh in halves(nsrc)]
-        nb1, cap1, nb2, cap2 = full_bin_plan(na)
-        assert nb1 < 4096 and nb2 * cap2 < 2**32
-        # a coarse bin receives Binomial(sum of senders, 2^s1 / (P - 1)) messages: 12 sigma + 1024
-        # node arrays (s, w) x2 + byte + buffers out (W - 1) and in (W) + coarse and fine bins
-        steady = na * (2 * 16 + 1 + 4) + 20 * (sum(caps_in) * 2) + 20 * (nb1 * cap1 + nb2 * cap2)
+        out_bytes = in_bytes = 0
+        for h in range(2):
+            r0, r1 = full_region(na, 2, h)
+            cap = full_bin_multi_cap(r1 - r0, s1, P)
+            m = (r1 - r0) * q
+            assert (cap - m) / math.sqrt(m * (1 - q)) >= 12.0
+            assert cap / m - 1 < 0.08  # the fixed capacities' share of the wire bytes
+            out_bytes += sum(fb_bins_bytes(nb[b], cap) for b in range(W) if b != a)
+            for p in range(W):
+                n_p = bounds[p + 1] - bounds[p]
+                p0, p1 = full_region(n_p, 2, h)
+                in_bytes += fb_bins_bytes(nb[a], full_bin_multi_cap(p1 - p0, s1, P))
+        # the messages a sends per round: 20 B each; the buffers add under 8 %
+        msgs = na * (P - na) / (P - 1) * 20
+        assert out_bytes < 1.08 * msgs + 1e6
+        nb2, cap2 = -(-na // 4096), 4992
+        steady = na * (2 * 16 + 1) + out_bytes + in_bytes + nb2 * cap2 * 20
         assert steady < 0.5 * HBM_BYTES
 
 

@@ -75,7 +75,7 @@ def pair_bytes(n, topo, alg, W, halves=1, lists=True, halo_compact=False):
     headers; full push-sum: `halves` regions, one per half of a's senders) and the halo
     bytes per neighbouring pair and direction (push-sum since round 5: the plane's direction
     bytes + HALO_CAP = 256 (s, w) slots per 1024-node chunk, gp_xchg.hpp)."""
-    from tests.multirank_emu import full_capacity, resolve, slab_bounds
+    from tests.multirank_emu import full_bin_multi_cap, full_bin_multi_s1, full_region, resolve, slab_bounds
     from tests.test_multigpu_plan import cap_of, imp3d_pair_stats
     P, _, g = resolve(n, topo)
     push = alg == "push-sum"
@@ -86,13 +86,19 @@ def pair_bytes(n, topo, alg, W, halves=1, lists=True, halo_compact=False):
     B = [[0] * W for _ in range(W)]
     halo = 0
     if topo == "full":
+        # push-sum since round 6: per region, the destination's coarse bins (FbBins: counts,
+        # sender ids, payloads at a fixed capacity per bin, gp_fullbin.hip)
+        from tests.test_multigpu_plan import fb_bins_bytes
         bounds, _ = slab_bounds(P, g, topo, W)
+        s1 = full_bin_multi_s1(bounds)
+        nb = [-(-(bounds[b + 1] - bounds[b]) // (1 << s1)) for b in range(W)]
         for a in range(W):
             na = bounds[a + 1] - bounds[a]
-            parts = (na,) if halves == 1 else (na // 2, na - na // 2)
             for b in range(W):
                 if b != a:
-                    B[a][b] = sum(xbuf(full_capacity(nh, bounds[b + 1] - bounds[b], P)) for nh in parts)
+                    for h in range(halves):
+                        r0, r1 = full_region(na, halves, h)
+                        B[a][b] += fb_bins_bytes(nb[b], full_bin_multi_cap(r1 - r0, s1, P))
     else:
         bounds, H = slab_bounds(P, g, topo, W)
         halo = H * (1 + (16 if push else 0))
@@ -152,7 +158,7 @@ def model(tdir, n, topo, alg, W, rounds, out=None):
         for name, v in by.items():
             if "rocclr_copy" in name:
                 cp += sum(v)
-            elif len(v) == W or (len(v) % W == 0 and "k_ps_tile" in name):
+            elif len(v) == W or (len(v) % W == 0 and ("k_ps_tile" in name or "k_fb_" in name)):
                 # (region-by-region rounds: the round kernel once per region and slab, slab k's
                 # launches at k, W + k, ...)
                 vs = [sum(v[h * W + k] for h in range(len(v) // W)) for k in range(W)]
@@ -178,7 +184,7 @@ def model(tdir, n, topo, alg, W, rounds, out=None):
         if npk and npk[-1] and npk[-1] % W == 0:
             halves = npk[-1] // W
     # (Imp3D push-sum since round 5: k_list_pack per region, no unpack -- the round kernel reads the
-    # received lists in place)
+    # received lists in place; full push-sum since round 6: no send / coarse pass, see below)
     first_k, second_k = ("k_fbm_send", "k_fbm_coarse") if topo == "full" else ("k_list_pack", None)
     # a round-4 build (A/B runs): {slot} / {count} buffers with an unpack pass
     legacy = topo != "full" and any("k_unpack" in k for k in per_slab_names(groups, short))
@@ -213,7 +219,25 @@ def model(tdir, n, topo, alg, W, rounds, out=None):
             regions = {"kernel_region_ms": [round(max(K[k][h] for k in range(W)), 4) for h in range(nreg)],
                        "pack_region_ms": [round(max(Pk[k][h] for k in range(W)), 4) for h in range(nreg)],
                        "K": K, "P": Pk}
-    if halves >= 2 and not regions:
+    # full push-sum (round 6, gp_api.hip launch_round_full_multi): per rank the splits of every
+    # region, then region by region the fold, whose messages travel (region h's transfer after
+    # its fold, in order on the link) while the next region folds
+    fused = None
+    if topo == "full" and alg == "push-sum":
+        sv, fv = [], []
+        for grp in groups:
+            a_ = [ms for name, ms in grp if short(name).startswith("k_fb_split")]
+            b_ = [ms for name, ms in grp if short(name).startswith("k_fb_fold")]
+            if len(a_) == halves * W and len(b_) == halves * W:
+                sv.append(a_)
+                fv.append(b_)
+        if fv:
+            Sp = [[statistics.mean(x[h * W + k] for x in sv) for h in range(halves)] for k in range(W)]
+            Fo = [[statistics.mean(x[h * W + k] for x in fv) for h in range(halves)] for k in range(W)]
+            fused = {"split_region_ms": [round(max(Sp[k][h] for k in range(W)), 4) for h in range(halves)],
+                     "fold_region_ms": [round(max(Fo[k][h] for k in range(W)), 4) for h in range(halves)],
+                     "S": Sp, "F": Fo}
+    if halves >= 2 and not regions and not fused:
         # per rank: send half 0, half 1; coarse half 0, half 1 (dispatch order), the rest
         hk = {}
         for grp in groups:
@@ -241,7 +265,9 @@ def model(tdir, n, topo, alg, W, rounds, out=None):
                "allreduce_latency_ms": ALLREDUCE_LAT_MS, "topology": "one xGMI link per rank pair (8-GPU node)"},
            "model": [], "pipelined_halves": piped,
            "round_regions": ({k: v for k, v in regions.items() if k in ("kernel_region_ms", "pack_region_ms")}
-                             if regions else None)}
+                             if regions else None),
+           "full_fused_regions": ({k: v for k, v in fused.items() if k in ("split_region_ms", "fold_region_ms")}
+                                  if fused else None)}
     for bw in LINK_GBPS:
         # the busiest link: a pair's buffer plus, between slab neighbours, the halo plane
         link = 0.0
@@ -252,7 +278,19 @@ def model(tdir, n, topo, alg, W, rounds, out=None):
         t_x = link / (bw * 1e9) * 1e3 + (GROUP_LAT_MS if link else 0.0) * halves
         serial = t_comp + t_x + ALLREDUCE_LAT_MS
         overlap = max(t_comp, t_x) + ALLREDUCE_LAT_MS
-        if regions:  # as scheduled, per rank: K_0 P_0 K_1 P_1 ...; x_h after P_h, in order on the link
+        if fused:  # as scheduled, per rank: S_0 S_1 F_0 F_1; x_h after F_h, in order on the link
+            Sp, Fo = fused["S"], fused["F"]
+            xh = t_x / halves
+            worst = 0.0
+            for k in range(W):
+                t = sum(Sp[k])
+                x_end = 0.0
+                for h in range(halves):
+                    t += Fo[k][h]
+                    x_end = max(x_end, t) + xh
+                worst = max(worst, max(t, x_end) + comp[k] - sum(Sp[k]) - sum(Fo[k]))
+            overlap = worst + ALLREDUCE_LAT_MS
+        elif regions:  # as scheduled, per rank: K_0 P_0 K_1 P_1 ...; x_h after P_h, in order on the link
             K, Pk = regions["K"], regions["P"]
             xh = t_x / nreg
             worst = 0.0
@@ -278,7 +316,7 @@ def model(tdir, n, topo, alg, W, rounds, out=None):
                 c_end = x_end + sum(ch)
             overlap = c_end + piped["rest_ms"] + ALLREDUCE_LAT_MS
         res["model"].append({"link_gbps": bw, "exchange_ms": round(t_x, 4), "round_ms_serial": round(serial, 4),
-                             "round_ms_as_scheduled": round(overlap, 4) if piped or regions else round(serial, 4),
+                             "round_ms_as_scheduled": round(overlap, 4) if piped or regions or fused else round(serial, 4),
                              "exchange_share_serial": round(t_x / serial, 3), "round_ms_overlapped": round(overlap, 4),
                              "node_updates_per_s_serial": P / (serial * 1e-3),
                              "node_updates_per_s_overlapped": P / (overlap * 1e-3)})
