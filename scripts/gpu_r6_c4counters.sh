@@ -13,3 +13,12 @@ done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o kt -- python3 tools/perf_round.py 100000000 full push-sum 40 > $O/kt.log 2>&1 || { tail $O/kt.log; exit 1; }
 python3 tools/kt_steady.py $O/kt k_fb_split --last 40 && python3 tools/kt_steady.py $O/kt k_fb_fold --last 40
 rm -f $O/kt/*/kt_kernel_trace.csv $O/kt/kt_kernel_trace.csv 2>/dev/null; true
+# the W = 8 model again (the state of the commit)
+d=$O/vr_c4w8
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $d -o kt -- python3 tools/mgpu_model.py run 100000000 full push-sum 8 20 > $d.log 2>&1 || { tail -20 $d.log; exit 1; }
+python3 tools/mgpu_model.py model $d 100000000 full push-sum 8 20 $O/model_c4w8.json > /dev/null || exit 1
+python3 -c "
+import json; d=json.load(open('$O/model_c4w8.json'))
+print('c4w8: rank compute max %.3f ms, regions %s, sched %.3f (128) / %.3f (64) ms' % (max(d['rank_compute_ms']), d['full_fused_regions'], d['model'][1]['round_ms_as_scheduled'], d['model'][0]['round_ms_as_scheduled']))
+print('   per-slab kernels', {k: round(sum(v)/len(v),4) for k,v in d['per_slab_kernel_ms'].items()})"
+rm -f $d/*/kt_kernel_trace.csv $d/kt_kernel_trace.csv 2>/dev/null; true
