@@ -37,6 +37,7 @@ namespace {
 
 constexpr int BK_THREADS = 1024;
 constexpr int BK_NPT = 5;  // nodes per thread: boxes of at most 5120 nodes
+constexpr int EPOCH = BLOCK_EPOCH;  // rounds between grid barriers
 
 struct BlockArgs {
     const double2* sw_in;   // round r0's state (id-indexed)
@@ -45,10 +46,13 @@ struct BlockArgs {
     const uint8_t* nb_in;
     uint8_t* nb_out;
     uint8_t* nb_alt;
+    double2* ck_sw;         // the epoch checkpoint: the input buffers (id-indexed)
+    uint8_t* ck_nb;
     uint32_t* fb;           // face node bytes, one word each [2][NB][6][fmax]
     double2* fs;            // face (s, w) [2][NB][6][fmax]
     unsigned int* bar;      // barrier arrivals (zeroed before the launch)
-    unsigned long long* acc;  // [3][2]: per-round alerts, newly active (zeroed before the launch)
+    unsigned int* flag;     // [NB][16]: the steps each box has published (zeroed before the launch)
+    unsigned long long* acc;  // [3][EPOCH][2]: per-round alerts, newly active (zeroed before the launch)
     unsigned int* err;      // set by a barrier that timed out
     Ctl* ctl;
     Geom G;
@@ -102,6 +106,48 @@ __device__ __forceinline__ bool grid_sync(unsigned int* bar, unsigned int k, uns
     return ok != 0u;
 }
 
+
+// Step s (s = 1, 2, ...) of this box is published (its faces of that step are performed:
+// vmcnt(0) in every wave before the workgroup barrier), then wave 0 waits until every
+// neighbour has published step s too: lane f polls the flag of the neighbour in direction f
+// (64-byte line per box, one writer, at most six readers).  A box therefore runs at most one
+// step ahead of any neighbour, which is what the two face buffers (parity s & 1) need: a box
+// overwrites the faces of step s only in step s + 2, after each neighbour has published step
+// s + 1 -- so has read the faces of step s.  Waits at most ~2 s, like grid_sync.
+__device__ __forceinline__ bool neighbour_sync(unsigned int* flag, unsigned int s, unsigned int hasm, uint32_t b,
+                                               uint32_t sx, uint32_t sy, unsigned int* err) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    __shared__ unsigned int ok;
+    if (threadIdx.x < 64) {
+        const uint32_t l = threadIdx.x;
+        if (l == 0) {
+            ok = 1u;
+            __hip_atomic_store(&flag[16u * b], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        const bool mine = l < 6u && ((hasm >> l) & 1u);
+        // the neighbour in direction l (slot order x-1, x+1, y+1, y-1, z+1, z-1)
+        const uint32_t d = l < 2u ? sx : l < 4u ? sy : 1u;
+        const uint32_t nb = (l == 0u || l == 3u || l == 5u) ? b - d : b + d;
+        const unsigned int* fl = flag + 16u * (mine ? nb : b);
+        const uint64_t t0 = now_10ns();
+        while (true) {
+            const bool pending = mine && __hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < s;
+            if (!__any(pending)) break;
+            if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || now_10ns() - t0 > 200000000ull) {
+                if (l == 0) {
+                    __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ok = 0u;
+                }
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    __syncthreads();
+    return ok != 0u;
+}
+
 }  // namespace
 
 __global__ __launch_bounds__(BK_THREADS) void k_ps_block(BlockArgs a) {
@@ -130,6 +176,9 @@ __global__ __launch_bounds__(BK_THREADS) void k_ps_block(BlockArgs a) {
     const uint32_t fsz[6] = {dyz, dyz, dx * dz, dx * dz, dx * dy, dx * dy};
     const bool has[6] = {ix > 0, ix + 1 < a.nbx, iy + 1 < a.nby, iy > 0, iz + 1 < a.nbz, iz > 0};
     const uint32_t nbr_b[6] = {b - a.nby * a.nbz, b + a.nby * a.nbz, b + a.nbz, b - a.nbz, b + 1, b - 1};
+    unsigned int hasm = 0;
+#pragma unroll
+    for (int f = 0; f < 6; ++f) hasm |= has[f] ? 1u << f : 0u;
 
     // the box's state into LDS
     for (uint32_t v = threadIdx.x; v < V; v += BK_THREADS) {
@@ -205,11 +254,15 @@ __global__ __launch_bounds__(BK_THREADS) void k_ps_block(BlockArgs a) {
         res = make_double2(acc_s, acc_w);
         bn[v] = (uint8_t)(flags | dir);
     };
-    for (uint32_t i = 0; i <= a.nrounds && !stop; ++i) {
-        const uint32_t r = a.r0 + i;
-        // (1) boundary layers of the current state -> face buffer (parity i & 1)
-        if (i < a.nrounds) {
-            const size_t fo = ((size_t)(i & 1u) * NB + b) * 6 * F;
+    // One round r as executed step `step` of this launch: (1) the box's boundary layers -> its face
+    // buffer (parity step & 1); (2) publish "step done" (flag), wait until every neighbour has
+    // published it too; (3) the neighbours' facing layers -> LDS halos; (4) every node of the box;
+    // (5) commit to LDS, the round's counts into its accumulator slot (count, or not: a replay).
+    // False if a neighbour's flag never came (err set).
+    auto one_round = [&](uint32_t r, uint32_t step, unsigned long long* slot) -> bool {
+        const size_t fp = (size_t)(step & 1u) * NB;
+        {
+            const size_t fo = (fp + b) * 6 * F;
 #pragma unroll
             for (int f = 0; f < 6; ++f) {
                 if (!has[f]) continue;
@@ -225,46 +278,20 @@ __global__ __launch_bounds__(BK_THREADS) void k_ps_block(BlockArgs a) {
                         v = lx * dyz + ly * dz + (f == 4 ? dz - 1u : 0u);
                     }
                     // device-coherent stores (agent-scope atomics: performed at the coherence
-                    // point, no L2 write-back needed before the barrier)
+                    // point, no L2 write-back needed before the flag)
                     const double2 mm = swl[v];
-                    unsigned long long* fp = reinterpret_cast<unsigned long long*>(a.fs + fo + f * F + t);
-                    __hip_atomic_store(&fp[0], __builtin_bit_cast(unsigned long long, mm.x), __ATOMIC_RELAXED,
+                    unsigned long long* q = reinterpret_cast<unsigned long long*>(a.fs + fo + f * F + t);
+                    __hip_atomic_store(&q[0], __builtin_bit_cast(unsigned long long, mm.x), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(&fp[1], __builtin_bit_cast(unsigned long long, mm.y), __ATOMIC_RELAXED,
+                    __hip_atomic_store(&q[1], __builtin_bit_cast(unsigned long long, mm.y), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
                     __hip_atomic_store(&a.fb[fo + f * F + t], (uint32_t)bl[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
         }
-        // (2) barrier i + 1: faces of round r written, round r - 1's counts complete
-        if (NB > 1 && !grid_sync(a.bar, i + 1u, NB, a.err)) break;
+        if (NB > 1 && !neighbour_sync(a.flag, step + 1u, hasm, b, a.nby * a.nbz, a.nbz, a.err)) return false;
         if (NB == 1) __syncthreads();
-        // (3) close round r - 1 (every block: the same cumulative count)
-        if (i > 0) {
-            const unsigned long long* cc = a.acc + 2 * ((r - 1u) % 3u);
-            const unsigned long long ra = __hip_atomic_load(&cc[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const unsigned long long rn = __hip_atomic_load(&cc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            total += ra;
-            act += rn;
-            if (b == 0 && threadIdx.x == 0) {
-                Ctl* ctl = a.ctl;
-                ctl->hist[(r - 1u) % HIST] = ra;
-                __hip_atomic_store(&ctl->alerts_total, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&ctl->active_total, act, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (act >= a.G.P) __hip_atomic_store(&ctl->all_active, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (total >= a.G.T) __hip_atomic_store(&ctl->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                // the accumulator of round r + 1 (every block read it, for round r - 2, before
-                // arriving at this barrier)
-                unsigned long long* zz = a.acc + 2 * ((r + 1u) % 3u);
-                __hip_atomic_store(&zz[0], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&zz[1], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            if (total >= a.G.T) break;  // (the same decision in every block)
-        }
-        if (i == a.nrounds) break;
-        // (4) the neighbours' facing layers -> LDS halos
         {
-            const size_t fp = (size_t)(i & 1u) * NB;
 #pragma unroll
             for (int f = 0; f < 6; ++f) {
                 if (!has[f]) continue;
@@ -280,7 +307,7 @@ __global__ __launch_bounds__(BK_THREADS) void k_ps_block(BlockArgs a) {
             }
         }
         __syncthreads();
-        // (5) the round for this thread's nodes: the new (s, w) of node slot q in n[q] (named
+        // the round for this thread's nodes: the new (s, w) of node slot q in n[q] (named
         // registers, selected by q: the slot loop is not unrolled -- unrolled, the compiler
         // interleaved all slots and spilled); the new node bytes go to bn
         uint32_t alerts = 0, newly = 0;
@@ -299,7 +326,6 @@ __global__ __launch_bounds__(BK_THREADS) void k_ps_block(BlockArgs a) {
             else n4 = res;
         }
         __syncthreads();  // every node has read the round-start state
-        // (6) commit: the new state into LDS; the round's counts into its accumulator
         {
             const double2 nq[BK_NPT] = {n0, n1, n2, n3, n4};
 #pragma unroll
@@ -321,18 +347,104 @@ __global__ __launch_bounds__(BK_THREADS) void k_ps_block(BlockArgs a) {
             red[0][threadIdx.x >> 6] = xa;
             red[1][threadIdx.x >> 6] = xn;
         }
-        __syncthreads();
-        if (threadIdx.x == 0) {
+        __syncthreads();  // (also: the commit is complete before the next round's face stores)
+        if (threadIdx.x == 0 && slot) {
             xa = xn = 0;
             for (int w = 0; w < BK_THREADS / 64; ++w) {
                 xa += red[0][w];
                 xn += red[1][w];
             }
-            unsigned long long* cc = a.acc + 2 * (r % 3u);
-            if (xa) __hip_atomic_fetch_add(&cc[0], (unsigned long long)xa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (xn) __hip_atomic_fetch_add(&cc[1], (unsigned long long)xn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (xa) __hip_atomic_fetch_add(&slot[0], (unsigned long long)xa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (xn) __hip_atomic_fetch_add(&slot[1], (unsigned long long)xn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        ++done_rounds;
+        return true;
+    };
+    // the box's state to / from the checkpoint (the launch's input buffers, id-indexed): written at
+    // every epoch's start, read back only for a replay (device-coherent loads: the lines the launch
+    // read at its start may still sit in this CU's vector L1)
+    auto box_io = [&](bool save) {
+        for (uint32_t v = threadIdx.x; v < V; v += BK_THREADS) {
+            const uint32_t lx = v / dyz, ly = (v - lx * dyz) / dz, lz = v - lx * dyz - ly * dz;
+            const uint32_t j = (x0 + lx) * g2 + (y0 + ly) * g + (z0 + lz);
+            unsigned long long* q = reinterpret_cast<unsigned long long*>(a.ck_sw + j);
+            if (save) {
+                q[0] = __builtin_bit_cast(unsigned long long, swl[v].x);
+                q[1] = __builtin_bit_cast(unsigned long long, swl[v].y);
+                a.ck_nb[j] = bl[v];
+            } else {
+                const unsigned long long sx = __hip_atomic_load(&q[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long wx = __hip_atomic_load(&q[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                swl[v] = make_double2(__builtin_bit_cast(double, sx), __builtin_bit_cast(double, wx));
+                bl[v] = __hip_atomic_load(&a.ck_nb[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        __syncthreads();
+    };
+    // Epochs of up to EPOCH rounds: inside one, boxes wait only for their neighbours (a box runs at
+    // most one round ahead of each neighbour); at its end the grid meets once, every box reads the
+    // epoch's per-round counts and finds the round R (if any) in which the cumulative alerts reach
+    // T.  The boxes have then run past R, so each reloads the epoch's starting state (checkpoint)
+    // and runs the epoch's rounds again up to R -- the same arithmetic, so the same state -- and the
+    // launch ends after round R (Program.fs:51-56).
+    // (One box: epochs of one round -- it checks after every round, nothing to replay.)
+    const uint32_t E = NB > 1 ? (uint32_t)EPOCH : 1u;
+    uint32_t step = 0, epoch = 0;
+    for (uint32_t e0 = 0; e0 < a.nrounds && !stop; e0 += E, ++epoch) {
+        const uint32_t n = min(E, a.nrounds - e0);
+        unsigned long long* slots = a.acc + 2 * EPOCH * (epoch % 3u);
+        if (NB > 1 && e0 > 0) box_io(true);  // (epoch 0: the checkpoint is the input)
+        bool ok = true;
+        for (uint32_t k = 0; k < n && ok; ++k) ok = one_round(a.r0 + e0 + k, step++, slots + 2 * k);
+        if (!ok) break;
+        // the epoch's barrier (a grid barrier for several boxes): every count of its rounds is in
+        if (NB > 1 && !grid_sync(a.bar, epoch + 1u, NB, a.err)) break;
+        if (NB == 1) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
+        uint32_t last = n;  // rounds of the epoch that count
+        bool conv = false;
+        unsigned long long tot = total, ac = act;
+        for (uint32_t k = 0; k < n; ++k) {
+            tot += __hip_atomic_load(&slots[2 * k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ac += __hip_atomic_load(&slots[2 * k + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (tot >= a.G.T) {
+                last = k + 1;
+                conv = true;
+                break;
+            }
+        }
+        if (b == 0 && threadIdx.x == 0) {
+            Ctl* ctl = a.ctl;
+            unsigned long long t2 = total, a2 = act;
+            for (uint32_t k = 0; k < last; ++k) {
+                const unsigned long long ra = __hip_atomic_load(&slots[2 * k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                t2 += ra;
+                a2 += __hip_atomic_load(&slots[2 * k + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ctl->hist[(a.r0 + e0 + k) % HIST] = ra;
+            }
+            __hip_atomic_store(&ctl->alerts_total, t2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&ctl->active_total, a2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (a2 >= a.G.P) __hip_atomic_store(&ctl->all_active, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (t2 >= a.G.T) __hip_atomic_store(&ctl->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // the slots of epoch + 2 (every box read them, for epoch - 1, before arriving here)
+            unsigned long long* zz = a.acc + 2 * EPOCH * ((epoch + 2u) % 3u);
+            for (int q = 0; q < 2 * EPOCH; ++q) __hip_atomic_store(&zz[q], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (conv) {  // converged in round a.r0 + e0 + last - 1: back to the epoch's start, replay
+            if (last < n) {
+                box_io(false);
+                for (uint32_t k = 0; k < last && ok; ++k) ok = one_round(a.r0 + e0 + k, step++, nullptr);
+                if (!ok) break;
+            }
+            done_rounds += last;
+            total = tot;
+            stop = true;
+            break;
+        }
+        done_rounds += n;
+        total = tot;
+        act = ac;
     }
     // the state after the last executed round, into that round's buffers (the tile kernel's
     // convention: round r writes buffer (r + 1) & 1)
@@ -397,14 +509,19 @@ hipError_t launch_round_block(const DevState& S, const BlockPlan& p, uint32_t r0
     a.nb_in = S.nb[cur];
     a.nb_out = S.nb[cur ^ 1];
     a.nb_alt = S.nb[cur];
+    a.ck_sw = S.sw[cur];
+    a.ck_nb = S.nb[cur];
     const size_t nb = (size_t)p.nbx * p.nby * p.nbz;
     a.fs = static_cast<double2*>(face);
     a.fb = reinterpret_cast<uint32_t*>(a.fs + 2 * nb * 6 * p.fmax);
-    // scratch (words): [0] barrier (groups arrived), [1] error flag, [2..14) 3 x 2 accumulators,
-    // [16 (1 + grp)] the arrivals of block group grp (a 64-byte line each)
+    // scratch (words): [0] barrier (groups arrived), [1] error flag, [16 (1 + grp)] the arrivals
+    // of block group grp (a 64-byte line each), [144, 144 + 12 EPOCH) 3 x EPOCH x 2 accumulators,
+    // then a 64-byte line of step flags per box
+    if (nb > BLOCK_MAX_BOXES) return hipErrorInvalidValue;
     a.bar = static_cast<unsigned int*>(scratch);
     a.err = a.bar + 1;
-    a.acc = reinterpret_cast<unsigned long long*>(a.bar + 2);
+    a.acc = reinterpret_cast<unsigned long long*>(a.bar + 144);
+    a.flag = a.bar + BLOCK_FLAG_WORD;
     a.ctl = S.ctl;
     a.G = S.G;
     a.k0 = S.k0;

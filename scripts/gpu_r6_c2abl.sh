@@ -1,0 +1,9 @@
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r6_c2abl; mkdir -p $O
+c2() {
+  local l=$1; shift
+  env "$@" timeout -k 10 200 python3 tools/perf_round.py 1000000 3D push-sum 4000 > $O/c2_$l.log 2>&1 || { tail -5 $O/c2_$l.log; return 1; }
+  echo "c2 $l: $(grep -o '[0-9.]* ms/round kernel' $O/c2_$l.log | head -1) $(grep -o 'no events: wall [0-9.]* ms/round' $O/c2_$l.log | head -1)"
+}
+c2 new GP_EXP=1 && c2 nowork GOSSIP_HIP_LIB_EXPERIMENT=build/ablate/lib_c2nowork.so GP_KERNEL=block && c2 nofaces GOSSIP_HIP_LIB_EXPERIMENT=build/ablate/lib_c2nofaces.so GP_KERNEL=block

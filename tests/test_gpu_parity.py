@@ -501,6 +501,8 @@ def test_round_close_parity(fuse, n, topo, seed, rounds, chk, monkeypatch):
 BLOCK_CASES = [  # (num_nodes, seed, rounds, checkpoint): 3D push-sum, the LDS-resident kernel
     (1000, 3, 3000, 1000),        # one box, no grid barrier; through convergence
     (27000, 5, 400, 100),         # several boxes
+    (8000, 7, 40000, 997),        # two boxes through convergence: batches and the converging
+                                  # round cut epochs (16 rounds) mid-way -> checkpoint replay
     (1000000, 1, 300, 150),       # C2 (g = 100): one box per CU
     (1030301, 2, 120, 60),        # g = 101: uneven boxes
 ]
