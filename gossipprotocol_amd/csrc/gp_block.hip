@@ -51,7 +51,6 @@ struct BlockArgs {
     uint32_t* fb;           // face node bytes, one word each [2][NB][6][fmax]
     double2* fs;            // face (s, w) [2][NB][6][fmax]
     unsigned int* bar;      // barrier arrivals (zeroed before the launch)
-    unsigned int* flag;     // [NB][16]: the steps each box has published (zeroed before the launch)
     unsigned long long* acc;  // [3][EPOCH][2]: per-round alerts, newly active (zeroed before the launch)
     unsigned int* err;      // set by a barrier that timed out
     Ctl* ctl;
@@ -107,47 +106,6 @@ __device__ __forceinline__ bool grid_sync(unsigned int* bar, unsigned int k, uns
 }
 
 
-// Step s (s = 1, 2, ...) of this box is published (its faces of that step are performed:
-// vmcnt(0) in every wave before the workgroup barrier), then wave 0 waits until every
-// neighbour has published step s too: lane f polls the flag of the neighbour in direction f
-// (64-byte line per box, one writer, at most six readers).  A box therefore runs at most one
-// step ahead of any neighbour, which is what the two face buffers (parity s & 1) need: a box
-// overwrites the faces of step s only in step s + 2, after each neighbour has published step
-// s + 1 -- so has read the faces of step s.  Waits at most ~2 s, like grid_sync.
-__device__ __forceinline__ bool neighbour_sync(unsigned int* flag, unsigned int s, unsigned int hasm, uint32_t b,
-                                               uint32_t sx, uint32_t sy, unsigned int* err) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    __shared__ unsigned int ok;
-    if (threadIdx.x < 64) {
-        const uint32_t l = threadIdx.x;
-        if (l == 0) {
-            ok = 1u;
-            __hip_atomic_store(&flag[16u * b], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        const bool mine = l < 6u && ((hasm >> l) & 1u);
-        // the neighbour in direction l (slot order x-1, x+1, y+1, y-1, z+1, z-1)
-        const uint32_t d = l < 2u ? sx : l < 4u ? sy : 1u;
-        const uint32_t nb = (l == 0u || l == 3u || l == 5u) ? b - d : b + d;
-        const unsigned int* fl = flag + 16u * (mine ? nb : b);
-        const uint64_t t0 = now_10ns();
-        while (true) {
-            const bool pending = mine && __hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < s;
-            if (!__any(pending)) break;
-            if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || now_10ns() - t0 > 200000000ull) {
-                if (l == 0) {
-                    __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    ok = 0u;
-                }
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-    __syncthreads();
-    return ok != 0u;
-}
-
 }  // namespace
 
 __global__ __launch_bounds__(BK_THREADS) void k_ps_block(BlockArgs a) {
@@ -172,13 +130,12 @@ __global__ __launch_bounds__(BK_THREADS) void k_ps_block(BlockArgs a) {
     uint8_t* bn = bl + ((NS + 1 + 3) & ~3u);                // [vmax]
     uint32_t* ct = reinterpret_cast<uint32_t*>(bn + ((a.vmax + 3) & ~3u));  // [vmax] lx | ly << 10 | lz << 20
     __shared__ uint32_t red[2][BK_THREADS / 64];
+    __shared__ unsigned int bad;  // a face never came (err set): the launch ends
+    constexpr unsigned long long SIGN = 1ull << 63;
     // face sizes and whether the neighbour in direction f exists (slot order: x-1, x+1, y+1, y-1, z+1, z-1)
     const uint32_t fsz[6] = {dyz, dyz, dx * dz, dx * dz, dx * dy, dx * dy};
     const bool has[6] = {ix > 0, ix + 1 < a.nbx, iy + 1 < a.nby, iy > 0, iz + 1 < a.nbz, iz > 0};
     const uint32_t nbr_b[6] = {b - a.nby * a.nbz, b + a.nby * a.nbz, b + a.nbz, b - a.nbz, b + 1, b - 1};
-    unsigned int hasm = 0;
-#pragma unroll
-    for (int f = 0; f < 6; ++f) hasm |= has[f] ? 1u << f : 0u;
 
     // the box's state into LDS
     for (uint32_t v = threadIdx.x; v < V; v += BK_THREADS) {
@@ -191,6 +148,7 @@ __global__ __launch_bounds__(BK_THREADS) void k_ps_block(BlockArgs a) {
     if (threadIdx.x == 0) {
         swl[NS] = make_double2(0.0, 0.0);
         bl[NS] = DIR_NONE;
+        bad = 0u;
     }
     unsigned long long total = __hip_atomic_load(&a.ctl->alerts_total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned long long act = __hip_atomic_load(&a.ctl->active_total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -255,12 +213,17 @@ __global__ __launch_bounds__(BK_THREADS) void k_ps_block(BlockArgs a) {
         bn[v] = (uint8_t)(flags | dir);
     };
     // One round r as executed step `step` of this launch: (1) the box's boundary layers -> its face
-    // buffer (parity step & 1); (2) publish "step done" (flag), wait until every neighbour has
-    // published it too; (3) the neighbours' facing layers -> LDS halos; (4) every node of the box;
-    // (5) commit to LDS, the round's counts into its accumulator slot (count, or not: a replay).
-    // False if a neighbour's flag never came (err set).
+    // buffer (parity step & 1), every word tagged with the step; (2) the neighbours' facing layers
+    // of this step -> LDS halos (waiting for them by their tags); (3) every node of the box; (4)
+    // commit to LDS, the round's counts into its accumulator slot (count, or not: a replay).
+    // False if a neighbour's face never came (err set).
     auto one_round = [&](uint32_t r, uint32_t step, unsigned long long* slot) -> bool {
         const size_t fp = (size_t)(step & 1u) * NB;
+        // every face word carries the step that wrote it: the sign bit of s and of w (both >= 0)
+        // tells step s from step s - 2 (the two steps that share a face buffer), the node-byte
+        // word carries step + 1 in its upper bits
+        const unsigned long long tb = (unsigned long long)(((step >> 1) & 1u) ^ 1u) << 63;
+        const uint32_t tw = (step + 1u) << 8;
         {
             const size_t fo = (fp + b) * 6 * F;
 #pragma unroll
@@ -277,36 +240,61 @@ __global__ __launch_bounds__(BK_THREADS) void k_ps_block(BlockArgs a) {
                         const uint32_t lx = t / dy, ly = t - lx * dy;
                         v = lx * dyz + ly * dz + (f == 4 ? dz - 1u : 0u);
                     }
-                    // device-coherent stores (agent-scope atomics: performed at the coherence
-                    // point, no L2 write-back needed before the flag)
+                    // device-coherent stores (agent-scope atomics), each word single-copy atomic
                     const double2 mm = swl[v];
                     unsigned long long* q = reinterpret_cast<unsigned long long*>(a.fs + fo + f * F + t);
-                    __hip_atomic_store(&q[0], __builtin_bit_cast(unsigned long long, mm.x), __ATOMIC_RELAXED,
+                    __hip_atomic_store(&q[0], __builtin_bit_cast(unsigned long long, mm.x) | tb, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(&q[1], __builtin_bit_cast(unsigned long long, mm.y), __ATOMIC_RELAXED,
+                    __hip_atomic_store(&q[1], __builtin_bit_cast(unsigned long long, mm.y) | tb, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(&a.fb[fo + f * F + t], (uint32_t)bl[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(&a.fb[fo + f * F + t], (uint32_t)bl[v] | tw, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
         }
-        if (NB > 1 && !neighbour_sync(a.flag, step + 1u, hasm, b, a.nby * a.nbz, a.nbz, a.err)) return false;
-        if (NB == 1) __syncthreads();
-        {
+        // the neighbours' facing layers of this step -> LDS halos: each thread loads its entry of
+        // every face at once (device-coherent loads) and loads again the entries whose tags are
+        // not yet this step's -- the face words themselves are the synchronisation
+        for (uint32_t t = threadIdx.x; t < F; t += BK_THREADS) {
+            unsigned long long sx[6], wx[6];
+            uint32_t bw[6], pend = 0;
 #pragma unroll
-            for (int f = 0; f < 6; ++f) {
-                if (!has[f]) continue;
-                const size_t fo = ((fp + nbr_b[f]) * 6 + (f ^ 1)) * F;
-                for (uint32_t t = threadIdx.x; t < fsz[f]; t += BK_THREADS) {
-                    // device-coherent loads (the other XCDs' faces, no L2 invalidate needed)
-                    unsigned long long* fq = reinterpret_cast<unsigned long long*>(a.fs + fo + t);
-                    const unsigned long long sx = __hip_atomic_load(&fq[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const unsigned long long wx = __hip_atomic_load(&fq[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    hb[f * F + t] = (uint8_t)__hip_atomic_load(&a.fb[fo + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    hsw[f * F + t] = make_double2(__builtin_bit_cast(double, sx), __builtin_bit_cast(double, wx));
+            for (int f = 0; f < 6; ++f) pend |= (has[f] && t < fsz[f]) ? 1u << f : 0u;
+            const uint32_t want = pend;
+            uint64_t t0 = 0;
+            while (true) {
+#pragma unroll
+                for (int f = 0; f < 6; ++f)
+                    if ((pend >> f) & 1u) {
+                        const size_t fo = ((fp + nbr_b[f]) * 6 + (f ^ 1)) * F + t;
+                        unsigned long long* fq = reinterpret_cast<unsigned long long*>(a.fs + fo);
+                        sx[f] = __hip_atomic_load(&fq[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        wx[f] = __hip_atomic_load(&fq[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        bw[f] = __hip_atomic_load(&a.fb[fo], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+#pragma unroll
+                for (int f = 0; f < 6; ++f)
+                    if (((pend >> f) & 1u) && (sx[f] & SIGN) == tb && (wx[f] & SIGN) == tb && (bw[f] & ~0xffu) == tw)
+                        pend &= ~(1u << f);
+                if (!pend) break;
+                if (!t0) t0 = now_10ns();
+                if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || now_10ns() - t0 > 200000000ull) {
+                    __hip_atomic_fetch_or(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    bad = 1u;
+                    break;
                 }
+                __builtin_amdgcn_s_sleep(1);
             }
+#pragma unroll
+            for (int f = 0; f < 6; ++f)
+                if ((want >> f) & 1u) {
+                    hb[f * F + t] = (uint8_t)bw[f];
+                    hsw[f * F + t] = make_double2(__builtin_bit_cast(double, sx[f] & ~SIGN),
+                                                  __builtin_bit_cast(double, wx[f] & ~SIGN));
+                }
         }
         __syncthreads();
+        if (bad) return false;
         // the round for this thread's nodes: the new (s, w) of node slot q in n[q] (named
         // registers, selected by q: the slot loop is not unrolled -- unrolled, the compiler
         // interleaved all slots and spilled); the new node bytes go to bn
@@ -517,11 +505,10 @@ hipError_t launch_round_block(const DevState& S, const BlockPlan& p, uint32_t r0
     // scratch (words): [0] barrier (groups arrived), [1] error flag, [16 (1 + grp)] the arrivals
     // of block group grp (a 64-byte line each), [144, 144 + 12 EPOCH) 3 x EPOCH x 2 accumulators,
     // then a 64-byte line of step flags per box
-    if (nb > BLOCK_MAX_BOXES) return hipErrorInvalidValue;
     a.bar = static_cast<unsigned int*>(scratch);
     a.err = a.bar + 1;
     a.acc = reinterpret_cast<unsigned long long*>(a.bar + 144);
-    a.flag = a.bar + BLOCK_FLAG_WORD;
+
     a.ctl = S.ctl;
     a.G = S.G;
     a.k0 = S.k0;
@@ -534,6 +521,7 @@ hipError_t launch_round_block(const DevState& S, const BlockPlan& p, uint32_t r0
     a.fmax = p.fmax;
     a.vmax = p.vmax;
     hipError_t e = hipMemsetAsync(scratch, 0, BLOCK_SCRATCH_BYTES, st);
+    if (e == hipSuccess) e = hipMemsetAsync(face, 0, block_face_bytes(p), st);  // (no face word carries a step)
     if (e != hipSuccess) return e;
     void* args[] = {&a};
     return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&k_ps_block), dim3((uint32_t)nb),
