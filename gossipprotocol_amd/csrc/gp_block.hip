@@ -159,7 +159,7 @@ __global__ __launch_bounds__(BK_THREADS) void k_ps_block(BlockArgs a) {
     // receiver's slot order -- Program.fs:246-257 -- acc + m * 0.5, the oracle's rounding;
     // a direction without a message adds +0.0, exact for the non-negative s and w), the
     // ratio test (Program.fs:114-123), the next direction by Philox.
-    auto node = [&](uint32_t v, uint32_t r, double2& res, uint32_t& alerts, uint32_t& newly) {
+    auto node = [&](uint32_t v, uint32_t draw, double2& res, uint32_t& alerts, uint32_t& newly) {
         const uint32_t c = ct[v];
         const uint32_t lx = c & 1023u, ly = (c >> 10) & 1023u, lz = c >> 20;
         const uint32_t x = x0 + lx, y = y0 + ly, z = z0 + lz;
@@ -208,9 +208,33 @@ __global__ __launch_bounds__(BK_THREADS) void k_ps_block(BlockArgs a) {
             }
         }
         uint32_t dir = DIR_NONE;
-        if (act_n && deg > 0) dir = slot_to_dir_fast(mask, uniform(a.k0, a.k1, S_PUSHSUM, x * g2 + y * g + z, r + 1, deg));
+        if (act_n && deg > 0) dir = slot_to_dir_fast(mask, draw);
         res = make_double2(acc_s, acc_w);
         bn[v] = (uint8_t)(flags | dir);
+    };
+    // The Philox draws of round r for this thread's node slots (the next direction's slot in
+    // [0, deg), Program.fs:101-131 via SRS v1 B.3), 3 bits per slot: they depend on the node and
+    // the round only, so they are computed between the face stores and the face loads.
+    auto draws = [&](uint32_t r) -> uint32_t {
+        uint32_t id[4], x[4], y[4], dg[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t c = ct[min(q * BK_THREADS + threadIdx.x, V - 1u)];
+            const uint32_t lx = c & 1023u, ly = (c >> 10) & 1023u, lz = c >> 20;
+            id[q] = (x0 + lx) * g2 + (y0 + ly) * g + (z0 + lz);
+            dg[q] = popc6(mask_xyz(x0 + lx, y0 + ly, z0 + lz, gm));
+        }
+        philox2_batch(id, r + 1, S_PUSHSUM, a.k0, a.k1, x, y);
+        uint32_t pk = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) pk |= uniform_from(x[q], y[q], dg[q]) << (3 * q);
+        if (V > 4u * BK_THREADS) {  // (a fifth slot: boxes of more than 4096 nodes)
+            const uint32_t c = ct[min(4u * BK_THREADS + threadIdx.x, V - 1u)];
+            const uint32_t lx = c & 1023u, ly = (c >> 10) & 1023u, lz = c >> 20;
+            const uint32_t dd = popc6(mask_xyz(x0 + lx, y0 + ly, z0 + lz, gm));
+            pk |= uniform(a.k0, a.k1, S_PUSHSUM, (x0 + lx) * g2 + (y0 + ly) * g + (z0 + lz), r + 1, dd) << 12;
+        }
+        return pk;
     };
     // One round r as executed step `step` of this launch: (1) the box's boundary layers -> its face
     // buffer (parity step & 1), every word tagged with the step; (2) the neighbours' facing layers
@@ -255,6 +279,7 @@ __global__ __launch_bounds__(BK_THREADS) void k_ps_block(BlockArgs a) {
         // the neighbours' facing layers of this step -> LDS halos: each thread loads its entry of
         // every face at once (device-coherent loads) and loads again the entries whose tags are
         // not yet this step's -- the face words themselves are the synchronisation
+        const uint32_t pk = draws(r);  // (while this step's face stores, and the neighbours', land)
         for (uint32_t t = threadIdx.x; t < F; t += BK_THREADS) {
             unsigned long long sx[6], wx[6];
             uint32_t bw[6], pend = 0;
@@ -306,7 +331,7 @@ __global__ __launch_bounds__(BK_THREADS) void k_ps_block(BlockArgs a) {
             const uint32_t v = q * BK_THREADS + threadIdx.x;
             if (v >= V) break;
             double2 res;
-            node(v, r, res, alerts, newly);
+            node(v, (pk >> (3 * q)) & 7u, res, alerts, newly);
             if (q == 0) n0 = res;
             else if (q == 1) n1 = res;
             else if (q == 2) n2 = res;
