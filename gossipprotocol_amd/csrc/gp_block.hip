@@ -131,6 +131,8 @@ __global__ __launch_bounds__(BK_THREADS) void k_ps_block(BlockArgs a) {
     uint32_t* ct = reinterpret_cast<uint32_t*>(bn + ((a.vmax + 3) & ~3u));  // [vmax] lx | ly << 10 | lz << 20
     __shared__ uint32_t red[2][BK_THREADS / 64];
     __shared__ unsigned int bad;  // a face never came (err set): the launch ends
+    __shared__ unsigned long long ecnt[2 * EPOCH];  // the epoch's per-round counts
+    static_assert(2 * EPOCH <= BK_THREADS, "one count per thread");
     constexpr unsigned long long SIGN = 1ull << 63;
     // face sizes and whether the neighbour in direction f exists (slot order: x-1, x+1, y+1, y-1, z+1, z-1)
     const uint32_t fsz[6] = {dyz, dyz, dx * dz, dx * dz, dx * dy, dx * dy};
@@ -415,34 +417,33 @@ __global__ __launch_bounds__(BK_THREADS) void k_ps_block(BlockArgs a) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
         }
+        // the epoch's counts into LDS (one load per thread), then every thread scans them
+        if (threadIdx.x < 2 * n) ecnt[threadIdx.x] = __hip_atomic_load(&slots[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
         uint32_t last = n;  // rounds of the epoch that count
         bool conv = false;
         unsigned long long tot = total, ac = act;
         for (uint32_t k = 0; k < n; ++k) {
-            tot += __hip_atomic_load(&slots[2 * k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            ac += __hip_atomic_load(&slots[2 * k + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            tot += ecnt[2 * k];
+            ac += ecnt[2 * k + 1];
             if (tot >= a.G.T) {
                 last = k + 1;
                 conv = true;
                 break;
             }
         }
-        if (b == 0 && threadIdx.x == 0) {
+        if (b == 0) {
             Ctl* ctl = a.ctl;
-            unsigned long long t2 = total, a2 = act;
-            for (uint32_t k = 0; k < last; ++k) {
-                const unsigned long long ra = __hip_atomic_load(&slots[2 * k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                t2 += ra;
-                a2 += __hip_atomic_load(&slots[2 * k + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ctl->hist[(a.r0 + e0 + k) % HIST] = ra;
+            if (threadIdx.x < last) ctl->hist[(a.r0 + e0 + threadIdx.x) % HIST] = ecnt[2 * threadIdx.x];
+            if (threadIdx.x == 0) {
+                __hip_atomic_store(&ctl->alerts_total, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&ctl->active_total, ac, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (ac >= a.G.P) __hip_atomic_store(&ctl->all_active, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (tot >= a.G.T) __hip_atomic_store(&ctl->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            __hip_atomic_store(&ctl->alerts_total, t2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&ctl->active_total, a2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (a2 >= a.G.P) __hip_atomic_store(&ctl->all_active, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (t2 >= a.G.T) __hip_atomic_store(&ctl->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             // the slots of epoch + 2 (every box read them, for epoch - 1, before arriving here)
             unsigned long long* zz = a.acc + 2 * EPOCH * ((epoch + 2u) % 3u);
-            for (int q = 0; q < 2 * EPOCH; ++q) __hip_atomic_store(&zz[q], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (threadIdx.x < 2 * EPOCH) __hip_atomic_store(&zz[threadIdx.x], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (conv) {  // converged in round a.r0 + e0 + last - 1: back to the epoch's start, replay
             if (last < n) {

@@ -280,7 +280,7 @@ hipError_t block_kernel_setup(const BlockPlan& p);
 bool block_plan_resident(const BlockPlan& p, int cus);
 // rounds [r0, r0 + nrounds) (fewer once the cumulative alerts reach T); scratch:
 // BLOCK_SCRATCH_BYTES, word 1 is set if a grid barrier timed out
-constexpr int BLOCK_EPOCH = 32;       // rounds between the kernel's grid barriers
+constexpr int BLOCK_EPOCH = 64;       // rounds between the kernel's grid barriers
 constexpr size_t BLOCK_SCRATCH_BYTES = 4 * (144 + 12 * BLOCK_EPOCH);
 hipError_t launch_round_block(const struct DevState& S, const BlockPlan& p, uint32_t r0, uint32_t nrounds, void* face,
                               void* scratch, hipStream_t st);
