@@ -107,7 +107,6 @@ struct TileLdsP {
     uint32_t xm[W_PLANE + DMA_SLACK];
     uint32_t xp[W_PLANE + DMA_SLACK];
     uint32_t ind[TILE / 8 + DMA_SLACK];  // in-degrees of the tile's nodes, a nibble each (DevState::ind4)
-    uint32_t snd[PsSlots<REMOTE>::SNDPF ? SLOTS + DMA_SLACK : 1];  // one rank: the next tile's in-edge senders
     unsigned long long bits[SLOT_FU * (TPB / 64) + 1];  // bit q: in-edge q (tile order) was used by its sender; then 0
     double2 msg[SLOTS];               // edge q's message at slot q
     uint32_t out[TILE / 4];
@@ -144,6 +143,8 @@ __device__ __forceinline__ void dma_copy(void* lds, const char* g16, uint32_t nb
 }
 // cache-policy bits of a single-use (streamed once per round) staging copy: nt
 constexpr int DMA_ONCE = 2;
+// s_waitcnt vmcnt(0) with the other counters left alone (gfx9 encoding: expcnt 7, lgkmcnt 15)
+constexpr int VMCNT0 = 0x0F70;
 
 // Node bytes nb[lo, hi) clamped to [ext_lo,
 // ext_hi); returns the node id of LDS byte 0 (up to 15 bytes below lo).  Reads
@@ -328,8 +329,8 @@ __device__ __forceinline__ void st_stream(uint32_t* p, uint32_t v) { __builtin_n
 //   4. next-round directions of the thread's NPT nodes as one Philox batch;
 //      node bytes out as words, random-edge bits as one ballot per wave.
 template <int TOPO, bool REMOTE>
-__device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLdsP<REMOTE>& L, bool all_active,
-                                         uint32_t& alerts, uint32_t& newly, bool& tiny) {
+__device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLdsP<REMOTE>& L, uint32_t* snd,
+                                         bool all_active, uint32_t& alerts, uint32_t& newly, bool& tiny) {
     const double2* __restrict__ swc = a.swc;
     double2* __restrict__ swn = a.swn;
     const uint64_t* __restrict__ rbc = a.rbc;
@@ -345,7 +346,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
     // loaded one tile ahead: the next tile's in-edge range (two uniform loads); the
     // staged tile's senders, FU words per thread (loaded at the tile's start)
     uint32_t pf_tile = 0xFFFFFFFFu, pf_lo = 0, pf_hi = 0;
-    uint32_t snd_tile = 0xFFFFFFFFu, snd_off = 0;  // SNDPF: L.snd holds tile snd_tile's senders from word snd_off
+    uint32_t snd_tile = 0xFFFFFFFFu, snd_off = 0;  // SNDPF: snd holds tile snd_tile's senders from word snd_off
     constexpr bool SNDPF = PsSlots<REMOTE>::SNDPF;
     uint32_t raw[FU];
 #pragma unroll
@@ -419,7 +420,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
 #pragma unroll
                     for (int m = 0; m < FU; ++m) {
                         const uint32_t q = threadIdx.x + m * TPB;
-                        raw[m] = q < cnt ? L.snd[snd_off + q] : 0u;
+                        raw[m] = q < cnt ? snd[snd_off + q] : 0u;
                     }
                 } else {
 #pragma unroll
@@ -751,6 +752,11 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                         if (!((from >> dM) & 1u)) zM = make_double2(0.0, 0.0);
                         else if (lane != 0u && j <= j0) zM = ld_sw(swc + j - 1);
                     }
+                    // every load of the slot retired here, on all paths: the slot's state store is then the
+                    // only memory operation the next slot's loads could wait for, and they do not
+                    // (without it the compiler waited vmcnt(0) before every slot's gathers -- a lane
+                    // range with no valid node skips the fold that consumes the loads)
+                    __builtin_amdgcn_s_waitcnt(VMCNT0);
                     if (valid) {
                         const uint32_t b = gst[h] & 0xFFu, mask = (gst[h] >> 8) & 63u, from = (gst[h] >> 14) & 63u;
                         const uint32_t deg = popc6(mask) + (TOPO == IMP3D ? 1u : 0u);
@@ -859,7 +865,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                 if (SNDPF && TOPO == IMP3D && k0 == 0) {
                     snd_tile = 0xFFFFFFFFu;
                     if (pf_tile != 0xFFFFFFFFu && pf_hi - pf_lo <= cap) {
-                        snd_off = dma_stage_words(L.snd, srcp, pf_lo, pf_hi);
+                        snd_off = dma_stage_words(snd, srcp, pf_lo, pf_hi);
                         snd_tile = pf_tile;
                     }
                 }
@@ -958,12 +964,16 @@ __device__ __forceinline__ void add_round_counts(Ctl* ctl, uint32_t x, uint32_t 
 template <int TOPO, bool REMOTE>
 __global__ __launch_bounds__(TPB, GP_MINB) void k_ps_tile(RoundArgs a, uint32_t r) {
     __shared__ TileLdsP<REMOTE> L;
+    // one rank: the next tile's in-edge senders, LDS-DMA'd during this tile's node phase.  An LDS
+    // object of its own, so the compiler can tell that the node phase's LDS reads do not read it
+    // and does not wait for the copy before each of them
+    __shared__ uint32_t snd[PsSlots<REMOTE>::SNDPF ? PsSlots<REMOTE>::SLOTS + DMA_SLACK : 1];
     Ctl* ctl = a.ctl;
     if (ld_agent(&ctl->done)) return;
     const bool all_active = ld_agent(&ctl->all_active) != 0;
     uint32_t alerts = 0, newly = 0;
     bool tiny = false;
-    ps_tiles<TOPO, REMOTE>(a, r, L, all_active, alerts, newly, tiny);
+    ps_tiles<TOPO, REMOTE>(a, r, L, snd, all_active, alerts, newly, tiny);
     if (__ballot(tiny) && (threadIdx.x & 63u) == 0) atomicOr(&ctl->tiny, 1u);
     block_counts(L.red, alerts, newly);
     if (threadIdx.x == 0) {
