@@ -389,8 +389,10 @@ int alloc_slab(gp_sim* s, Slab& sl, int r) {
             S.fb_cap1 = f1.cap1;
             S.fb_fused = fused && f1.nb1 <= full_bin_fused_max_bins() ? 1u : 0u;
             const size_t m1 = (size_t)f1.nb1 * f1.cap1;
-            if ((rc = dev_alloc_t(s, &S.fb_cnt1, f1.nb1)) || (rc = dev_alloc_t(s, &S.fb_hdr1, m1)) ||
-                (rc = dev_alloc_t(s, &S.fb_pay1, m1)))
+            // (+ FB_JUNK: the fold's write-out sends lanes without a message to the slots past the
+            // last bin, so every thread issues the same number of stores)
+            if ((rc = dev_alloc_t(s, &S.fb_cnt1, f1.nb1)) || (rc = dev_alloc_t(s, &S.fb_hdr1, m1 + FB_JUNK)) ||
+                (rc = dev_alloc_t(s, &S.fb_pay1, m1 + FB_JUNK)))
                 return rc;
         } else {
             // several ranks (round 6): the coarse bins are the exchange buffers (setup_exchange) --

@@ -622,7 +622,9 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
         const uint32_t n = pf ? n_pf : min(ld_agent(&a.cnt2[f]), (uint32_t)a.cap2);
         // the next tile's message count, early (a scalar load; its messages are loaded later)
         const uint32_t fn = f + gridDim.x;
-        if (pf) n_pf = fn < t_hi ? min(ld_agent(&a.cnt2[fn]), (uint32_t)a.cap2) : 0u;
+        // (a scalar load: an agent-scope vector load here was waited for at once, and with it
+        // every store of the last tile's write-out)
+        if (pf) n_pf = fn < t_hi ? min(ld_const(a.cnt2 + fn), (uint32_t)a.cap2) : 0u;
         // every load of the tile in flight at once (indices clamped, validity at use)
         uint32_t x[FQ], y[FQ], vr[FQ], rk[FQ];
         uint8_t bk[NPT];
@@ -779,7 +781,8 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
             // trip overlaps it
             static_assert(FBF_MAXB1 <= FBF_THREADS, "one key per thread");
             uint32_t res = 0u;
-            const uint32_t q0 = threadIdx.x;
+            uint32_t q0 = threadIdx.x;
+            asm volatile("" : "+v"(q0));  // (the reservation address is not hoisted out of the tile loop and spilled)
             if (q0 < nkeys) {
                 const uint32_t n = (q0 + 1 < nkeys ? cnt[q0 + 1] : total) - cnt[q0];
                 if (n) {
@@ -792,8 +795,10 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
                 }
             }
             // the next tile's messages, issued after the reservation (so that waiting for its
-            // result does not wait for them) and in flight through the scatter and write-out
-            if (fn < t_hi) load_msgs(fn, n_pf);
+            // result does not wait for them) and in flight through the scatter and write-out.
+            // Unconditional (the last tile reloads its own): with the loads on one path only,
+            // the compiler's wait for the reservation became vmcnt(0), i.e. for them too
+            load_msgs(fn < t_hi ? fn : f, n_pf);
 #pragma unroll
             for (int k = 0; k < NPT; ++k) {
                 if (key[k] == FB_NONE) continue;
@@ -803,24 +808,35 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
                 idx[p] = (uint16_t)key[k];
             }
             if (q0 < nkeys) sbase[q0] = res;
+            // the reservation retired on every path -- only the 2 FQ message loads above may still
+            // be in flight -- so no later register reuse makes the compiler wait for those loads
+            // or for the write-out's stores below
+            __builtin_amdgcn_s_waitcnt(vmcnt_enc(2 * FQ));
             lds_barrier();
-            // write-out in key order: consecutive threads, consecutive slots of one run
+            // write-out in key order: consecutive threads, consecutive slots of one run.  One
+            // rank: two stores per slot k on every lane (a lane without a message writes the junk
+            // slots past the last bin), so the wait for the next tile's messages, loaded before
+            // these stores, is an exact count and does not wait for the stores to be acknowledged
+            bool ovf = false;
 #pragma unroll
             for (int k = 0; k < NPT; ++k) {
                 const uint32_t p = k * FBF_THREADS + threadIdx.x;
-                if (p >= total) break;
-                const uint32_t q = idx[p];
-                const uint32_t slot = sbase[q] + (p - cnt[q]);
                 if constexpr (RANKS) {
-                    O[0].store(q, slot, src[p], msg[p], a.overflow);
-                } else if (slot < a.cap1) {
-                    const size_t o = (size_t)q * a.cap1 + slot;
+                    if (p >= total) break;
+                    const uint32_t q = idx[p];
+                    O[0].store(q, sbase[q] + (p - cnt[q]), src[p], msg[p], a.overflow);
+                } else {
+                    const bool has = p < total;
+                    const uint32_t q = has ? idx[p] : 0u;
+                    const uint32_t slot = sbase[q] + (p - cnt[q]);
+                    ovf |= has && slot >= a.cap1;
+                    const size_t o = has && slot < a.cap1 ? (size_t)q * a.cap1 + slot
+                                                          : (size_t)a.nb1 * a.cap1 + (threadIdx.x & (FB_JUNK - 1));
                     a.hdr1[o] = src[p];
                     a.pay1[o] = msg[p];
-                } else {
-                    atomicOr(a.overflow, 1u);
                 }
             }
+            if (ovf) atomicOr(a.overflow, 1u);
             lds_barrier();
             for (uint32_t v = threadIdx.x; v < nkeys; v += FBF_THREADS) cnt[v] = 0u;
             lds_barrier();

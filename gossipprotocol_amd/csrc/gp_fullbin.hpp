@@ -12,6 +12,10 @@ constexpr int FB_TB = 12;
 // messages per fine tile: expected 2^FB_TB + 12 sigma + 128 (4992 at 4096 receivers)
 constexpr int FB_CAP2 = ((1 << FB_TB) + 12 * (1 << (FB_TB / 2)) * (FB_TB % 2 ? 1414 : 1000) / 1000 + 128 + 63) / 64 * 64;
 
+// one rank: slots past the last coarse bin (hdr1 / pay1) that the fused fold's write-out sends
+// its lanes without a message to, so that every thread issues the same stores (k_fb_fold)
+constexpr size_t FB_JUNK = 64;
+
 struct FullBinPlan {
     uint32_t s1;    // coarse bin = target >> s1
     uint32_t nb1;   // coarse bins

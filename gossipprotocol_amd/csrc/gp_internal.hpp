@@ -14,6 +14,22 @@ namespace gp {
 constexpr int HIST = 4096;            // per-round alert ring (host syncs at least every HIST rounds)
 constexpr uint32_t INJ_CHUNK = 65536; // injector live-list chunk (ids); 2048 bitmap words
 constexpr int BULK_THREADS = 256;
+
+// The immediate of `s_waitcnt vmcnt(n)` with the other counters left alone (gfx9 encoding:
+// vmcnt bits 3:0 and 15:14, expcnt 6:4 = 7, lgkmcnt 11:8 = 15), for __builtin_amdgcn_s_waitcnt.
+// vmcnt retires in issue order, so an explicit count can wait for an older operation without
+// waiting for the n newest; the compiler takes such a wait into its own accounting.
+constexpr int vmcnt_enc(int n) { return 0x0F70 | (n & 15) | ((n >> 4) << 14); }
+
+// A load of data the running kernel does not write (in-lists, the walk's tile list, counts an
+// earlier kernel produced) through the constant address space: at a wave-uniform address it
+// becomes a scalar load, counted by lgkmcnt, so waiting for it does not also wait for the
+// wave's earlier vector stores (vmcnt retires in issue order).  The scalar cache is invalidated
+// at every kernel start.
+template <typename T>
+__device__ __forceinline__ T ld_const(const T* p) {
+    return *(const __attribute__((address_space(4))) T*)(p);
+}
 constexpr int FIN_THREADS = 1024;
 constexpr int RREG_MAX = 8;           // round kernel launches per round, at most (DevState::rregions)
 

@@ -143,8 +143,6 @@ __device__ __forceinline__ void dma_copy(void* lds, const char* g16, uint32_t nb
 }
 // cache-policy bits of a single-use (streamed once per round) staging copy: nt
 constexpr int DMA_ONCE = 2;
-// s_waitcnt vmcnt(0) with the other counters left alone (gfx9 encoding: expcnt 7, lgkmcnt 15)
-constexpr int VMCNT0 = 0x0F70;
 
 // Node bytes nb[lo, hi) clamped to [ext_lo,
 // ext_hi); returns the node id of LDS byte 0 (up to 15 bytes below lo).  Reads
@@ -250,7 +248,7 @@ struct TileWalk {
     // tile (relative to lo / TILE) of walk item t; false: empty item (block-uniform)
     __device__ __forceinline__ bool tile(uint32_t& rel) const {
         if (mode == 3) {
-            rel = wl[t];
+            rel = ld_const(wl + t);
             return true;
         }
         if (mode != 2) {
@@ -358,7 +356,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
         if (blockIdx.x == 0 && threadIdx.x < 8) a.tq_next[threadIdx.x * TQ_STRIDE] = 0u;  // next round's counters
         if (threadIdx.x == 0) L.qn[0] = atomicAdd(tw.qc, 1u);
         __syncthreads();
-        tw.t = L.qn[0];
+        tw.t = __builtin_amdgcn_readfirstlane(L.qn[0]);
         ++it;
     }
     // walk 3: once this XCD's list is exhausted, the block takes items from the other
@@ -375,7 +373,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
             if (dyn) {
                 if (threadIdx.x == 0) L.qn[it & 1] = claim;
                 __syncthreads();
-                tw.t = L.qn[it & 1];
+                tw.t = __builtin_amdgcn_readfirstlane(L.qn[it & 1]);
                 ++it;
             } else {
                 tw.t += tw.step;
@@ -394,8 +392,8 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                 e_lo = pf_lo;
                 e_hi = pf_hi;
             } else {
-                e_lo = a.in_off[j0];
-                e_hi = a.in_off[j1];
+                e_lo = ld_const(a.in_off + j0);
+                e_hi = ld_const(a.in_off + j1);
             }
         }
         const uint32_t cnt = e_hi - e_lo;
@@ -407,8 +405,8 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
             pf_tile = 0xFFFFFFFFu;
             if (nw.t < nw.end && nw.tile(nti)) {
                 const uint32_t nT = (a.lo / TILE + nti) * TILE;
-                pf_lo = a.in_off[max(a.lo, nT)];
-                pf_hi = a.in_off[min(a.lo + a.nloc, nT + TILE)];
+                pf_lo = ld_const(a.in_off + max(a.lo, nT));
+                pf_hi = ld_const(a.in_off + min(a.lo + a.nloc, nT + TILE));
                 pf_tile = nti;
             }
         }
@@ -606,7 +604,10 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
         }
         uint32_t t_next = tw.t + tw.step;
         if (dyn) {
-            t_next = L.qn[it & 1];
+            // (block-uniform, and known to be: the next tile's in-list range is then two scalar
+            // loads, not vector loads whose wait at the next tile's start also waited for this
+            // tile's state stores)
+            t_next = __builtin_amdgcn_readfirstlane(L.qn[it & 1]);
             ++it;
             // the next tile's in-edge range (two uniform loads, consumed next tile)
             if (TOPO == IMP3D) {
@@ -616,8 +617,8 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                 pf_tile = 0xFFFFFFFFu;
                 if (nw.t < nw.end && nw.tile(nti)) {
                     const uint32_t nT = (a.lo / TILE + nti) * TILE;
-                    pf_lo = a.in_off[max(a.lo, nT)];
-                    pf_hi = a.in_off[min(a.lo + a.nloc, nT + TILE)];
+                    pf_lo = ld_const(a.in_off + max(a.lo, nT));
+                    pf_hi = ld_const(a.in_off + min(a.lo + a.nloc, nT + TILE));
                     pf_tile = nti;
                 }
             }
@@ -756,7 +757,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                     // only memory operation the next slot's loads could wait for, and they do not
                     // (without it the compiler waited vmcnt(0) before every slot's gathers -- a lane
                     // range with no valid node skips the fold that consumes the loads)
-                    __builtin_amdgcn_s_waitcnt(VMCNT0);
+                    __builtin_amdgcn_s_waitcnt(vmcnt_enc(0));
                     if (valid) {
                         const uint32_t b = gst[h] & 0xFFu, mask = (gst[h] >> 8) & 63u, from = (gst[h] >> 14) & 63u;
                         const uint32_t deg = popc6(mask) + (TOPO == IMP3D ? 1u : 0u);
@@ -918,7 +919,7 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
         tw.end = a.wo[c + 1] - a.wo[c];
         if (threadIdx.x == 0) L.qn[it & 1] = atomicAdd(tw.qc, 1u);
         __syncthreads();
-        tw.t = L.qn[it & 1];
+        tw.t = __builtin_amdgcn_readfirstlane(L.qn[it & 1]);
         ++it;
     }
 }
@@ -1013,8 +1014,8 @@ __global__ __launch_bounds__(TPB, GP_MINB) void k_gossip_tile(RoundArgs a, uint3
         const uint32_t j1 = min(a.lo + a.nloc, T + TILE);
         uint32_t e_lo = 0, e_hi = 0;
         if (TOPO == IMP3D) {
-            e_lo = a.in_off[j0];
-            e_hi = a.in_off[j1];
+            e_lo = ld_const(a.in_off + j0);
+            e_hi = ld_const(a.in_off + j1);
         }
         int32_t c0[NPT];
 #pragma unroll
