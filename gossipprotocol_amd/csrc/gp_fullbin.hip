@@ -460,8 +460,8 @@ struct MultiOutLds {
             return;
         }
         const size_t o = (size_t)c * cap[b] + pos;
-        hdr[b][o] = h;
-        pay[b][o] = v;
+        *gptr(hdr[b] + o) = h;
+        st_global(pay[b] + o, v);
     }
 };
 
@@ -505,7 +505,7 @@ __global__ __launch_bounds__(FBR_THREADS, 1) void k_fbm_send(FullBinArgs a, uint
     __syncthreads();
     for (uint32_t q = threadIdx.x; q < nk; q += FBR_THREADS) {
         const uint32_t n = base[q], b = O.keyb[q];
-        base[q] = n ? atomicAdd(O.cnt[b] + (q - O.kb[b]), n) : 0u;
+        base[q] = n ? __hip_atomic_fetch_add(gptr(O.cnt[b] + (q - O.kb[b])), n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
     }
     // sweep 2: into the bins' runs
     for (uint64_t c0 = i0; c0 < i1; c0 += FBR_CHUNK) {
@@ -788,7 +788,7 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
                 if (n) {
                     if constexpr (RANKS) {
                         const uint32_t b = O[0].keyb[q0];
-                        res = atomicAdd(O[0].cnt[b] + (q0 - O[0].kb[b]), n);
+                        res = __hip_atomic_fetch_add(gptr(O[0].cnt[b] + (q0 - O[0].kb[b])), n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     } else {
                         res = atomicAdd(&a.cnt1[q0], n);
                     }

@@ -30,6 +30,22 @@ template <typename T>
 __device__ __forceinline__ T ld_const(const T* p) {
     return *(const __attribute__((address_space(4))) T*)(p);
 }
+
+// A pointer known to address global memory.  Pointers a kernel reads from LDS or from a
+// per-lane-indexed table are generic to the compiler, which then emits flat instructions:
+// those count in lgkmcnt as well as vmcnt, so every later LDS wait also waited for them.
+template <typename T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* gptr(T* p) {
+    return (__attribute__((address_space(1))) T*)(p);
+}
+typedef double gp_d2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void st_global(double2* p, double2 v) {
+    *gptr(reinterpret_cast<gp_d2v*>(p)) = gp_d2v{v.x, v.y};
+}
+__device__ __forceinline__ double2 ld_global(const double2* p) {
+    const gp_d2v t = *gptr(reinterpret_cast<gp_d2v*>(const_cast<double2*>(p)));
+    return make_double2(t.x, t.y);
+}
 constexpr int FIN_THREADS = 1024;
 constexpr int RREG_MAX = 8;           // round kernel launches per round, at most (DevState::rregions)
 

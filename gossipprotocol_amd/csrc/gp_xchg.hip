@@ -340,7 +340,10 @@ __global__ __launch_bounds__(LP_THREADS) void k_list_pack(ListPackArgs a) {
     const uint32_t tb = a.t0 + blockIdx.x * LP_TILES;
     if (tb >= a.t1) return;
     const int ntl = (int)min((uint32_t)LP_TILES, a.t1 - tb);
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63u;
+    // the wave's index, known uniform: its tiles' buffer resources are then scalar (a per-lane
+    // resource made every buffer load a waterfall loop)
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t me = (uint32_t)a.me;
     const int W = a.W;
     for (uint32_t q = threadIdx.x; q < LP_TILES * 2 * LIST_LW; q += LP_THREADS) (&mk[0][0])[q] = 0u;
@@ -464,7 +467,7 @@ __global__ __launch_bounds__(LP_THREADS) void k_list_pack(ListPackArgs a) {
                 const uint32_t w = lw[tt][d] + (rho >> 6), bit = rho & 63u;
                 const unsigned long long m = ((unsigned long long)mk[tt][2 * w + 1] << 32) | mk[tt][2 * w];
                 const uint32_t idx = off[d] + tn[tt][d] + wb[tt][w] + (uint32_t)__popcll(m & ((1ull << bit) - 1ull));
-                if (idx < ocap[d]) ovals[d][idx] = v[h];
+                if (idx < ocap[d]) st_global(ovals[d] + idx, v[h]);
                 else atomicOr(a.overflow, 1u);
             }
         }
@@ -500,9 +503,9 @@ __global__ __launch_bounds__(256) void k_halo(HaloArgs a) {
         if (rank >= a.cap) {
             if (PACK) atomicOr(a.overflow, 1u);
         } else if (PACK) {
-            *slot = a.sw[i];
+            st_global(slot, ld_global(a.sw + i));
         } else {
-            a.sw[i] = *slot;
+            st_global(a.sw + i, ld_global(slot));
         }
     }
 }
