@@ -158,8 +158,8 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
             if (d[h] == none) continue;
             const uint32_t k = d[h];
             if (idx[h] < cap[k]) {
-                oslots[k][idx[h]] = a.counts ? ent[h] - bnd[k] : ent[h];
-                if (a.push) ovals[k][idx[h]] = v[h];
+                *gptr(oslots[k] + idx[h]) = a.counts ? ent[h] - bnd[k] : ent[h];
+                if (a.push) st_global(ovals[k] + idx[h], v[h]);
             } else {
                 atomicOr(a.overflow, 1u);
             }
