@@ -736,6 +736,17 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                     const uint32_t jl = k * TPB + threadIdx.x;
                     const uint32_t j = T + jl;
                     const bool valid = j >= j0 && j < j1;
+                    // Imp3D, staged tile: the node's window of the used-in-edge bitmap and its first
+                    // used in-edge's message, read from LDS while the slot's loads are in flight (the
+                    // fold needed both after the loads, one LDS round trip after the other).  A node's
+                    // in-edges fit one 32-bit window (in-degree <= 14 outside `wide` tiles).
+                    uint32_t pwin = 0u, pqb = 0u;
+                    if (TOPO == IMP3D && staged && !wide) {
+                        const uint32_t* bw = reinterpret_cast<const uint32_t*>(L.bits);
+                        pqb = epre[h];
+                        const uint32_t nd = gst[h] >> 20;
+                        pwin = __builtin_amdgcn_alignbit(bw[(pqb >> 5) + 1], bw[pqb >> 5], pqb & 31u) & ((1u << nd) - 1u);
+                    }
                     // j + 1 / j - 1: the neighbour lane's own (s, w) by DPP (all lanes active
                     // here), across the wave's ends from the values staged in L.zb; a load
                     // only where that lane's node is outside the tile's valid range
@@ -794,7 +805,17 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                                 e_b = a.in_off[j];
                                 e_e = a.in_off[j + 1];
                             }
-                            if (staged) {
+                            if (staged && !wide) {
+                                // the window and first message read above; the rest set bit by set
+                                // bit (ascending sender = canonical order), edge q's message at slot q
+                                uint32_t win = pwin;
+                                while (win) {
+                                    const uint32_t q = pqb + (uint32_t)__builtin_ctz(win);
+                                    win &= win - 1u;
+                                    fold(L.msg[q]);
+                                    recv = true;
+                                }
+                            } else if (staged) {
                                 // the node's used in-edges: its window of the tile bitmap, 32 bits
                                 // at a time (funnel shift of two LDS words), walked set bit by set
                                 // bit (ascending sender = canonical order); edge q's message is at
