@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 end state (after the wait / flat-store changes), part A: smoke and the whole GPU suite.
 export TMPDIR=/tmp
-O=${O:-gpurun_out/r6_final2}
+O=${O:-gpurun_out/r6_final3}
 mkdir -p $O
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log

@@ -3,7 +3,7 @@
 # convergence.
 set -o pipefail
 export TMPDIR=/tmp
-O=${O:-gpurun_out/r6_final2}
+O=${O:-gpurun_out/r6_final3}
 mkdir -p $O
 timeout -k 10 600 python -u bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
 cat $O/bench.json
