@@ -671,7 +671,6 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
                 const uint32_t p = cnt[vr[k]] + rk[k];
                 src[p] = snd[k];
                 msg[p] = make_double2(ps[k], pw[k]);
-                idx[p] = (uint16_t)p;
             }
         }
         lds_barrier();
@@ -708,15 +707,15 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
         auto sort_receiver = [&](uint32_t p0, uint32_t p1) {
             for (uint32_t p = p0 + 1; p < p1; ++p) {
                 const uint32_t s = src[p];
-                const uint16_t xi = idx[p];
+                const double2 mv = msg[p];
                 uint32_t q = p;
                 while (q > p0 && src[q - 1] > s) {
                     src[q] = src[q - 1];
-                    idx[q] = idx[q - 1];
+                    msg[q] = msg[q - 1];
                     --q;
                 }
                 src[q] = s;
-                idx[q] = xi;
+                msg[q] = mv;
             }
         };
         // FG receivers folded in lock step (one LDS chain each in flight, each receiver's own
@@ -744,16 +743,15 @@ __global__ __launch_bounds__(FBF_THREADS) void k_fb_fold(FullBinArgs a, uint32_t
                 fw[i] = active && P > 1 ? svk[k].y * 0.5 : svk[k].y;
             }
             for (uint32_t t = 0; t < most; ++t) {
-                uint16_t xi[FG];
+                double2 m[FG];
 #pragma unroll
-                for (int i = 0; i < FG; ++i) xi[i] = idx[min(fp0[i] + t, (uint32_t)FB_CAP2 - 1u)];
+                for (int i = 0; i < FG; ++i) m[i] = msg[min(fp0[i] + t, (uint32_t)FB_CAP2 - 1u)];
 #pragma unroll
-                for (int i = 0; i < FG; ++i)
-                    if (fp0[i] + t < fp1[i]) {
-                        const double2 m = msg[xi[i]];  // already halved by the sender
-                        fs[i] = fs[i] + m.x;
-                        fw[i] = fw[i] + m.y;
-                    }
+                for (int i = 0; i < FG; ++i) {
+                    const bool ok = fp0[i] + t < fp1[i];
+                    fs[i] = fs[i] + (ok ? m[i].x : 0.0);  // already halved by the sender
+                    fw[i] = fw[i] + (ok ? m[i].y : 0.0);
+                }
             }
 #pragma unroll
             for (int i = 0; i < FG; ++i) close_receiver(g0 + i, fp0[i], fp1[i], fs[i], fw[i]);
