@@ -7,6 +7,6 @@ c2() {
   echo "c2 $l: $(grep -o '[0-9.]* ms/round kernel' $O/c2_$l.log | head -1) $(grep -o 'no events: wall [0-9.]* ms/round' $O/c2_$l.log | head -1)"
 }
 for i in 1 2 3; do
-  c2 nb$i GOSSIP_HIP_LIB_EXPERIMENT=build/ablate/lib_c2nb.so || exit 1
+  c2 pf$i GOSSIP_HIP_LIB_EXPERIMENT=build/ablate/lib_c2pf.so || exit 1
   c2 sel$i GOSSIP_HIP_LIB_EXPERIMENT=build/ablate/lib_c2sel.so || exit 1
 done
