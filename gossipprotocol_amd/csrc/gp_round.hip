@@ -427,6 +427,18 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                         raw[m] = q < cnt ? __builtin_nontemporal_load(srcp + e_lo + q) : 0u;
                     }
                 }
+                // REMOTE: the list keys of the tile's in-edges (meaningful for remote senders),
+                // issued with the senders so their latency hides behind the draws (round 5 loaded
+                // them after the draws: live across the Philox batch they spilled then; at 96 VGPRs
+                // now without spills, C5 W = 8 REMOTE kernel -1.5 %, profiles/r06/remote/)
+                uint32_t rkv[REMOTE ? FU : 1];
+                if constexpr (REMOTE) {
+#pragma unroll
+                    for (int m = 0; m < FU; ++m) {
+                        const uint32_t q = threadIdx.x + m * TPB;
+                        rkv[m] = q < cnt ? __builtin_nontemporal_load(a.rk + e_lo + q) : 0u;
+                    }
+                }
                 uint32_t isrc[FU];
                 bool sent[FU], pick[FU];
 #pragma unroll
@@ -502,14 +514,6 @@ __device__ __forceinline__ void ps_tiles(const RoundArgs& a, uint32_t r, TileLds
                 // so no load waits under a branch.
                 uint32_t ridx[REMOTE ? FU : 1];
                 if constexpr (REMOTE) {
-                    // the list keys of the tile's in-edges (meaningful for remote senders), after
-                    // the draws: live across the Philox batch they cost spills
-                    uint32_t rkv[FU];
-#pragma unroll
-                    for (int m = 0; m < FU; ++m) {
-                        const uint32_t q = threadIdx.x + m * TPB;
-                        rkv[m] = q < cnt ? __builtin_nontemporal_load(a.rk + e_lo + q) : 0u;
-                    }
                     uint2 hm[FU];
                     uint32_t hb[FU];
 #pragma unroll
